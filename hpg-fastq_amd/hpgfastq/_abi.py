@@ -1,0 +1,160 @@
+"""ctypes declarations mirroring include/hpgq.h (no torch types cross it)."""
+import ctypes as C
+import os
+import sys
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "libhpgq.so")
+
+NO_VALUE, MIN_VALUE, MAX_VALUE = -1, 0, 100000
+LMAX_LIMIT = 1024
+NUM_SCALARS = 8
+(S_NUM_INPUT, S_NUM_PASSED, S_NUM_FAILED, S_NUM_EDITED,
+ S_NUM_STATS, S_ACC_MEANQ_FX16, S_LONG_READS) = range(7)
+MEANQ_BINS, GC_BINS = 256, 101
+CGR_ALL_READS, CGR_ONLY_VALID_READS = 0, 1
+
+ERRORS = {0: "ok", -1: "invalid argument", -2: "HIP runtime error", -3: "out of memory",
+          -4: "read longer than lmax", -5: "no HIP device", -6: "RCCL error",
+          -7: "invalid ctx state"}
+
+
+class HpgqError(RuntimeError):
+    def __init__(self, code, where=""):
+        self.code = code
+        super().__init__(f"hpgq error {code} ({ERRORS.get(code, '?')}) in {where}")
+
+
+def check(rc, where=""):
+    if rc != 0:
+        raise HpgqError(rc, where)
+    return rc
+
+
+_PARAM_FIELDS = [
+    "phred", "lmax", "stats_on", "filter_on", "edit_on", "paired",
+    "min_read_length", "max_read_length", "min_read_quality", "max_read_quality",
+    "max_out_of_quality", "left_length", "min_left_quality", "max_left_quality",
+    "right_length", "min_right_quality", "max_right_quality", "max_N",
+    "edit_left_length", "edit_min_left_quality", "edit_max_left_quality",
+    "edit_right_length", "edit_min_right_quality", "edit_max_right_quality",
+]
+
+
+class Params(C.Structure):
+    _fields_ = [(f, C.c_int32) for f in _PARAM_FIELDS]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f in _PARAM_FIELDS}
+
+
+class Batch(C.Structure):
+    _fields_ = [("num_reads", C.c_int64), ("seq", C.c_void_p), ("quality", C.c_void_p),
+                ("data_indices", C.c_void_p)]
+
+
+class Synth(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("read_length", C.c_int32), ("trunc_pct", C.c_int32),
+                ("bad_pct", C.c_int32), ("n_per_1024", C.c_int32), ("phred", C.c_int32),
+                ("mate", C.c_int32)]
+
+
+class Summary(C.Structure):
+    _fields_ = [("num_reads", C.c_uint64), ("num_passed", C.c_uint64),
+                ("num_failed", C.c_uint64), ("num_edited", C.c_uint64),
+                ("num_input", C.c_uint64), ("min_length", C.c_int32),
+                ("max_length", C.c_int32), ("acc_length", C.c_uint64),
+                ("mean_length", C.c_double), ("mean_quality_raw", C.c_double),
+                ("num_A", C.c_uint64), ("num_C", C.c_uint64), ("num_G", C.c_uint64),
+                ("num_T", C.c_uint64), ("num_N", C.c_uint64)]
+
+
+def counters_len(lmax):
+    return NUM_SCALARS + (lmax + 1) + MEANQ_BINS + GC_BINS + 6 * lmax
+
+
+def layout(lmax):
+    o = {"hist_len": NUM_SCALARS}
+    o["hist_meanq"] = o["hist_len"] + lmax + 1
+    o["hist_gc"] = o["hist_meanq"] + MEANQ_BINS
+    o["pos_qsum"] = o["hist_gc"] + GC_BINS
+    for i, b in enumerate("ACGTN"):
+        o["pos_" + b] = o["pos_qsum"] + lmax * (1 + i)
+    o["len"] = counters_len(lmax)
+    return o
+
+
+# (name, restype, argtypes) — every symbol include/hpgq.h exports
+_SIGS = [
+    ("hpgq_params_init", None, [C.POINTER(Params)]),
+    ("hpgq_counters_summary", C.c_int, [C.c_void_p, C.c_int, C.POINTER(Summary)]),
+    ("hpgq_open", C.c_int, [C.POINTER(C.c_void_p), C.c_int, C.POINTER(Params)]),
+    ("hpgq_close", None, [C.c_void_p]),
+    ("hpgq_run_device", C.c_int, [C.c_void_p, C.POINTER(Batch), C.POINTER(Batch),
+                                  C.c_void_p, C.c_void_p]),
+    ("hpgq_run_host", C.c_int, [C.c_void_p, C.POINTER(Batch), C.POINTER(Batch),
+                                C.c_void_p, C.c_void_p]),
+    ("hpgq_sync", C.c_int, [C.c_void_p]),
+    ("hpgq_reset", C.c_int, [C.c_void_p]),
+    ("hpgq_counters_size", C.c_size_t, [C.c_void_p]),
+    ("hpgq_read_counters", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
+    ("hpgq_counters_device", C.c_void_p, [C.c_void_p]),
+    ("hpgq_stream", C.c_void_p, [C.c_void_p]),
+    ("hpgq_comm_unique_id", C.c_int, [C.c_char_p]),
+    ("hpgq_comm_init", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_char_p]),
+    ("hpgq_allreduce", C.c_int, [C.c_void_p]),
+    ("hpgq_cgr_open", C.c_int, [C.POINTER(C.c_void_p), C.c_int, C.c_int, C.c_int]),
+    ("hpgq_cgr_close", None, [C.c_void_p]),
+    ("hpgq_cgr_fill_device", C.c_int, [C.c_void_p, C.POINTER(Batch), C.c_void_p, C.c_int]),
+    ("hpgq_cgr_sync", C.c_int, [C.c_void_p]),
+    ("hpgq_cgr_reset", C.c_int, [C.c_void_p]),
+    ("hpgq_cgr_read", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    ("hpgq_cgr_stream", C.c_void_p, [C.c_void_p]),
+    ("hpgq_cgr_last_replays", C.c_int64, [C.c_void_p]),
+    ("hpgq_synth_length", C.c_int32, [C.POINTER(Synth), C.c_int64]),
+    ("hpgq_synth_indices_host", C.c_int, [C.POINTER(Synth), C.c_int64, C.c_int64, C.c_void_p]),
+    ("hpgq_synth_device", C.c_int, [C.POINTER(Synth), C.c_int64, C.c_int64, C.c_void_p,
+                                    C.c_void_p, C.c_void_p, C.c_void_p]),
+    ("hpgq_device_count", C.c_int, []),
+    ("hpgq_strerror", C.c_char_p, [C.c_int]),
+    ("hpgq_version", C.c_char_p, []),
+]
+
+
+def exported_symbols():
+    return [s[0] for s in _SIGS]
+
+
+def _load():
+    # PyTorch-ROCm bundles its own libamdhip64/libhsa-runtime64 (same SONAMEs as
+    # /opt/rocm's).  If libhpgq loads first, a later `import torch` maps a second
+    # HIP/HSA runtime into the process and one of them cannot open the device.
+    # Importing torch first makes libhpgq bind to the already-loaded runtime by
+    # SONAME, so a process that uses both (bench, tests) has exactly one.
+    if "torch" not in sys.modules:
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} not built: run `make -C hpg-fastq_amd` "
+                          "(the HIP engine has no CPU fallback)")
+    lib = C.CDLL(LIB_PATH)
+    for name, res, args in _SIGS:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def params_default(**kw):
+    p = Params()
+    lib.hpgq_params_init(C.byref(p))
+    for k, v in kw.items():
+        if not hasattr(p, k):
+            raise KeyError(k)
+        setattr(p, k, int(v))
+    return p

@@ -1,0 +1,163 @@
+"""Engine / ChaosGame: Python handles over libhpgq contexts.
+
+Host arrays are numpy; device buffers are passed as raw pointers (ints), so a
+caller may own HBM through torch, hipMalloc or anything else.  Mirrors the
+reference's worker-stage call shape: one call per batch, counters merged on
+the device until read back (src/stats_fastq.c:202-253).
+"""
+import ctypes as C
+
+import numpy as np
+
+from ._abi import (lib, check, Params, Batch, Summary, counters_len, CGR_ALL_READS)
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def host_batch(seq, qual, idx):
+    """hpgq_batch_t over host numpy arrays (uint8, uint8, int32 of n+1)."""
+    assert seq.dtype == np.uint8 and qual.dtype == np.uint8 and idx.dtype == np.int32
+    assert seq.flags.c_contiguous and qual.flags.c_contiguous and idx.flags.c_contiguous
+    return Batch(len(idx) - 1, seq.ctypes.data, qual.ctypes.data, idx.ctypes.data)
+
+
+def device_batch(num_reads, seq_ptr, qual_ptr, idx_ptr):
+    return Batch(int(num_reads), int(seq_ptr), int(qual_ptr), int(idx_ptr))
+
+
+class Engine:
+    """One hpgq_ctx: a HIP stream + device counters on `device`."""
+
+    def __init__(self, params, device=0):
+        if not isinstance(params, Params):
+            raise TypeError("params must be hpgfastq.Params")
+        self.params = params
+        self.lmax = params.lmax
+        self.nsets = 2 if params.paired else 1
+        h = C.c_void_p()
+        check(lib.hpgq_open(C.byref(h), device, C.byref(params)), "hpgq_open")
+        self._h = h
+
+    def close(self):
+        if self._h:
+            lib.hpgq_close(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def stream(self):
+        return lib.hpgq_stream(self._h)
+
+    def run_host(self, batch, batch2=None, mask=None, trim=None):
+        """Host numpy batch; mask/trim are numpy outputs valid after sync()."""
+        check(lib.hpgq_run_host(self._h, C.byref(batch), C.byref(batch2) if batch2 else None,
+                                _ptr(mask), _ptr(trim)), "hpgq_run_host")
+
+    def run_device(self, batch, batch2=None, mask_ptr=None, trim_ptr=None):
+        check(lib.hpgq_run_device(self._h, C.byref(batch), C.byref(batch2) if batch2 else None,
+                                  mask_ptr, trim_ptr), "hpgq_run_device")
+
+    def sync(self):
+        check(lib.hpgq_sync(self._h), "hpgq_sync")
+
+    def reset(self):
+        check(lib.hpgq_reset(self._h), "hpgq_reset")
+
+    def counters(self):
+        n = lib.hpgq_counters_size(self._h)
+        out = np.zeros(n, dtype=np.uint64)
+        check(lib.hpgq_read_counters(self._h, _ptr(out), n), "hpgq_read_counters")
+        return out
+
+    def counters_device_ptr(self):
+        return lib.hpgq_counters_device(self._h)
+
+    def comm_init(self, nranks, rank, uid):
+        check(lib.hpgq_comm_init(self._h, nranks, rank, uid), "hpgq_comm_init")
+
+    def allreduce(self):
+        check(lib.hpgq_allreduce(self._h), "hpgq_allreduce")
+
+    def process(self, seq, qual, idx, seq2=None, qual2=None, idx2=None):
+        """Convenience: one host batch -> (mask, trim); counters accumulate."""
+        n = len(idx) - 1
+        b = host_batch(seq, qual, idx)
+        b2 = host_batch(seq2, qual2, idx2) if self.params.paired else None
+        mask = np.zeros(n, dtype=np.uint8)
+        trim = np.zeros(n * self.nsets, dtype=np.uint32)
+        self.run_host(b, b2, mask, trim)
+        self.sync()
+        return mask, trim
+
+
+def comm_unique_id():
+    buf = C.create_string_buffer(128)
+    check(lib.hpgq_comm_unique_id(buf), "hpgq_comm_unique_id")
+    return buf.raw
+
+
+def summary(counter_set, lmax):
+    s = Summary()
+    arr = np.ascontiguousarray(counter_set[:counters_len(lmax)], dtype=np.uint64)
+    check(lib.hpgq_counters_summary(_ptr(arr), lmax, C.byref(s)), "hpgq_counters_summary")
+    return {f: getattr(s, f) for f, _ in Summary._fields_}
+
+
+class ChaosGame:
+    """hpgq_cgr: chaos_game_fill_tables on the device (old/chaos_game.c:165)."""
+
+    def __init__(self, k, base_quality=33, device=0):
+        self.k = k
+        self.dim = 1 << k
+        h = C.c_void_p()
+        check(lib.hpgq_cgr_open(C.byref(h), device, k, base_quality), "hpgq_cgr_open")
+        self._h = h
+
+    def close(self):
+        if self._h:
+            lib.hpgq_cgr_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def stream(self):
+        return lib.hpgq_cgr_stream(self._h)
+
+    def fill_device(self, batch, status_ptr=None, mode=CGR_ALL_READS):
+        check(lib.hpgq_cgr_fill_device(self._h, C.byref(batch), status_ptr, mode),
+              "hpgq_cgr_fill_device")
+
+    def sync(self):
+        check(lib.hpgq_cgr_sync(self._h), "hpgq_cgr_sync")
+
+    def reset(self):
+        check(lib.hpgq_cgr_reset(self._h), "hpgq_cgr_reset")
+
+    def last_replays(self):
+        return int(lib.hpgq_cgr_last_replays(self._h))
+
+    def tables(self):
+        cells = self.dim * self.dim
+        ts = np.zeros(cells, dtype=np.uint32)
+        tq = np.zeros(cells, dtype=np.uint32)
+        wc = np.zeros(1, dtype=np.uint32)
+        check(lib.hpgq_cgr_read(self._h, _ptr(ts), _ptr(tq), _ptr(wc)), "hpgq_cgr_read")
+        return ts.reshape(self.dim, self.dim), tq.reshape(self.dim, self.dim), int(wc[0])

@@ -1,0 +1,304 @@
+/*
+ * hpgq.h — C-ABI of the MI355X FASTQ QC engine (libhpgq.so).
+ *
+ * This is the drop-in boundary for the per-read hot path of hpg-fastq
+ * (SURVEY.md §8b).  Every entry point replaces one bioinfo-libs call made by
+ * the reference's workflow workers, or the serial consumer merge that follows
+ * them:
+ *
+ *   fastq_filter(reads, passed, failed, opts)     src/stats_fastq.c:224,
+ *                                                 src/filter_fastq.c:148,
+ *                                                 src/edit_fastq.c:166
+ *   fastq_reads_stats(reads, rs_opts, fq_stats)   src/stats_fastq.c:230,244
+ *   fastq_stats_consumer per-read + per-base merge src/stats_fastq.c:257-417
+ *   fastq_edit(reads, opts)                       src/edit_fastq.c:154
+ *   chaos_game_fill_tables(cg_data, batch, mode)  old/chaos_game.c:165-267
+ *
+ * The batch layout mirrors the SoA `fastq_batch_t` the old GPU path used
+ * (fields evidenced at old/chaos_game.c:174-193): concatenated `seq` and
+ * `quality` byte buffers plus `data_indices` with read i occupying
+ * [data_indices[i], data_indices[i+1]).
+ *
+ * All functions return 0 on success or a negative HPGQ_E* code; no function
+ * exits the process (the reference calls exit()/LOG_FATAL instead).
+ * Plain pointers and sizes only — no C++ or framework types cross this line.
+ */
+#ifndef HPGQ_H
+#define HPGQ_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------------- */
+/* constants                                                              */
+/* ---------------------------------------------------------------------- */
+
+/* src/commons_fastq.h:21-23 */
+#define HPGQ_NO_VALUE   (-1)
+#define HPGQ_MIN_VALUE  0
+#define HPGQ_MAX_VALUE  100000
+
+/* quality encodings (stats/edit --quality-encoding, src/stats_options.c:124-137) */
+#define HPGQ_PHRED33 33
+#define HPGQ_PHRED64 64
+
+/* longest read the per-position counters can hold (dense arrays) */
+#define HPGQ_LMAX_LIMIT 1024
+
+/* error codes */
+#define HPGQ_OK                  0
+#define HPGQ_E_INVALID         (-1)   /* bad argument / parameter            */
+#define HPGQ_E_HIP             (-2)   /* HIP runtime error                    */
+#define HPGQ_E_NOMEM           (-3)   /* device or host allocation failed     */
+#define HPGQ_E_READ_TOO_LONG   (-4)   /* a read longer than params.lmax seen  */
+#define HPGQ_E_NO_DEVICE       (-5)   /* no HIP device                        */
+#define HPGQ_E_RCCL            (-6)   /* RCCL communicator / collective error */
+#define HPGQ_E_STATE           (-7)   /* call not valid in this ctx state     */
+
+/* ---------------------------------------------------------------------- */
+/* batch                                                                  */
+/* ---------------------------------------------------------------------- */
+
+/*
+ * SoA read batch (fastq_batch_t, old/chaos_game.c:176-193).  Read i is
+ * seq[data_indices[i] .. data_indices[i+1]) and the same range of quality.
+ * data_indices has num_reads+1 entries, is non-decreasing and is `int` like
+ * the reference's, so one batch holds < 2 GiB of bases.  Offsets are
+ * absolute into seq/quality (data_indices[0] need not be 0).
+ */
+typedef struct hpgq_batch {
+  int64_t        num_reads;
+  const char    *seq;
+  const char    *quality;
+  const int32_t *data_indices;
+} hpgq_batch_t;
+
+/* ---------------------------------------------------------------------- */
+/* parameters                                                             */
+/* ---------------------------------------------------------------------- */
+
+/*
+ * Engine parameters.  Filter fields follow fastq_filter_options_new's
+ * argument order (src/filter_fastq.c:140-145); edit fields follow
+ * fastq_edit_options_new (src/edit_fastq.c:148-151).  Values are already
+ * defaulted the way the reference drivers do it (NO_VALUE -> MIN/MAX_VALUE,
+ * src/filter_fastq.c:195-206); hpgq_params_init() gives those defaults.
+ * Quality thresholds are Phred scores; the engine compares them with
+ * (quality_char - phred).
+ */
+typedef struct hpgq_params {
+  int32_t phred;              /* 33 or 64                                    */
+  int32_t lmax;               /* per-position array length, 1..HPGQ_LMAX_LIMIT */
+
+  int32_t stats_on;           /* accumulate stats counters                   */
+  int32_t filter_on;          /* apply the filter (else every read passes)   */
+  int32_t edit_on;            /* 5'/3' trim before filter and stats          */
+  int32_t paired;             /* batches are mate pairs; pair passes iff both */
+
+  /* fastq_filter_options_new(...) */
+  int32_t min_read_length, max_read_length;
+  int32_t min_read_quality, max_read_quality;
+  int32_t max_out_of_quality;
+  int32_t left_length, min_left_quality, max_left_quality;
+  int32_t right_length, min_right_quality, max_right_quality;
+  int32_t max_N;
+
+  /* fastq_edit_options_new(left_len, minL, maxL, right_len, minR, maxR, 0,0,0) */
+  int32_t edit_left_length, edit_min_left_quality, edit_max_left_quality;
+  int32_t edit_right_length, edit_min_right_quality, edit_max_right_quality;
+} hpgq_params_t;
+
+/* Defaults: phred33, lmax 256, stats on, filter/edit off, ranges open. */
+void hpgq_params_init(hpgq_params_t *p);
+
+/* ---------------------------------------------------------------------- */
+/* packed counters (what the stats consumer merges; RCCL all-reduces)     */
+/* ---------------------------------------------------------------------- */
+
+/*
+ * One counter set is a flat uint64_t array.  Offsets depend on lmax:
+ *
+ *   [0 .. 8)                 scalars, HPGQ_S_*
+ *   hist_len   [lmax+1]      reads per length               (kh_length_histogram)
+ *   hist_meanq [256]         reads per round(mean raw Q)     (kh_quality_histogram)
+ *   hist_gc    [101]         reads per 100*(G+C)/len         (kh_gc_histogram)
+ *   pos_qsum   [lmax]        sum of raw quality per position (kh_acc_quality_per_nt)
+ *   pos_base   [5][lmax]     A, C, G, T, N per position      (kh_num_*_per_nt)
+ *
+ * kh_count_quality_per_nt[j] = sum_{L>j} hist_len[L] and the scalar totals of
+ * stats_counters_t (src/stats_fastq.h:35-73) are derived from these by
+ * hpgq_counters_summary().  A paired ctx holds two sets back to back
+ * (mate 1, mate 2).  Everything is an exact integer sum, so shards merge by
+ * plain addition.
+ */
+#define HPGQ_S_NUM_INPUT      0  /* reads seen                                 */
+#define HPGQ_S_NUM_PASSED     1  /* reads that passed (== input if no filter)  */
+#define HPGQ_S_NUM_FAILED     2
+#define HPGQ_S_NUM_EDITED     3  /* reads whose trim removed >= 1 base         */
+#define HPGQ_S_NUM_STATS      4  /* reads merged into stats (counters->num_reads) */
+#define HPGQ_S_ACC_MEANQ_FX16 5  /* sum of floor(65536*sumQraw/len) (acc_quality) */
+#define HPGQ_S_LONG_READS     6  /* reads longer than lmax (error)             */
+#define HPGQ_S_RESERVED       7
+#define HPGQ_NUM_SCALARS      8
+
+#define HPGQ_MEANQ_BINS 256
+#define HPGQ_GC_BINS    101
+
+static inline size_t hpgq_off_hist_len(int lmax)   { (void)lmax; return HPGQ_NUM_SCALARS; }
+static inline size_t hpgq_off_hist_meanq(int lmax) { return HPGQ_NUM_SCALARS + (size_t)lmax + 1; }
+static inline size_t hpgq_off_hist_gc(int lmax)    { return hpgq_off_hist_meanq(lmax) + HPGQ_MEANQ_BINS; }
+static inline size_t hpgq_off_pos_qsum(int lmax)   { return hpgq_off_hist_gc(lmax) + HPGQ_GC_BINS; }
+static inline size_t hpgq_off_pos_base(int lmax, int b) {
+  return hpgq_off_pos_qsum(lmax) + (size_t)lmax * (size_t)(1 + b);
+}
+static inline size_t hpgq_counters_len(int lmax)   { return hpgq_off_pos_base(lmax, 5); }
+
+/* base order inside pos_base */
+#define HPGQ_BASE_A 0
+#define HPGQ_BASE_C 1
+#define HPGQ_BASE_G 2
+#define HPGQ_BASE_T 3
+#define HPGQ_BASE_N 4
+
+/* Derived view of one counter set (stats_counters_t, src/stats_fastq.h:35-73). */
+typedef struct hpgq_summary {
+  uint64_t num_reads;        /* reads merged into stats                       */
+  uint64_t num_passed, num_failed, num_edited, num_input;
+  int32_t  min_length, max_length;   /* 100000 / 0 when no reads (stats_counters_new) */
+  uint64_t acc_length;
+  double   mean_length;
+  double   mean_quality_raw; /* acc_quality/num_reads, raw units (fx16 exact sum) */
+  uint64_t num_A, num_C, num_G, num_T, num_N;
+} hpgq_summary_t;
+
+int hpgq_counters_summary(const uint64_t *set, int lmax, hpgq_summary_t *out);
+
+/* ---------------------------------------------------------------------- */
+/* engine context                                                         */
+/* ---------------------------------------------------------------------- */
+
+typedef struct hpgq_ctx hpgq_ctx_t;
+
+/* Open a ctx on HIP device `device` (its own stream, counters zeroed). */
+int  hpgq_open(hpgq_ctx_t **ctx, int device, const hpgq_params_t *p);
+void hpgq_close(hpgq_ctx_t *ctx);
+
+/*
+ * Resident path: all pointers are DEVICE pointers (HBM).  Runs the fused
+ * edit -> filter -> stats kernel asynchronously on the ctx stream and
+ * accumulates into the ctx counters.  mask_out[i] = 1 if read (pair) i
+ * passed, 0 otherwise; trim_out[i] = trim_start | trim_end << 16 when edit
+ * is on (for pairs: mate 1 in trim_out[i], mate 2 in trim_out[num_reads+i]).
+ * Either output may be NULL.  For paired ctxs b2 is mate 2 (same num_reads),
+ * else it must be NULL.
+ */
+int  hpgq_run_device(hpgq_ctx_t *ctx, const hpgq_batch_t *b, const hpgq_batch_t *b2,
+                     uint8_t *mask_out, uint32_t *trim_out);
+
+/*
+ * Host path: pointers are HOST memory.  Copies the batch to the device
+ * (pinned staging, async), runs the kernel and copies mask/trim back; the
+ * outputs are valid after hpgq_sync().
+ */
+int  hpgq_run_host(hpgq_ctx_t *ctx, const hpgq_batch_t *b, const hpgq_batch_t *b2,
+                   uint8_t *mask_out, uint32_t *trim_out);
+
+/* Wait for all work on the ctx stream; reports HPGQ_E_READ_TOO_LONG. */
+int  hpgq_sync(hpgq_ctx_t *ctx);
+
+/* Zero the ctx counters (async on the ctx stream). */
+int  hpgq_reset(hpgq_ctx_t *ctx);
+
+/* Number of uint64 in this ctx's counter buffer (1 or 2 sets). */
+size_t hpgq_counters_size(const hpgq_ctx_t *ctx);
+
+/* Copy the counters to host memory (synchronises the ctx). */
+int  hpgq_read_counters(hpgq_ctx_t *ctx, uint64_t *out, size_t n);
+
+/* Device pointer of the counter buffer (for an external all-reduce). */
+uint64_t *hpgq_counters_device(hpgq_ctx_t *ctx);
+
+/* HIP stream (hipStream_t) the ctx runs on. */
+void *hpgq_stream(hpgq_ctx_t *ctx);
+
+/* ---------------------------------------------------------------------- */
+/* multi-GPU: RCCL over xGMI (one process per GPU)                        */
+/* ---------------------------------------------------------------------- */
+
+#define HPGQ_COMM_ID_BYTES 128
+
+/* rank 0 creates the id and ships it to the other ranks out of band */
+int  hpgq_comm_unique_id(char id[HPGQ_COMM_ID_BYTES]);
+int  hpgq_comm_init(hpgq_ctx_t *ctx, int nranks, int rank, const char id[HPGQ_COMM_ID_BYTES]);
+/* in-place ncclAllReduce(sum, uint64) of the packed counters on the ctx stream */
+int  hpgq_allreduce(hpgq_ctx_t *ctx);
+
+/* ---------------------------------------------------------------------- */
+/* chaos-game (CGR) accumulator, old/chaos_game.c:165-267                 */
+/* ---------------------------------------------------------------------- */
+
+#define HPGQ_CGR_ALL_READS        0
+#define HPGQ_CGR_ONLY_VALID_READS 1   /* mode == ONLY_VALID_READS (:188) */
+
+typedef struct hpgq_cgr hpgq_cgr_t;
+
+/*
+ * k: word size (dim = 2^k, tables dim x dim, 1 <= k <= 12);
+ * base_quality: subtracted k times per word (chaos_game_data_init :97).
+ */
+int  hpgq_cgr_open(hpgq_cgr_t **cg, int device, int k, int base_quality);
+void hpgq_cgr_close(hpgq_cgr_t *cg);
+
+/*
+ * One chaos_game_fill_tables() call over a DEVICE batch.  The double CGR
+ * state starts at (dim/2, dim/2) for every call and is carried across the
+ * reads of the batch exactly as the reference does.  status (device, may be
+ * NULL) is read_status[]; in ONLY_VALID_READS mode reads with status[i] != 1
+ * (VALID_READ) are skipped.
+ */
+int  hpgq_cgr_fill_device(hpgq_cgr_t *cg, const hpgq_batch_t *b, const uint8_t *status, int mode);
+int  hpgq_cgr_sync(hpgq_cgr_t *cg);
+int  hpgq_cgr_reset(hpgq_cgr_t *cg);
+/* table_seq, table_q: dim*dim uint32 each, row-major [co_x][co_y]; word_count: fq_word_count */
+int  hpgq_cgr_read(hpgq_cgr_t *cg, uint32_t *table_seq, uint32_t *table_q, uint32_t *word_count);
+void *hpgq_cgr_stream(hpgq_cgr_t *cg);
+/* reads the last fill call had to replay sequentially (diagnostic) */
+int64_t hpgq_cgr_last_replays(hpgq_cgr_t *cg);
+
+/* ---------------------------------------------------------------------- */
+/* synthetic input (bench / tests): counter-based, identical on host & GPU */
+/* ---------------------------------------------------------------------- */
+
+typedef struct hpgq_synth {
+  uint64_t seed;
+  int32_t  read_length;      /* L                                            */
+  int32_t  trunc_pct;        /* % of reads truncated to U[20, L]            */
+  int32_t  bad_pct;          /* % of reads with Q centred at 12             */
+  int32_t  n_per_1024;       /* 'N' probability x 1024                      */
+  int32_t  phred;            /* quality offset                              */
+  int32_t  mate;             /* 0 or 1 (mate 2 reuses mate 1's lengths)     */
+} hpgq_synth_t;
+
+/* read length of read `idx` (host, no device needed) */
+int32_t hpgq_synth_length(const hpgq_synth_t *s, int64_t idx);
+/* data_indices (n+1 entries, starting at 0) of reads [first, first+n) */
+int  hpgq_synth_indices_host(const hpgq_synth_t *s, int64_t first, int64_t n, int32_t *idx_host);
+/* Fill seq/quality of reads [first, first+n) on the device; idx_dev must
+ * already hold hpgq_synth_indices_host()'s output. Async on `stream`. */
+int  hpgq_synth_device(const hpgq_synth_t *s, int64_t first, int64_t n,
+                       char *seq_dev, char *qual_dev, const int32_t *idx_dev, void *stream);
+
+/* number of visible HIP devices (0 when none or the runtime fails) */
+int  hpgq_device_count(void);
+
+const char *hpgq_strerror(int code);
+const char *hpgq_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HPGQ_H */

@@ -1,0 +1,384 @@
+/*
+ * hpgq_oracle.c — CPU restatement of hpg-fastq's per-read QC hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This file is the parity checker for the HIP
+ * engine in hpg-fastq_amd/ and the timed CPU baseline of bench.py
+ * (cpu_baseline.kind = "port").  Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load it; the product never links it.
+ *
+ * PARITY STATUS:
+ *   - stats merge (A4): restates the consumer merge of the reference,
+ *     src/stats_fastq.c:257-417, over dense u64 counters.
+ *   - filter (A5), per-read stats (A3), edit/trim (A6): the reference calls
+ *     fastq_filter / fastq_reads_stats / fastq_edit from the bioinfo-libs
+ *     submodule, which is EMPTY in /root/reference (.gitmodules:1-6; pinned
+ *     version unknown).  These follow the written spec in DESIGN.md §3,
+ *     derived from the call sites and help texts cited inline.
+ *     -> "parity unpinned": the reference holds no tests, fixtures or golden
+ *        vectors for this path, and its CPU path cannot be built here.
+ *   - CGR (A7): line-by-line restatement of chaos_game_fill_tables,
+ *     old/chaos_game.c:165-267.  The reference file needs an absent header
+ *     (qc_batch.h) so it is not built here -> also "parity unpinned".
+ *   Every restated rule is cross-checked against an independent pure-Python
+ *   restatement (oracle/pyref.py) on the hand-written fixtures in
+ *   tests/golden/.
+ *
+ * Build: make -C oracle  ->  oracle/liboracle.so (gcc -O3 -fopenmp).
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <omp.h>
+
+#include "../include/hpgq.h"
+
+/* ------------------------------------------------------------------ */
+/* synthetic generator (restated independently of the product copy;   */
+/* SURVEY §8d input description)                                      */
+/* ------------------------------------------------------------------ */
+
+static inline uint64_t o_mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+static inline uint64_t o_read_key(const hpgq_synth_t *s, int64_t idx) {
+  return o_mix64(s->seed * 0x9E3779B97F4A7C15ULL + (uint64_t)idx);
+}
+
+int32_t oracle_synth_length(const hpgq_synth_t *s, int64_t idx) {
+  uint64_t r = o_read_key(s, idx);
+  int32_t L = s->read_length;
+  if (L >= 20 && (int32_t)(r % 100) < s->trunc_pct)
+    L = 20 + (int32_t)(o_mix64(r ^ 1ULL) % (uint64_t)(s->read_length - 20 + 1));
+  return L;
+}
+
+/* fills reads [first, first+n); idx gets n+1 offsets starting at 0 */
+void oracle_synth(const hpgq_synth_t *s, int64_t first, int64_t n,
+                  char *seq, char *qual, int32_t *idx) {
+  static const char acgt[4] = {'A', 'C', 'G', 'T'};
+  idx[0] = 0;
+  for (int64_t i = 0; i < n; i++) idx[i + 1] = idx[i] + oracle_synth_length(s, first + i);
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < n; i++) {
+    uint64_t r = o_read_key(s, first + i);
+    uint64_t mk = s->mate ? o_mix64(r ^ 0x5EEDULL) : r;
+    int bad = (int32_t)((mk >> 20) % 100) < s->bad_pct;
+    int32_t L = idx[i + 1] - idx[i];
+    for (int32_t j = 0; j < L; j++) {
+      uint64_t h = o_mix64(mk + (uint64_t)(j + 1) * 0xD1B54A32D192ED03ULL);
+      char b = ((int32_t)(h & 1023) < s->n_per_1024) ? 'N' : acgt[(h >> 10) & 3];
+      int32_t noise = (int32_t)((h >> 12) % 13) - 6;
+      int32_t q = bad ? 12 + noise : 40 - (20 * j) / L + noise;
+      if (q < 2) q = 2;
+      if (q > 41) q = 41;
+      seq[idx[i] + j] = b;
+      qual[idx[i] + j] = (char)(q + s->phred);
+    }
+  }
+}
+
+/* ------------------------------------------------------------------ */
+/* per-read arithmetic                                                */
+/* ------------------------------------------------------------------ */
+
+typedef struct {
+  int32_t ts, te;     /* trim start / end (A6) */
+  int     pass;
+} o_read_result_t;
+
+/* mean-Q window check: min*k <= sum(Q) <= max*k, exact integers
+ * (equals min <= sum/k <= max for the float mean the help text implies,
+ *  src/stats_options.c:276,278,280) */
+static inline int o_mean_in(int64_t sumq, int64_t k, int64_t lo, int64_t hi) {
+  return lo * k <= sumq && sumq <= hi * k;
+}
+
+/*
+ * fastq_edit (A6), build-defined: within the first left_len bases drop the
+ * leading run with Q outside [minL,maxL]; within the last right_len bases of
+ * what is left drop the trailing run with Q outside [minR,maxR]
+ * (src/edit_options.c:280-283 "leftmost nucleotides to take into account to
+ *  trim"; old/README:48-49,81-82 "trim of the first or last nucleotides if
+ *  the selected criteria is not accomplished").
+ */
+static void o_trim(const hpgq_params_t *p, const unsigned char *q, int32_t n,
+                   int32_t *ts_out, int32_t *te_out) {
+  int32_t ts = 0, te = 0;
+  if (p->edit_left_length > 0) {
+    int32_t lim = p->edit_left_length < n ? p->edit_left_length : n;
+    while (ts < lim) {
+      int32_t Q = (int32_t)q[ts] - p->phred;
+      if (Q >= p->edit_min_left_quality && Q <= p->edit_max_left_quality) break;
+      ts++;
+    }
+  }
+  if (p->edit_right_length > 0) {
+    int32_t rem = n - ts;
+    int32_t lim = p->edit_right_length < rem ? p->edit_right_length : rem;
+    while (te < lim) {
+      int32_t Q = (int32_t)q[n - 1 - te] - p->phred;
+      if (Q >= p->edit_min_right_quality && Q <= p->edit_max_right_quality) break;
+      te++;
+    }
+  }
+  *ts_out = ts;
+  *te_out = te;
+}
+
+/*
+ * fastq_filter (A5), build-defined from fastq_filter_options_new's 12
+ * arguments (src/filter_fastq.c:140-145) and the option help texts
+ * (src/stats_options.c:275-282).  Thresholds are Phred (Q = char - phred).
+ */
+static int o_filter(const hpgq_params_t *p, const unsigned char *s,
+                    const unsigned char *q, int32_t n) {
+  if (n < p->min_read_length || n > p->max_read_length) return 0;
+  int64_t sumq = 0, nN = 0, oor = 0;
+  for (int32_t j = 0; j < n; j++) {
+    int32_t Q = (int32_t)q[j] - p->phred;
+    sumq += Q;
+    if (s[j] == 'N') nN++;
+    if (Q < p->min_read_quality || Q > p->max_read_quality) oor++;
+  }
+  if (nN > p->max_N) return 0;
+  if (!o_mean_in(sumq, n, p->min_read_quality, p->max_read_quality)) return 0;
+  if (oor > p->max_out_of_quality) return 0;
+  if (p->left_length > 0) {
+    int32_t k = p->left_length < n ? p->left_length : n;
+    int64_t sl = 0;
+    for (int32_t j = 0; j < k; j++) sl += (int32_t)q[j] - p->phred;
+    if (k > 0 && !o_mean_in(sl, k, p->min_left_quality, p->max_left_quality)) return 0;
+  }
+  if (p->right_length > 0) {
+    int32_t k = p->right_length < n ? p->right_length : n;
+    int64_t sr = 0;
+    for (int32_t j = n - k; j < n; j++) sr += (int32_t)q[j] - p->phred;
+    if (k > 0 && !o_mean_in(sr, k, p->min_right_quality, p->max_right_quality)) return 0;
+  }
+  return 1;
+}
+
+/*
+ * Per-read stats + the consumer merge (A3 + A4), src/stats_fastq.c:283-382:
+ *   length histogram             :306-314 (key = read_length)
+ *   quality histogram            :316-324 (key = round(quality_average), raw units)
+ *   GC histogram                 :326-334 (key = 100*(G+C)/read_length, integer division)
+ *   per position j < read_length :338-382 (quality[j] raw; A/T/C/G/N exact uppercase)
+ *   acc_quality (float, :297)    -> exact fixed point sum, HPGQ_S_ACC_MEANQ_FX16
+ * len 0 reads get no quality/GC bin (quirk Q8: the reference divides by zero).
+ */
+static void o_merge(uint64_t *c, int lmax, const unsigned char *s,
+                    const unsigned char *q, int32_t n) {
+  c[HPGQ_S_NUM_STATS]++;
+  if (n > lmax) { c[HPGQ_S_LONG_READS]++; return; }
+  c[hpgq_off_hist_len(lmax) + n]++;
+  uint64_t sraw = 0, gc = 0;
+  uint64_t *pq = c + hpgq_off_pos_qsum(lmax);
+  for (int32_t j = 0; j < n; j++) {
+    sraw += q[j];
+    pq[j] += q[j];
+    int b = -1;
+    switch (s[j]) {
+      case 'A': b = HPGQ_BASE_A; break;
+      case 'C': b = HPGQ_BASE_C; gc++; break;
+      case 'G': b = HPGQ_BASE_G; gc++; break;
+      case 'T': b = HPGQ_BASE_T; break;
+      case 'N': b = HPGQ_BASE_N; break;
+      default: break;
+    }
+    if (b >= 0) c[hpgq_off_pos_base(lmax, b) + j]++;
+  }
+  if (n > 0) {
+    uint64_t key = (2 * sraw + (uint64_t)n) / (2 * (uint64_t)n);   /* round(sraw/n) */
+    c[hpgq_off_hist_meanq(lmax) + key]++;
+    c[hpgq_off_hist_gc(lmax) + (100 * gc) / (uint64_t)n]++;
+    c[HPGQ_S_ACC_MEANQ_FX16] += (sraw << 16) / (uint64_t)n;
+  }
+}
+
+static void o_read_eval(const hpgq_params_t *p, const hpgq_batch_t *b, int64_t i,
+                        o_read_result_t *r) {
+  int32_t a = b->data_indices[i], e = b->data_indices[i + 1];
+  int32_t n = e - a;
+  const unsigned char *q = (const unsigned char *)b->quality + a;
+  const unsigned char *s = (const unsigned char *)b->seq + a;
+  r->ts = r->te = 0;
+  if (p->edit_on) o_trim(p, q, n, &r->ts, &r->te);
+  int32_t m = n - r->ts - r->te;
+  r->pass = p->filter_on ? o_filter(p, s + r->ts, q + r->ts, m) : 1;
+}
+
+static void o_account(const hpgq_params_t *p, const hpgq_batch_t *b, int64_t i,
+                      const o_read_result_t *r, int pass, uint64_t *c) {
+  int32_t a = b->data_indices[i], e = b->data_indices[i + 1];
+  int32_t n = e - a;
+  c[HPGQ_S_NUM_INPUT]++;
+  if (pass) c[HPGQ_S_NUM_PASSED]++; else c[HPGQ_S_NUM_FAILED]++;
+  if (r->ts + r->te > 0) c[HPGQ_S_NUM_EDITED]++;
+  if (p->stats_on && pass)
+    o_merge(c, p->lmax, (const unsigned char *)b->seq + a + r->ts,
+            (const unsigned char *)b->quality + a + r->ts, n - r->ts - r->te);
+}
+
+/*
+ * One engine call: edit -> filter -> stats over a host batch (and its mate
+ * batch when p->paired).  counters: hpgq_counters_len(lmax) u64 per set
+ * (2 sets when paired), ACCUMULATED into.  nthreads <= 0: OpenMP default.
+ */
+int oracle_run(const hpgq_params_t *p, const hpgq_batch_t *b, const hpgq_batch_t *b2,
+               uint8_t *mask, uint32_t *trim, uint64_t *counters, int nthreads) {
+  int lmax = p->lmax;
+  size_t clen = hpgq_counters_len(lmax);
+  int nsets = p->paired ? 2 : 1;
+  if (p->paired && (!b2 || b2->num_reads != b->num_reads)) return HPGQ_E_INVALID;
+  int nt = nthreads > 0 ? nthreads : omp_get_max_threads();
+  uint64_t *part = (uint64_t *)calloc((size_t)nt * nsets * clen, sizeof(uint64_t));
+  if (!part) return HPGQ_E_NOMEM;
+  int64_t nr = b->num_reads;
+#pragma omp parallel num_threads(nt)
+  {
+    int t = omp_get_thread_num();
+    uint64_t *c0 = part + (size_t)t * nsets * clen;
+    uint64_t *c1 = c0 + clen;
+#pragma omp for schedule(static)
+    for (int64_t i = 0; i < nr; i++) {
+      o_read_result_t r1, r2;
+      o_read_eval(p, b, i, &r1);
+      int pass = r1.pass;
+      if (p->paired) {
+        o_read_eval(p, b2, i, &r2);
+        pass = pass && r2.pass;   /* pair-consistent filter */
+      }
+      if (mask) mask[i] = (uint8_t)pass;
+      if (trim) {
+        trim[i] = (uint32_t)r1.ts | ((uint32_t)r1.te << 16);
+        if (p->paired) trim[nr + i] = (uint32_t)r2.ts | ((uint32_t)r2.te << 16);
+      }
+      o_account(p, b, i, &r1, pass, c0);
+      if (p->paired) o_account(p, b2, i, &r2, pass, c1);
+    }
+  }
+  for (int t = 0; t < nt; t++) {
+    const uint64_t *src = part + (size_t)t * nsets * clen;
+    for (size_t k = 0; k < nsets * clen; k++) counters[k] += src[k];
+  }
+  free(part);
+  return HPGQ_OK;
+}
+
+/* ------------------------------------------------------------------ */
+/* chaos game: chaos_game_fill_tables, old/chaos_game.c:165-267       */
+/* ------------------------------------------------------------------ */
+
+#define O_EPSILON 0.00001          /* old/chaos_game.h:41 */
+
+/*
+ * One call = one batch.  f starts at dim/2 (:107-108 read back at :180-181;
+ * the function never stores f back, so every call restarts there) and is
+ * carried across the reads of the batch; the word counter and quality
+ * accumulator reset per read (:263-264).  table_seq/table_q are dim*dim u32
+ * row-major [co_x][co_y] and are accumulated into; *word_count is
+ * fq_word_count (u32, wraps).
+ */
+int oracle_cgr_fill(int k, int base_quality, const hpgq_batch_t *b, const uint8_t *status,
+                    int mode, uint32_t *table_seq, uint32_t *table_q, uint32_t *word_count) {
+  if (k < 1 || k > 12) return HPGQ_E_INVALID;
+  int dim_n = 1 << k;
+  int word_size = k;
+  int word_quality_substract = base_quality * word_size;     /* :185 */
+  int nt_word_count = 0;
+  unsigned int acc_word_quality = 0;
+  double f_x = (double)(dim_n * 0.5), f_y = f_x;            /* :107-108 */
+  const char *seq = b->seq, *quality = b->quality;
+  for (int64_t i = 0; i < b->num_reads; i++) {
+    if (mode == HPGQ_CGR_ONLY_VALID_READS && (!status || status[i] != 1)) continue;  /* :188 */
+    int read_position = b->data_indices[i];
+    int read_length = b->data_indices[i + 1] - b->data_indices[i];
+    int quality_position = read_position;
+    for (int j = 0; j < read_length; j++) {
+      char quality_character = quality[quality_position++];
+      switch (seq[read_position++]) {
+        case 65:   /* A :201-207 */
+          f_x = f_x + ((dim_n - f_x) * 0.5);
+          f_y = f_y * 0.5;
+          nt_word_count++;
+          acc_word_quality += quality_character;
+          break;
+        case 67:   /* C :208-214 */
+          f_x = f_x * 0.5;
+          f_y = f_y * 0.5;
+          nt_word_count++;
+          acc_word_quality += quality_character;
+          break;
+        case 71:   /* G :215-221 */
+          f_x = f_x * 0.5;
+          f_y = f_y + ((dim_n - f_y) * 0.5);
+          nt_word_count++;
+          acc_word_quality += quality_character;
+          break;
+        case 84:   /* T :222-228 */
+          f_x = f_x + ((dim_n - f_x) * 0.5);
+          f_y = f_y + ((dim_n - f_y) * 0.5);
+          nt_word_count++;
+          acc_word_quality += quality_character;
+          break;
+        case 78:   /* N :229-233 */
+          nt_word_count = 0;
+          acc_word_quality = 0;
+          break;
+        default:
+          break;
+      }
+      if (nt_word_count == word_size) {                       /* :236-260 */
+        int co_x = (int)f_x;
+        int co_y = (int)f_y;
+        if (co_x == dim_n) { co_x = dim_n - 1; f_x = f_x - O_EPSILON; }
+        if (co_y == dim_n) { co_y = dim_n - 1; f_y = f_y - O_EPSILON; }
+        table_seq[(size_t)co_x * dim_n + co_y]++;
+        (*word_count)++;
+        nt_word_count--;
+        table_q[(size_t)co_x * dim_n + co_y] += (acc_word_quality - word_quality_substract);
+        acc_word_quality = acc_word_quality - quality[quality_position - word_size];
+      }
+    }
+    nt_word_count = 0;                                          /* :263-264 */
+    acc_word_quality = 0;
+  }
+  return HPGQ_OK;
+}
+
+/* independent batches (each its own fill call) in parallel: the CPU baseline
+ * for config C5 (state resets per call, so batches are independent). */
+int oracle_cgr_fill_batches(int k, int base_quality, const hpgq_batch_t *bs, int nb,
+                            uint32_t *table_seq, uint32_t *table_q, uint32_t *word_count,
+                            int nthreads) {
+  int dim = 1 << k;
+  size_t cells = (size_t)dim * dim;
+  int nt = nthreads > 0 ? nthreads : omp_get_max_threads();
+  uint32_t *ts = (uint32_t *)calloc((size_t)nt * cells * 2, sizeof(uint32_t));
+  uint32_t *wc = (uint32_t *)calloc((size_t)nt, sizeof(uint32_t));
+  if (!ts || !wc) { free(ts); free(wc); return HPGQ_E_NOMEM; }
+  int err = 0;
+#pragma omp parallel for num_threads(nt) schedule(dynamic, 1)
+  for (int i = 0; i < nb; i++) {
+    int t = omp_get_thread_num();
+    int e = oracle_cgr_fill(k, base_quality, &bs[i], NULL, HPGQ_CGR_ALL_READS,
+                            ts + (size_t)t * cells * 2, ts + (size_t)t * cells * 2 + cells, wc + t);
+    if (e) err = e;
+  }
+  for (int t = 0; t < nt; t++) {
+    for (size_t c = 0; c < cells; c++) {
+      table_seq[c] += ts[(size_t)t * cells * 2 + c];
+      table_q[c] += ts[(size_t)t * cells * 2 + cells + c];
+    }
+    *word_count += wc[t];
+  }
+  free(ts);
+  free(wc);
+  return err;
+}
+
+int oracle_max_threads(void) { return omp_get_max_threads(); }

@@ -1,0 +1,208 @@
+"""HIP engine parity: libhpgq (gfx950) vs the CPU oracle, bit for bit.
+
+Every test runs the fused edit -> filter -> stats kernel through the C-ABI and
+compares masks, trims and the packed u64 counters with oracle/liboracle.so on
+the same seeded input (the oracle restates
+src/stats_fastq.c:257-417 plus the build-defined filter/edit spec).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import hpgfastq as H
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+
+def gpu_host_path(params, reads, reads2=None):
+    with H.Engine(params) as e:
+        b2 = (reads2.seq, reads2.qual, reads2.idx) if reads2 is not None else (None,) * 3
+        mask, trim = e.process(reads.seq, reads.qual, reads.idx, *b2)
+        return mask, trim, e.counters()
+
+
+def assert_same(params, reads, reads2=None, gpu=None):
+    m_o, t_o, c_o = O.run(params, reads, reads2)
+    m_g, t_g, c_g = gpu if gpu is not None else gpu_host_path(params, reads, reads2)
+    np.testing.assert_array_equal(m_g, m_o)
+    if params.edit_on:
+        np.testing.assert_array_equal(t_g, t_o)
+    if not np.array_equal(c_g, c_o):
+        bad = np.nonzero(c_g != c_o)[0]
+        raise AssertionError(f"counters differ at {bad[:10]} gpu={c_g[bad[:10]]} "
+                             f"oracle={c_o[bad[:10]]} layout={H.layout(params.lmax)}")
+    return c_o
+
+
+STATS_CASES = {
+    "stats": dict(),
+    "c2_filter": dict(read_quality_range="20,", read_length_range="50,"),
+    "all_filters": dict(read_length_range="60,140", read_quality_range="22,38", max_N=0,
+                        max_out_of_quality=10, left_length=10, left_quality_range="25,",
+                        right_length=15, right_quality_range="15,40"),
+    "max_n": dict(max_N=1),
+    "oor_only": dict(read_quality_range="10,35", max_out_of_quality=3),
+}
+
+
+@pytest.mark.parametrize("name", sorted(STATS_CASES))
+def test_stats_filter_synthetic(name):
+    reads = O.synth(20000, seed=2, L=150, trunc_pct=5, n_per_1024=8)
+    p = H.stats_params(lmax=150, **STATS_CASES[name])
+    c = assert_same(p, reads)
+    assert c[H.S_NUM_INPUT] == reads.n
+
+
+def test_filter_only_mask():
+    reads = O.synth(30000, seed=3, L=150, trunc_pct=10)
+    p = H.filter_params(lmax=150, read_quality_range="20,", read_length_range="50,")
+    assert_same(p, reads)
+
+
+@pytest.mark.parametrize("L,lmax", [(250, 250), (100, 256), (300, 512), (1000, 1024), (37, 40)])
+def test_read_lengths(L, lmax):
+    reads = O.synth(3000, seed=7, L=L, trunc_pct=30, n_per_1024=20)
+    p = H.stats_params(lmax=lmax, read_quality_range="15,", read_length_range="30,")
+    assert_same(p, reads)
+
+
+def test_edit_trim_stats():
+    reads = O.synth(20000, seed=4, L=150, trunc_pct=5)
+    p = H.edit_params(lmax=150, stats=True, left_length=10, left_quality_range="20,",
+                      right_length=30, right_quality_range="20,")
+    c = assert_same(p, reads)
+    assert c[H.S_NUM_EDITED] > 0
+
+
+def test_edit_with_filter():
+    reads = O.synth(20000, seed=5, L=150, trunc_pct=20)
+    p = H.edit_params(lmax=150, stats=True, left_length=40, left_quality_range="30,",
+                      right_length=60, right_quality_range="25,38",
+                      read_length_range="60,", read_quality_range="20,", max_N=2)
+    assert_same(p, reads)
+
+
+def test_paired_end():
+    r1 = O.synth(10000, seed=6, L=150, trunc_pct=5, mate=0)
+    r2 = O.synth(10000, seed=6, L=150, trunc_pct=5, mate=1)
+    assert np.array_equal(np.diff(r1.idx), np.diff(r2.idx))
+    p = H.stats_params(lmax=150, read_quality_range="20,", read_length_range="50,")
+    p.paired = 1
+    c = assert_same(p, r1, r2)
+    ln = H.counters_len(150)
+    assert c[H.S_NUM_PASSED] == c[ln + H.S_NUM_PASSED]
+
+
+def test_paired_edit():
+    r1 = O.synth(5000, seed=8, L=150, mate=0)
+    r2 = O.synth(5000, seed=8, L=150, mate=1)
+    p = H.edit_params(lmax=150, stats=True, left_length=10, left_quality_range="20,",
+                      right_length=30, right_quality_range="20,", read_quality_range="25,")
+    p.paired = 1
+    assert_same(p, r1, r2)
+
+
+def _edge_reads():
+    rd = []
+    rd.append((b"", b""))                                   # length 0
+    rd.append((b"A", b"I"))                                 # length 1
+    rd.append((b"GGGGCCCCGGGG", b"IIIIIIIIIIII"))           # GC 100
+    rd.append((b"ATATATATAT", b"##########"))               # GC 0, Q2
+    rd.append((b"NNNNNNNN", b"!!!!!!!!"))                   # all N, Q0
+    rd.append((b"acgtnACGTN", b"IIIIIIIIII"))               # lowercase ignored
+    rd.append((b"RYKMSWBDHV-.*ACGT", b"?" * 17))            # IUPAC / junk
+    rd.append((b"ACGT" * 37 + b"AC", bytes(range(40, 190))))  # qualities >= 128
+    rd.append((b"ACGTACGTAC", b"\xff\x80\x7f\x00\x01IIIII"))
+    for L in (2, 3, 4, 5, 63, 64, 65, 127, 128, 129, 149, 150):
+        rd.append(((b"CAGT" * 40)[:L], (b"5?I+" * 40)[:L]))
+    return rd
+
+
+@pytest.mark.parametrize("name", sorted(STATS_CASES))
+def test_edge_reads(name):
+    reads = O.Reads.from_pairs(_edge_reads() * 7)
+    p = H.stats_params(lmax=150, **STATS_CASES[name])
+    assert_same(p, reads)
+
+
+def test_edge_reads_edit_phred64():
+    reads = O.Reads.from_pairs(_edge_reads() * 5)
+    p = H.edit_params(lmax=150, stats=True, quality_encoding="phred64", left_length=5,
+                      left_quality_range="0,10", right_length=7, right_quality_range="3,",
+                      read_quality_range="1,")
+    assert_same(p, reads)
+
+
+def test_all_fail_and_empty_batch():
+    reads = O.synth(5000, seed=9, L=150)
+    p = H.stats_params(lmax=150, read_length_range="151,")
+    c = assert_same(p, reads)
+    assert c[H.S_NUM_PASSED] == 0
+    empty = O.Reads(np.zeros(0, np.uint8), np.zeros(0, np.uint8), np.zeros(1, np.int32))
+    with H.Engine(p) as e:
+        mask, _ = e.process(empty.seq, empty.qual, empty.idx)
+        assert e.counters().sum() == 0
+
+
+def test_read_too_long_reports_error():
+    reads = O.synth(100, seed=1, L=200)
+    p = H.stats_params(lmax=150)
+    with H.Engine(p) as e:
+        with pytest.raises(H.HpgqError) as ei:
+            e.process(reads.seq, reads.qual, reads.idx)
+        assert ei.value.code == -4
+
+
+def test_accumulates_across_batches_and_offsets():
+    """Counters merge over calls; data_indices need not start at 0."""
+    reads = O.synth(12000, seed=10, L=150, trunc_pct=15)
+    p = H.stats_params(lmax=150, read_quality_range="20,")
+    _, _, c_o = O.run(p, reads)
+    with H.Engine(p) as e:
+        for lo, hi in [(0, 5000), (5000, 5001), (5001, 12000)]:
+            idx = reads.idx[lo:hi + 1].copy()   # absolute offsets into the full buffers
+            b = H.engine.host_batch(reads.seq, reads.qual, idx)
+            mask = np.zeros(hi - lo, np.uint8)
+            e.run_host(b, None, mask, None)
+            e.sync()
+        np.testing.assert_array_equal(e.counters(), c_o)
+
+
+def test_device_path_torch_buffers():
+    torch = pytest.importorskip("torch")
+    reads = O.synth(50000, seed=11, L=150, trunc_pct=5)
+    p = H.stats_params(lmax=150, read_quality_range="20,", read_length_range="50,")
+    dev = torch.device("cuda", 0)
+    seq = torch.from_numpy(reads.seq).to(dev)
+    qual = torch.from_numpy(reads.qual).to(dev)
+    idx = torch.from_numpy(reads.idx).to(dev)
+    mask = torch.zeros(reads.n, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    with H.Engine(p) as e:
+        b = H.engine.device_batch(reads.n, seq.data_ptr(), qual.data_ptr(), idx.data_ptr())
+        e.run_device(b, None, mask.data_ptr(), None)
+        e.sync()
+        gpu = (mask.cpu().numpy(), None, e.counters())
+    assert_same(p, reads, gpu=gpu)
+
+
+def test_synth_device_matches_oracle_generator():
+    torch = pytest.importorskip("torch")
+    n = 20000
+    s = H.Synth(77, 150, 5, 5, 1, 33, 1)
+    idx = np.zeros(n + 1, np.int32)
+    H.check(H.lib.hpgq_synth_indices_host(C.byref(s), 1234, n, idx.ctypes.data), "idx")
+    ref = O.synth(n, seed=77, L=150, trunc_pct=5, bad_pct=5, n_per_1024=1, mate=1, first=1234)
+    np.testing.assert_array_equal(idx, ref.idx)
+    dev = torch.device("cuda", 0)
+    seq = torch.zeros(int(idx[-1]), dtype=torch.uint8, device=dev)
+    qual = torch.zeros(int(idx[-1]), dtype=torch.uint8, device=dev)
+    didx = torch.from_numpy(idx).to(dev)
+    torch.cuda.synchronize()
+    H.check(H.lib.hpgq_synth_device(C.byref(s), 1234, n, seq.data_ptr(), qual.data_ptr(),
+                                    didx.data_ptr(), None), "synth")
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(seq.cpu().numpy(), ref.seq)
+    np.testing.assert_array_equal(qual.cpu().numpy(), ref.qual)
