@@ -1,0 +1,300 @@
+// hpgq_engine_tri.h — FAST single-end stats/filter kernel, three reads per wave.
+//
+// Same contract and outputs as engine_kernel<1, *, false> (hpgq_engine_kernel.h)
+// for batches whose reads are at most 160 bases: the per-read fixed cost (the
+// DPP reduction, the scalar pass/fail decision, bookkeeping) is shared by three
+// reads and lane utilisation goes from 38/64 to 57/64 at 150 bp.
+//
+//   * the wave is cut into 3 segments of 21 lanes (lane 63 idle); segment k
+//     works on read 3t + k of the block.  Lane ls < 20 of a segment owns
+//     positions 8ls..8ls+7 (160 per read); lane 20 only donates its first dword
+//     to lane 19.
+//   * each lane fetches its segment's read offsets from the block prologue
+//     registers with ds_bpermute, then ONE buffer_load_dwordx2 per buffer
+//     (SRD bounds check), DPP wave_shl:1 for the neighbour's dword and two
+//     v_alignbyte per buffer realign the 8 bytes.
+//   * per-read sums (raw quality | G+C << 18) use ONE inclusive DPP prefix scan
+//     for the three segments; segment totals are differences of the scan at
+//     lanes 20, 41, 62 (SALU).
+//   * per-position counters as in engine_kernel (6-bit base fields, 16-bit
+//     quality pairs), 8 positions per lane, segment masks from the pass bits.
+// The stats layout, histogram rules and workgroup epilogue are identical, so
+// the two kernels are interchangeable (the tests run both against the oracle).
+#pragma once
+#include "hpgq_engine_kernel.h"
+
+namespace hpgq {
+
+constexpr int kTriW = 21;       // lanes per segment
+constexpr int kTriPos = 160;    // positions per segment (20 owning lanes x 8)
+constexpr int kTriBlock = 60;   // reads per block (20 triples)
+constexpr int kTriU = 5;        // triples per pipeline group (4 groups per full block)
+
+typedef unsigned v2u __attribute__((ext_vector_type(2)));
+
+struct TriPending {
+  v2u s, q;        // raw dword pairs
+  uint32_t info;   // this lane's read: n | als << 16 | alq << 20
+};
+
+__device__ __forceinline__ uint32_t next_lane0(uint32_t v) {   // lane i <- lane i+1, lane 63 <- 0
+  return __builtin_amdgcn_mov_dpp(v, 0x130, 0xF, 0xF, true);
+}
+
+// inclusive prefix sum over the wave (row scans + row broadcasts)
+__device__ __forceinline__ uint32_t wave_scan(uint32_t v) {
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xF, 0xF, true);
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xF, 0xF, true);
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xF, 0xF, true);
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xF, 0xF, true);
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xA, 0xF, false);
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xC, 0xF, false);
+  return v;
+}
+
+struct TriAcc {
+  uint32_t pk[8];           // positions p0..p0+7, 6-bit base fields
+  uint32_t q02[2], q13[2];  // quality 16-bit pairs per dword
+  __device__ __forceinline__ void zero() {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) pk[i] = 0;
+    q02[0] = q02[1] = q13[0] = q13[1] = 0;
+  }
+  __device__ __forceinline__ void add_word(int w, uint32_t sw, uint32_t qw, uint32_t m) {
+    const uint32_t s = (sw & m) | (0x08080808u & ~m);   // pad -> garbage field
+    const uint32_t q = qw & m;
+    const uint32_t codes = (s >> 1) & 0x07070707u;
+    uint32_t sh = __builtin_amdgcn_perm(kShHi, kShLo, codes);
+    const uint32_t ex = __builtin_amdgcn_perm(kExpHi, kExpLo, codes);
+    if (__builtin_expect(s != ex, 0)) {   // bytes that are not exactly A/C/G/T/N
+      const uint32_t d = s ^ ex;
+      const uint32_t nz = (((d & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | d) & 0x80808080u;
+      const uint32_t ff = (nz >> 7) * 0xFFu;
+      sh = (sh & ~ff) | (0x1E1E1E1Eu & ff);
+    }
+    pk[4 * w + 0] += 1u << (sh & 31u);
+    pk[4 * w + 1] += 1u << ((sh >> 8) & 31u);
+    pk[4 * w + 2] += 1u << ((sh >> 16) & 31u);
+    pk[4 * w + 3] += 1u << ((sh >> 24) & 31u);
+    q02[w] += q & 0x00FF00FFu;
+    q13[w] += (q >> 8) & 0x00FF00FFu;
+  }
+  __device__ __forceinline__ void flush(uint32_t *pos_acc, int lmax, int p0) {
+#pragma unroll
+    for (int w = 0; w < 2; ++w) {
+      const uint32_t qv[4] = {q02[w] & 0xFFFFu, q13[w] & 0xFFFFu, q02[w] >> 16, q13[w] >> 16};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int pos = p0 + 4 * w + i;
+        if (pos < lmax) {
+          atomicAdd(&pos_acc[pos], qv[i]);
+#pragma unroll
+          for (int b = 0; b < 5; ++b)
+            atomicAdd(&pos_acc[(1 + b) * lmax + pos], (pk[4 * w + i] >> (6 * b)) & 63u);
+        }
+        pk[4 * w + i] = 0;
+      }
+      q02[w] = q13[w] = 0;
+    }
+  }
+};
+
+__global__ void __launch_bounds__(kWG) engine_tri_kernel(EngineArgs A) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = uni(tid >> 6);
+  const int lmax = A.lmax;
+  const int hlen = lmax + 1 + HPGQ_MEANQ_BINS + HPGQ_GC_BINS;
+  const int seg = lane / kTriW;                 // 0..2, lane 63 -> 3 (idle)
+  const int ls = lane - seg * kTriW;            // 0..20
+  const bool owner = seg < 3 && ls < 20;
+  const int p0 = owner ? 8 * ls : 0x40000000;   // first position of this lane
+  const uint32_t lane8 = 8u * (uint32_t)ls;
+  const bool stats = A.flags & F_STATS, filter = A.flags & F_FILTER;
+
+  // LDS: pos_acc [6][lmax] u32 | hist [hlen] u32 | sc [8] u64
+  uint32_t *pos_acc = reinterpret_cast<uint32_t *>(lds);
+  uint32_t *hist = pos_acc + 6 * lmax;
+  const int hist_words = (hlen + 1) & ~1;
+  unsigned long long *sc = reinterpret_cast<unsigned long long *>(hist + hist_words);
+  for (int i = tid; i < 6 * lmax + hist_words; i += kWG) pos_acc[i] = 0;
+  for (int i = tid; i < HPGQ_NUM_SCALARS; i += kWG) sc[i] = 0;
+  __syncthreads();
+
+  const MateBuf mb = make_mate(A.seq[0], A.qual[0], uni(A.idx[0][A.num_reads]));
+  TriAcc acc;
+  acc.zero();
+  int since_flush = 0;
+  uint64_t fx16 = 0;
+  uint32_t cnt[7] = {0, 0, 0, 0, 0, 0, 0};   // input, passed, failed, edited, stats, long, any-long
+
+  const int64_t nblocks = (A.num_reads + kTriBlock - 1) / kTriBlock;
+  const int64_t gw = (int64_t)blockIdx.x * kWaves + wave;
+  const int64_t nw = (int64_t)gridDim.x * kWaves;
+
+  // block prologue: lane j (< 60) describes read r0 + j
+  auto load_block = [&](int64_t blk, uint32_t &os, uint32_t &oq, uint32_t &inf) {
+    const int64_t r0 = blk * kTriBlock;
+    const int nr = (int)min((int64_t)kTriBlock, A.num_reads - r0);
+    const int l = min(lane, nr - 1);
+    const int a = A.idx[0][r0 + l], e = A.idx[0][r0 + l + 1];
+    const uint32_t xs = (uint32_t)(mb.bs + a), xq = (uint32_t)(mb.bq + a);
+    os = xs & ~3u;
+    oq = xq & ~3u;
+    inf = (uint32_t)(e - a) | ((xs & 3u) << 16) | ((xq & 3u) << 20);
+  };
+
+  TriPending grp[2][kTriU];
+  // issue group g (kTriU triples) of the block described by (os, oq, inf)
+  auto load_group = [&](uint32_t os, uint32_t oq, uint32_t inf, int nt, int g, int slot) {
+#pragma unroll
+    for (int u = 0; u < kTriU; ++u) {
+      const int t = min(g * kTriU + u, nt - 1);   // past the block end: reload the last triple
+      const int src = 4 * min(3 * t + seg, 63);
+      const uint32_t ros = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)os);
+      const uint32_t roq = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)oq);
+      grp[slot][u].info = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)inf);
+      grp[slot][u].s = __builtin_amdgcn_raw_buffer_load_b64(mb.rs, ros + lane8, 0, 0);
+      grp[slot][u].q = __builtin_amdgcn_raw_buffer_load_b64(mb.rq, roq + lane8, 0, 0);
+    }
+  };
+
+  uint32_t os, oq, inf, osn, oqn, infn;
+  int64_t blk = gw;
+  if (blk < nblocks) {
+    load_block(blk, os, oq, inf);
+    const int nr0 = (int)min((int64_t)kTriBlock, A.num_reads - blk * kTriBlock);
+    load_group(os, oq, inf, (nr0 + 2) / 3, 0, 0);
+  }
+  for (; blk < nblocks; blk += nw) {
+    const int64_t r0 = blk * kTriBlock;
+    const int nr = (int)min((int64_t)kTriBlock, A.num_reads - r0);
+    const int nt = (nr + 2) / 3;
+    const int64_t nblk = blk + nw < nblocks ? blk + nw : blk;   // next block (or self)
+    const int nnt = ((int)min((int64_t)kTriBlock, A.num_reads - nblk * kTriBlock) + 2) / 3;
+    load_block(nblk, osn, oqn, infn);
+    uint32_t res_r1 = 0;        // lane j: raw quality sum | GC << 18 of read r0 + j
+    uint64_t passmask = 0;      // bit j: read r0 + j passed
+
+    auto process_group = [&](int g, int slot) {
+#pragma unroll
+      for (int u = 0; u < kTriU; ++u) {
+        const int t = g * kTriU + u;
+        if (t >= nt) break;
+        const TriPending &p = grp[slot][u];
+        const int n = (int)(p.info & 0xFFFFu);
+        const uint32_t als = (p.info >> 16) & 3u, alq = (p.info >> 20) & 3u;
+        const uint32_t s0 = __builtin_amdgcn_alignbyte(p.s.y, p.s.x, als);
+        const uint32_t s1 = __builtin_amdgcn_alignbyte(next_lane0(p.s.x), p.s.y, als);
+        const uint32_t q0 = __builtin_amdgcn_alignbyte(p.q.y, p.q.x, alq);
+        const uint32_t q1 = __builtin_amdgcn_alignbyte(next_lane0(p.q.x), p.q.y, alq);
+        const int nv = n - p0;
+        uint32_t m0 = byte_mask(nv), m1 = byte_mask(nv - 4);
+        // packed per-lane partial: raw quality | G+C << 18
+        uint32_t x = __builtin_amdgcn_sad_u8(q1 & m1, 0u, __builtin_amdgcn_sad_u8(q0 & m0, 0u, 0u));
+        const uint32_t g0 = zero_bytes((s0 | 0x04040404u) ^ 0x47474747u) & m0 & 0x80808080u;
+        const uint32_t g1 = zero_bytes((s1 | 0x04040404u) ^ 0x47474747u) & m1 & 0x80808080u;
+        x += (uint32_t)(__builtin_popcount(g0) + __builtin_popcount(g1)) << 18;
+        const uint32_t P = wave_scan(x);
+        const uint32_t P20 = __builtin_amdgcn_readlane(P, 20);
+        const uint32_t P41 = __builtin_amdgcn_readlane(P, 41);
+        const uint32_t P62 = __builtin_amdgcn_readlane(P, 62);
+        const uint32_t T[3] = {P20, P41 - P20, P62 - P41};
+        uint32_t passbits = 0;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const int j = 3 * t + k;
+          if (j < nr) {
+            const int wn = (int)(__builtin_amdgcn_readlane(p.info, kTriW * k) & 0xFFFFu);
+            bool pass = true;
+            if (filter) {
+              const int sq = (int)(T[k] & 0x3FFFFu) - A.phred * wn;
+              pass = (wn >= A.min_len) & (wn <= A.max_len) & (A.min_q * wn <= sq) &
+                     (sq <= A.max_q * wn);
+            }
+            passbits |= (uint32_t)pass << k;
+            res_r1 = put_lane(res_r1, T[k], j);
+          }
+        }
+        passmask |= (uint64_t)passbits << (3 * t);
+        if (stats && passbits) {
+          const uint32_t keep = 0u - ((passbits >> (seg & 3)) & 1u);   // this lane's read passed
+          m0 &= keep;
+          m1 &= keep;
+          acc.add_word(0, s0, q0, m0);
+          acc.add_word(1, s1, q1, m1);
+          if (++since_flush == kFlushEvery) {
+            acc.flush(pos_acc, lmax, p0);
+            since_flush = 0;
+          }
+        }
+      }
+    };
+
+    const int ngroups = (nt + kTriU - 1) / kTriU;
+    for (int g = 0; g < ngroups; g += 2) {
+      if (g + 1 < ngroups) load_group(os, oq, inf, nt, g + 1, 1);
+      else load_group(osn, oqn, infn, nnt, 0, 1);
+      process_group(g, 0);
+      if (g + 1 < ngroups) {
+        if (g + 2 < ngroups) load_group(os, oq, inf, nt, g + 2, 0);
+        else load_group(osn, oqn, infn, nnt, 0, 0);
+        process_group(g + 1, 1);
+      }
+    }
+
+    // ---- block epilogue (lane j = read r0 + j) ----------------------------
+    const bool valid = lane < nr;
+    const int n = (int)(inf & 0xFFFFu);
+    const bool pass = valid && ((passmask >> lane) & 1u);
+    const bool lg = valid && n > lmax;
+    if (valid && A.mask) A.mask[r0 + lane] = (uint8_t)pass;
+    cnt[0] += (uint32_t)nr;
+    cnt[1] += (uint32_t)__builtin_popcountll(__ballot(pass));
+    cnt[2] += (uint32_t)__builtin_popcountll(__ballot(valid && !pass));
+    cnt[6] += (uint32_t)__builtin_popcountll(__ballot(lg));
+    if (stats) {
+      cnt[4] += (uint32_t)__builtin_popcountll(__ballot(pass));
+      cnt[5] += (uint32_t)__builtin_popcountll(__ballot(pass && lg));
+      if (pass && !lg) {
+        const uint32_t s = res_r1 & 0x3FFFFu, gc = res_r1 >> 18, wn = (uint32_t)n;
+        atomicAdd(&hist[wn], 1u);
+        if (wn > 0) {
+          atomicAdd(&hist[lmax + 1 + (2 * s + wn) / (2 * wn)], 1u);
+          atomicAdd(&hist[lmax + 1 + HPGQ_MEANQ_BINS + (100 * gc) / wn], 1u);
+          const uint32_t q = s / wn, rem = s - q * wn;
+          fx16 += ((uint64_t)q << 16) + (((uint32_t)rem << 16) / wn);
+        }
+      }
+    }
+    os = osn;
+    oq = oqn;
+    inf = infn;
+  }
+
+  // ---- workgroup epilogue ---------------------------------------------------
+  acc.flush(pos_acc, lmax, p0);
+  {
+    const uint32_t lo = (uint32_t)fx16, hi = (uint32_t)(fx16 >> 32);
+    const uint64_t tot = (uint64_t)wave_sum(lo & 0xFFFFu) + ((uint64_t)wave_sum(lo >> 16) << 16) +
+                         ((uint64_t)wave_sum(hi) << 32);
+    if (lane == 0) {
+      if (cnt[0]) atomicAdd(&sc[HPGQ_S_NUM_INPUT], (unsigned long long)cnt[0]);
+      if (cnt[1]) atomicAdd(&sc[HPGQ_S_NUM_PASSED], (unsigned long long)cnt[1]);
+      if (cnt[2]) atomicAdd(&sc[HPGQ_S_NUM_FAILED], (unsigned long long)cnt[2]);
+      if (cnt[4]) atomicAdd(&sc[HPGQ_S_NUM_STATS], (unsigned long long)cnt[4]);
+      if (cnt[5]) atomicAdd(&sc[HPGQ_S_LONG_READS], (unsigned long long)cnt[5]);
+      if (tot) atomicAdd(&sc[HPGQ_S_ACC_MEANQ_FX16], (unsigned long long)tot);
+      if (cnt[6] && A.err) atomicOr(A.err, 1);
+    }
+  }
+  __syncthreads();
+  uint64_t *row = A.slab + (size_t)blockIdx.x * A.clen;
+  const int off_pos = HPGQ_NUM_SCALARS + hlen;
+  for (int i = tid; i < HPGQ_NUM_SCALARS; i += kWG) row[i] += sc[i];
+  for (int i = tid; i < hlen; i += kWG) row[HPGQ_NUM_SCALARS + i] += hist[i];
+  for (int i = tid; i < 6 * lmax; i += kWG) row[off_pos + i] += pos_acc[i];
+}
+
+}  // namespace hpgq

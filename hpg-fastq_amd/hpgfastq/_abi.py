@@ -98,6 +98,7 @@ _SIGS = [
     ("hpgq_reset", C.c_int, [C.c_void_p]),
     ("hpgq_counters_size", C.c_size_t, [C.c_void_p]),
     ("hpgq_read_counters", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
+    ("hpgq_fold", C.c_int, [C.c_void_p]),
     ("hpgq_counters_device", C.c_void_p, [C.c_void_p]),
     ("hpgq_stream", C.c_void_p, [C.c_void_p]),
     ("hpgq_comm_unique_id", C.c_int, [C.c_char_p]),

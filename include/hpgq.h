@@ -219,7 +219,12 @@ size_t hpgq_counters_size(const hpgq_ctx_t *ctx);
 /* Copy the counters to host memory (synchronises the ctx). */
 int  hpgq_read_counters(hpgq_ctx_t *ctx, uint64_t *out, size_t n);
 
-/* Device pointer of the counter buffer (for an external all-reduce). */
+/* Fold the per-workgroup partials into the counter buffer (async on the ctx
+ * stream).  hpgq_read_counters and hpgq_allreduce fold implicitly. */
+int  hpgq_fold(hpgq_ctx_t *ctx);
+
+/* Device pointer of the counter buffer (for an external all-reduce); holds
+ * the totals after hpgq_fold(). */
 uint64_t *hpgq_counters_device(hpgq_ctx_t *ctx);
 
 /* HIP stream (hipStream_t) the ctx runs on. */

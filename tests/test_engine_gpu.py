@@ -47,15 +47,33 @@ STATS_CASES = {
 }
 
 
+@pytest.fixture(params=["auto", "single"])
+def kernel_choice(request, monkeypatch):
+    """Run a test with the default kernel choice and with the one-read-per-wave
+    kernel forced (HPGQ_KERNEL=single), so both FAST kernels meet the oracle."""
+    if request.param == "single":
+        monkeypatch.setenv("HPGQ_KERNEL", "single")
+    else:
+        monkeypatch.delenv("HPGQ_KERNEL", raising=False)
+    return request.param
+
+
 @pytest.mark.parametrize("name", sorted(STATS_CASES))
-def test_stats_filter_synthetic(name):
+def test_stats_filter_synthetic(name, kernel_choice):
     reads = O.synth(20000, seed=2, L=150, trunc_pct=5, n_per_1024=8)
     p = H.stats_params(lmax=150, **STATS_CASES[name])
     c = assert_same(p, reads)
     assert c[H.S_NUM_INPUT] == reads.n
 
 
-def test_filter_only_mask():
+@pytest.mark.parametrize("L,lmax", [(160, 160), (150, 150), (60, 64), (3, 8)])
+def test_tri_kernel_lengths(L, lmax, kernel_choice):
+    reads = O.synth(7001, seed=12, L=L, trunc_pct=40, n_per_1024=30)
+    p = H.stats_params(lmax=lmax, read_quality_range="18,", read_length_range="2,")
+    assert_same(p, reads)
+
+
+def test_filter_only_mask(kernel_choice):
     reads = O.synth(30000, seed=3, L=150, trunc_pct=10)
     p = H.filter_params(lmax=150, read_quality_range="20,", read_length_range="50,")
     assert_same(p, reads)
@@ -121,7 +139,7 @@ def _edge_reads():
 
 
 @pytest.mark.parametrize("name", sorted(STATS_CASES))
-def test_edge_reads(name):
+def test_edge_reads(name, kernel_choice):
     reads = O.Reads.from_pairs(_edge_reads() * 7)
     p = H.stats_params(lmax=150, **STATS_CASES[name])
     assert_same(p, reads)
@@ -155,7 +173,7 @@ def test_read_too_long_reports_error():
         assert ei.value.code == -4
 
 
-def test_accumulates_across_batches_and_offsets():
+def test_accumulates_across_batches_and_offsets(kernel_choice):
     """Counters merge over calls; data_indices need not start at 0."""
     reads = O.synth(12000, seed=10, L=150, trunc_pct=15)
     p = H.stats_params(lmax=150, read_quality_range="20,")
@@ -170,7 +188,7 @@ def test_accumulates_across_batches_and_offsets():
         np.testing.assert_array_equal(e.counters(), c_o)
 
 
-def test_device_path_torch_buffers():
+def test_device_path_torch_buffers(kernel_choice):
     torch = pytest.importorskip("torch")
     reads = O.synth(50000, seed=11, L=150, trunc_pct=5)
     p = H.stats_params(lmax=150, read_quality_range="20,", read_length_range="50,")

@@ -1,0 +1,62 @@
+"""Profiling driver: the C2 engine kernel on one resident 10M-read batch.
+
+Run under rocprofv3 (kernel trace or --pmc passes); no timing of its own.
+  python tools/prof_engine.py [--reads N] [--iters K] [--mode c2|stats|edit|pe]
+"""
+import argparse
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "hpg-fastq_amd"))
+import torch  # noqa: E402  (device buffers; imported before hpgfastq: one HIP runtime)
+import hpgfastq as H  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--reads", type=int, default=10_000_000)
+ap.add_argument("--iters", type=int, default=5)
+ap.add_argument("--mode", default="c2")
+ap.add_argument("--L", type=int, default=150)
+args = ap.parse_args()
+
+dev = torch.device("cuda", 0)
+n, L = args.reads, args.L
+if args.mode == "c2":
+    p = H.stats_params(lmax=L, read_quality_range="20,", read_length_range="50,")
+elif args.mode == "stats":
+    p = H.stats_params(lmax=L)
+elif args.mode == "edit":
+    p = H.edit_params(lmax=L, stats=True, left_length=10, left_quality_range="20,",
+                      right_length=30, right_quality_range="20,")
+else:
+    p = H.stats_params(lmax=L, read_quality_range="20,", read_length_range="50,")
+    p.paired = 1
+nm = 2 if p.paired else 1
+bufs = []
+for m in range(nm):
+    s = H.Synth(2, L, 5, 5, 1, 33, m)
+    idx = np.zeros(n + 1, np.int32)
+    H.check(H.lib.hpgq_synth_indices_host(C.byref(s), 0, n, idx.ctypes.data), "idx")
+    nb = int(idx[-1])
+    sq = torch.empty(nb + 64, dtype=torch.uint8, device=dev)
+    ql = torch.empty(nb + 64, dtype=torch.uint8, device=dev)
+    ix = torch.from_numpy(idx).to(dev)
+    torch.cuda.synchronize()
+    H.check(H.lib.hpgq_synth_device(C.byref(s), 0, n, sq.data_ptr(), ql.data_ptr(),
+                                    ix.data_ptr(), None), "synth")
+    torch.cuda.synchronize()
+    bufs.append((sq, ql, ix))
+mask = torch.empty(n, dtype=torch.uint8, device=dev)
+trim = torch.empty(n * nm, dtype=torch.int32, device=dev)
+eng = H.Engine(p)
+bs = [H.engine.device_batch(n, sq.data_ptr(), ql.data_ptr(), ix.data_ptr()) for sq, ql, ix in bufs]
+for _ in range(args.iters):
+    eng.run_device(bs[0], bs[1] if nm == 2 else None, mask.data_ptr(),
+                   trim.data_ptr() if p.edit_on else None)
+eng.sync()
+c = eng.counters()
+print("reads", n, "passed", int(c[H.S_NUM_PASSED]), "iters", args.iters)
+eng.close()
