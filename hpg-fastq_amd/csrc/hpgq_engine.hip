@@ -121,7 +121,13 @@ static const void *kernel_nch(int nch) {
 }
 
 static const void *kernel_for(int nm, int nch, bool gen, bool tri) {
-  if (tri) return (const void *)hpgq::engine_tri_kernel;
+  if (tri) {
+    const char *w = std::getenv("HPGQ_TRI_WAVES");   // occupancy experiment knob
+    const int mw = w ? std::atoi(w) : 6;
+    if (mw <= 4) return (const void *)hpgq::engine_tri_kernel<4>;
+    if (mw == 5) return (const void *)hpgq::engine_tri_kernel<5>;
+    return (const void *)hpgq::engine_tri_kernel<6>;
+  }
   if (nm == 2) return gen ? kernel_nch<2, true>(nch) : kernel_nch<2, false>(nch);
   return gen ? kernel_nch<1, true>(nch) : kernel_nch<1, false>(nch);
 }

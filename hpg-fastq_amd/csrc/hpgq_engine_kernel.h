@@ -152,13 +152,15 @@ __device__ __forceinline__ uint32_t put_lane(uint32_t v, uint32_t val, int j) {
   return v;
 }
 
-// field shift per base code; code = (byte >> 1) & 7:
-//   'A'->0 'C'->1 'T'->2 'G'->3 pad(0x08)->4 5,6 unused 'N'->7
-// fields: A bits 0-5, C 6-11, G 12-17, T 18-23, N 24-29, bits 30-31 garbage
-constexpr uint32_t kExpLo = 0x47544341u;
-constexpr uint32_t kExpHi = 0x4E000008u;
-constexpr uint32_t kShLo = 0x0C120600u;
-constexpr uint32_t kShHi = 0x181E1E1Eu;
+// field shift per base code; code = byte & 7 is one-to-one on A,C,G,T,N:
+//   pad(0x08)->0 'A'->1 'C'->3 'T'->4 'N'->6 'G'->7, codes 2 and 5 unused
+// fields: A bits 0-5, C 6-11, G 12-17, T 18-23, N 24-29, bits 30-31 garbage.
+// A byte whose code matches but whose value does not (lowercase, IUPAC, ...)
+// fails the `expected byte` check and is sent to the garbage field.
+constexpr uint32_t kExpLo = 0x43004108u;   // expected byte for codes 0..3
+constexpr uint32_t kExpHi = 0x474E0054u;   // codes 4..7
+constexpr uint32_t kShLo = 0x061E001Eu;    // shifts for codes 0..3: 30, 0, 30, 6
+constexpr uint32_t kShHi = 0x0C181E12u;    // codes 4..7: 18, 30, 24, 12
 
 // ---------------------------------------------------------------------------
 // per-mate buffers
@@ -255,7 +257,7 @@ struct PosAcc {
     for (int c = 0; c < NCH; ++c) {
       const uint32_t s = (sw[c] & m[c]) | (0x08080808u & ~m[c]);   // pad -> garbage field
       const uint32_t q = qw[c] & m[c];
-      const uint32_t codes = (s >> 1) & 0x07070707u;
+      const uint32_t codes = s & 0x07070707u;
       uint32_t sh = __builtin_amdgcn_perm(kShHi, kShLo, codes);
       const uint32_t ex = __builtin_amdgcn_perm(kExpHi, kExpLo, codes);
       if (__builtin_expect(s != ex, 0)) {   // bytes that are not exactly A/C/G/T/N

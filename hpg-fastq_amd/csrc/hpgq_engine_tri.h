@@ -27,8 +27,8 @@ namespace hpgq {
 
 constexpr int kTriW = 21;       // lanes per segment
 constexpr int kTriPos = 160;    // positions per segment (20 owning lanes x 8)
-constexpr int kTriBlock = 60;   // reads per block (20 triples)
-constexpr int kTriU = 5;        // triples per pipeline group (4 groups per full block)
+constexpr int kTriBlock = 54;   // reads per block (18 triples)
+constexpr int kTriU = 3;        // triples per pipeline group (6 groups per full block)
 
 typedef unsigned v2u __attribute__((ext_vector_type(2)));
 
@@ -60,6 +60,9 @@ struct TriAcc {
     for (int i = 0; i < 8; ++i) pk[i] = 0;
     q02[0] = q02[1] = q13[0] = q13[1] = 0;
   }
+  // SUB = true takes a read back out (it was added in the same flush window,
+  // so no field underflows)
+  template <bool SUB>
   __device__ __forceinline__ void add_word(int w, uint32_t sw, uint32_t qw, uint32_t m) {
     const uint32_t s = (sw & m) | (0x08080808u & ~m);   // pad -> garbage field
     const uint32_t q = qw & m;
@@ -72,12 +75,21 @@ struct TriAcc {
       const uint32_t ff = (nz >> 7) * 0xFFu;
       sh = (sh & ~ff) | (0x1E1E1E1Eu & ff);
     }
-    pk[4 * w + 0] += 1u << (sh & 31u);
-    pk[4 * w + 1] += 1u << ((sh >> 8) & 31u);
-    pk[4 * w + 2] += 1u << ((sh >> 16) & 31u);
-    pk[4 * w + 3] += 1u << ((sh >> 24) & 31u);
-    q02[w] += q & 0x00FF00FFu;
-    q13[w] += (q >> 8) & 0x00FF00FFu;
+    if (SUB) {
+      pk[4 * w + 0] -= 1u << (sh & 31u);
+      pk[4 * w + 1] -= 1u << ((sh >> 8) & 31u);
+      pk[4 * w + 2] -= 1u << ((sh >> 16) & 31u);
+      pk[4 * w + 3] -= 1u << ((sh >> 24) & 31u);
+      q02[w] -= q & 0x00FF00FFu;
+      q13[w] -= (q >> 8) & 0x00FF00FFu;
+    } else {
+      pk[4 * w + 0] += 1u << (sh & 31u);
+      pk[4 * w + 1] += 1u << ((sh >> 8) & 31u);
+      pk[4 * w + 2] += 1u << ((sh >> 16) & 31u);
+      pk[4 * w + 3] += 1u << ((sh >> 24) & 31u);
+      q02[w] += q & 0x00FF00FFu;
+      q13[w] += (q >> 8) & 0x00FF00FFu;
+    }
   }
   __device__ __forceinline__ void flush(uint32_t *pos_acc, int lmax, int p0) {
 #pragma unroll
@@ -99,7 +111,9 @@ struct TriAcc {
   }
 };
 
-__global__ void __launch_bounds__(kWG) engine_tri_kernel(EngineArgs A) {
+// MINW: minimum waves per SIMD the register allocation must allow (occupancy)
+template <int MINW>
+__global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -112,6 +126,8 @@ __global__ void __launch_bounds__(kWG) engine_tri_kernel(EngineArgs A) {
   const int p0 = owner ? 8 * ls : 0x40000000;   // first position of this lane
   const uint32_t lane8 = 8u * (uint32_t)ls;
   const bool stats = A.flags & F_STATS, filter = A.flags & F_FILTER;
+  // raw-sum bounds: pass iff min_len <= n <= max_len and lo_r*n <= S <= hi_r*n
+  const int lo_r = A.min_q + A.phred, hi_r = A.max_q + A.phred;
 
   // LDS: pos_acc [6][lmax] u32 | hist [hlen] u32 | sc [8] u64
   uint32_t *pos_acc = reinterpret_cast<uint32_t *>(lds);
@@ -125,7 +141,7 @@ __global__ void __launch_bounds__(kWG) engine_tri_kernel(EngineArgs A) {
   const MateBuf mb = make_mate(A.seq[0], A.qual[0], uni(A.idx[0][A.num_reads]));
   TriAcc acc;
   acc.zero();
-  int since_flush = 0;
+  int since_flush = 0;   // triples added since the last flush (a field grows <= 1 per triple)
   uint64_t fx16 = 0;
   uint32_t cnt[7] = {0, 0, 0, 0, 0, 0, 0};   // input, passed, failed, edited, stats, long, any-long
 
@@ -133,7 +149,8 @@ __global__ void __launch_bounds__(kWG) engine_tri_kernel(EngineArgs A) {
   const int64_t gw = (int64_t)blockIdx.x * kWaves + wave;
   const int64_t nw = (int64_t)gridDim.x * kWaves;
 
-  // block prologue: lane j (< 60) describes read r0 + j
+  // block prologue: lane j describes read r0 + j; lanes >= nr get length 0,
+  // so whatever gathers them contributes nothing
   auto load_block = [&](int64_t blk, uint32_t &os, uint32_t &oq, uint32_t &inf) {
     const int64_t r0 = blk * kTriBlock;
     const int nr = (int)min((int64_t)kTriBlock, A.num_reads - r0);
@@ -142,21 +159,39 @@ __global__ void __launch_bounds__(kWG) engine_tri_kernel(EngineArgs A) {
     const uint32_t xs = (uint32_t)(mb.bs + a), xq = (uint32_t)(mb.bq + a);
     os = xs & ~3u;
     oq = xq & ~3u;
-    inf = (uint32_t)(e - a) | ((xs & 3u) << 16) | ((xq & 3u) << 20);
+    inf = (lane < nr ? (uint32_t)(e - a) : 0u) | ((xs & 3u) << 16) | ((xq & 3u) << 20);
+  };
+  // lane -> source lane (in the prologue registers) of its segment's read
+  auto gather = [&](uint32_t os, uint32_t oq, uint32_t inf, int src_lane, TriPending &pd) {
+    const int src = 4 * src_lane;
+    const uint32_t ros = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)os);
+    const uint32_t roq = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)oq);
+    pd.info = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)inf);
+    pd.s = __builtin_amdgcn_raw_buffer_load_b64(mb.rs, ros + lane8, 0, 0);
+    pd.q = __builtin_amdgcn_raw_buffer_load_b64(mb.rq, roq + lane8, 0, 0);
+  };
+  // window-aligned words of a gathered triple
+  auto unpack = [&](const TriPending &pd, uint32_t &s0, uint32_t &s1, uint32_t &q0, uint32_t &q1,
+                    uint32_t &m0, uint32_t &m1) {
+    const int n = (int)(pd.info & 0xFFFFu);
+    const uint32_t als = (pd.info >> 16) & 3u, alq = (pd.info >> 20) & 3u;
+    s0 = __builtin_amdgcn_alignbyte(pd.s.y, pd.s.x, als);
+    s1 = __builtin_amdgcn_alignbyte(next_lane0(pd.s.x), pd.s.y, als);
+    q0 = __builtin_amdgcn_alignbyte(pd.q.y, pd.q.x, alq);
+    q1 = __builtin_amdgcn_alignbyte(next_lane0(pd.q.x), pd.q.y, alq);
+    const int nv = n - p0;
+    m0 = byte_mask(nv);
+    m1 = byte_mask(nv - 4);
   };
 
   TriPending grp[2][kTriU];
-  // issue group g (kTriU triples) of the block described by (os, oq, inf)
+  // issue group g (kTriU triples); triples past the block end gather lane 63
+  // (length 0), so they add nothing
   auto load_group = [&](uint32_t os, uint32_t oq, uint32_t inf, int nt, int g, int slot) {
 #pragma unroll
     for (int u = 0; u < kTriU; ++u) {
-      const int t = min(g * kTriU + u, nt - 1);   // past the block end: reload the last triple
-      const int src = 4 * min(3 * t + seg, 63);
-      const uint32_t ros = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)os);
-      const uint32_t roq = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)oq);
-      grp[slot][u].info = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)inf);
-      grp[slot][u].s = __builtin_amdgcn_raw_buffer_load_b64(mb.rs, ros + lane8, 0, 0);
-      grp[slot][u].q = __builtin_amdgcn_raw_buffer_load_b64(mb.rq, roq + lane8, 0, 0);
+      const int t = g * kTriU + u;
+      gather(os, oq, inf, t < nt ? min(3 * t + seg, 63) : 63, grp[slot][u]);
     }
   };
 
@@ -167,6 +202,7 @@ __global__ void __launch_bounds__(kWG) engine_tri_kernel(EngineArgs A) {
     const int nr0 = (int)min((int64_t)kTriBlock, A.num_reads - blk * kTriBlock);
     load_group(os, oq, inf, (nr0 + 2) / 3, 0, 0);
   }
+  const uint64_t not_seg_first = 0x6DB6DB6DB6DB6DB6ull;   // lanes j with j % 3 != 0
   for (; blk < nblocks; blk += nw) {
     const int64_t r0 = blk * kTriBlock;
     const int nr = (int)min((int64_t)kTriBlock, A.num_reads - r0);
@@ -174,60 +210,34 @@ __global__ void __launch_bounds__(kWG) engine_tri_kernel(EngineArgs A) {
     const int64_t nblk = blk + nw < nblocks ? blk + nw : blk;   // next block (or self)
     const int nnt = ((int)min((int64_t)kTriBlock, A.num_reads - nblk * kTriBlock) + 2) / 3;
     load_block(nblk, osn, oqn, infn);
-    uint32_t res_r1 = 0;        // lane j: raw quality sum | GC << 18 of read r0 + j
-    uint64_t passmask = 0;      // bit j: read r0 + j passed
+    if (stats && since_flush > kFlushEvery - kTriBlock / 3) {   // keep every field <= 63
+      acc.flush(pos_acc, lmax, p0);
+      since_flush = 0;
+    }
+    // lane 3t+k <- inclusive prefix (over the wave) at the end of segment k of
+    // triple t, i.e. sum over segments <= k of (raw quality | G+C << 18)
+    uint32_t ends = 0;
 
     auto process_group = [&](int g, int slot) {
 #pragma unroll
       for (int u = 0; u < kTriU; ++u) {
         const int t = g * kTriU + u;
-        if (t >= nt) break;
-        const TriPending &p = grp[slot][u];
-        const int n = (int)(p.info & 0xFFFFu);
-        const uint32_t als = (p.info >> 16) & 3u, alq = (p.info >> 20) & 3u;
-        const uint32_t s0 = __builtin_amdgcn_alignbyte(p.s.y, p.s.x, als);
-        const uint32_t s1 = __builtin_amdgcn_alignbyte(next_lane0(p.s.x), p.s.y, als);
-        const uint32_t q0 = __builtin_amdgcn_alignbyte(p.q.y, p.q.x, alq);
-        const uint32_t q1 = __builtin_amdgcn_alignbyte(next_lane0(p.q.x), p.q.y, alq);
-        const int nv = n - p0;
-        uint32_t m0 = byte_mask(nv), m1 = byte_mask(nv - 4);
+        uint32_t s0, s1, q0, q1, m0, m1;
+        unpack(grp[slot][u], s0, s1, q0, q1, m0, m1);
         // packed per-lane partial: raw quality | G+C << 18
         uint32_t x = __builtin_amdgcn_sad_u8(q1 & m1, 0u, __builtin_amdgcn_sad_u8(q0 & m0, 0u, 0u));
         const uint32_t g0 = zero_bytes((s0 | 0x04040404u) ^ 0x47474747u) & m0 & 0x80808080u;
         const uint32_t g1 = zero_bytes((s1 | 0x04040404u) ^ 0x47474747u) & m1 & 0x80808080u;
         x += (uint32_t)(__builtin_popcount(g0) + __builtin_popcount(g1)) << 18;
         const uint32_t P = wave_scan(x);
-        const uint32_t P20 = __builtin_amdgcn_readlane(P, 20);
-        const uint32_t P41 = __builtin_amdgcn_readlane(P, 41);
-        const uint32_t P62 = __builtin_amdgcn_readlane(P, 62);
-        const uint32_t T[3] = {P20, P41 - P20, P62 - P41};
-        uint32_t passbits = 0;
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-          const int j = 3 * t + k;
-          if (j < nr) {
-            const int wn = (int)(__builtin_amdgcn_readlane(p.info, kTriW * k) & 0xFFFFu);
-            bool pass = true;
-            if (filter) {
-              const int sq = (int)(T[k] & 0x3FFFFu) - A.phred * wn;
-              pass = (wn >= A.min_len) & (wn <= A.max_len) & (A.min_q * wn <= sq) &
-                     (sq <= A.max_q * wn);
-            }
-            passbits |= (uint32_t)pass << k;
-            res_r1 = put_lane(res_r1, T[k], j);
-          }
-        }
-        passmask |= (uint64_t)passbits << (3 * t);
-        if (stats && passbits) {
-          const uint32_t keep = 0u - ((passbits >> (seg & 3)) & 1u);   // this lane's read passed
-          m0 &= keep;
-          m1 &= keep;
-          acc.add_word(0, s0, q0, m0);
-          acc.add_word(1, s1, q1, m1);
-          if (++since_flush == kFlushEvery) {
-            acc.flush(pos_acc, lmax, p0);
-            since_flush = 0;
-          }
+        // gather the three segment ends into lanes 3t, 3t+1, 3t+2
+        const int k = lane - 3 * t;
+        const uint32_t e = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * (kTriW * k + 20), (int)P);
+        if (t < nt && (unsigned)k < 3u) ends = e;
+        // every read is added; failed ones are subtracted in the block epilogue
+        if (stats) {
+          acc.add_word<false>(0, s0, q0, m0);
+          acc.add_word<false>(1, s1, q1, m1);
         }
       }
     };
@@ -243,22 +253,30 @@ __global__ void __launch_bounds__(kWG) engine_tri_kernel(EngineArgs A) {
         process_group(g + 1, 1);
       }
     }
+    since_flush += nt;
 
     // ---- block epilogue (lane j = read r0 + j) ----------------------------
     const bool valid = lane < nr;
     const int n = (int)(inf & 0xFFFFu);
-    const bool pass = valid && ((passmask >> lane) & 1u);
+    // per-read sums: difference of consecutive segment ends within a triple
+    const uint32_t prev = __builtin_amdgcn_mov_dpp(ends, 0x138, 0xF, 0xF, true);   // lane j-1
+    const uint32_t r1 = ends - (((not_seg_first >> lane) & 1u) ? prev : 0u);
+    const int sraw = (int)(r1 & 0x3FFFFu);
+    bool pass = valid;
+    if (filter)
+      pass = pass && n >= A.min_len && n <= A.max_len && lo_r * n <= sraw && sraw <= hi_r * n;
     const bool lg = valid && n > lmax;
     if (valid && A.mask) A.mask[r0 + lane] = (uint8_t)pass;
+    const uint64_t failed = __ballot(valid && !pass);
     cnt[0] += (uint32_t)nr;
     cnt[1] += (uint32_t)__builtin_popcountll(__ballot(pass));
-    cnt[2] += (uint32_t)__builtin_popcountll(__ballot(valid && !pass));
+    cnt[2] += (uint32_t)__builtin_popcountll(failed);
     cnt[6] += (uint32_t)__builtin_popcountll(__ballot(lg));
     if (stats) {
       cnt[4] += (uint32_t)__builtin_popcountll(__ballot(pass));
       cnt[5] += (uint32_t)__builtin_popcountll(__ballot(pass && lg));
       if (pass && !lg) {
-        const uint32_t s = res_r1 & 0x3FFFFu, gc = res_r1 >> 18, wn = (uint32_t)n;
+        const uint32_t gc = r1 >> 18, wn = (uint32_t)n, s = (uint32_t)sraw;
         atomicAdd(&hist[wn], 1u);
         if (wn > 0) {
           atomicAdd(&hist[lmax + 1 + (2 * s + wn) / (2 * wn)], 1u);
@@ -266,6 +284,20 @@ __global__ void __launch_bounds__(kWG) engine_tri_kernel(EngineArgs A) {
           const uint32_t q = s / wn, rem = s - q * wn;
           fx16 += ((uint64_t)q << 16) + (((uint32_t)rem << 16) / wn);
         }
+      }
+      // take the failed reads back out, a triple at a time (same lanes as the add)
+      uint64_t fl = failed;
+      while (fl) {
+        const int j = (int)__builtin_ctzll(fl);
+        const int t = j / 3;
+        const uint32_t fbits = (uint32_t)(fl >> (3 * t)) & 7u;
+        fl &= ~(7ull << (3 * t));
+        TriPending pd;
+        gather(os, oq, inf, ((fbits >> (seg & 3)) & 1u) ? min(3 * t + seg, 63) : 63, pd);
+        uint32_t s0, s1, q0, q1, m0, m1;
+        unpack(pd, s0, s1, q0, q1, m0, m1);
+        acc.add_word<true>(0, s0, q0, m0);
+        acc.add_word<true>(1, s1, q1, m1);
       }
     }
     os = osn;
