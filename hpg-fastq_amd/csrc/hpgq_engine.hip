@@ -218,6 +218,10 @@ int hpgq_open(hpgq_ctx_t **out, int device, const hpgq_params_t *p) {
     const size_t hist_words = ((size_t)c->nm * hlen + 1) & ~(size_t)1;
     c->lds_bytes = ((size_t)c->nm * 6 * p->lmax + hist_words) * 4 +
                    (size_t)c->nm * HPGQ_NUM_SCALARS * 8 + sizeof(hpgq::ColdParams);
+    // the three-read kernel also keeps per-wave read tables (2 x 1 KB + 256 B)
+    const size_t tri_lds = ((size_t)6 * p->lmax + hist_words) * 4 + HPGQ_NUM_SCALARS * 8 + 16 +
+                           (size_t)hpgq::kWaves * (2 * 256 + 64) * 4;
+    if (tri_lds > c->lds_bytes) c->lds_bytes = tri_lds;
   }
   HPGQ_HIP_TRY(hipSetDevice(device));
   HPGQ_HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));

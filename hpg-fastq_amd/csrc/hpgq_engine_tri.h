@@ -66,7 +66,7 @@ struct TriAcc {
   __device__ __forceinline__ void add_word(int w, uint32_t sw, uint32_t qw, uint32_t m) {
     const uint32_t s = (sw & m) | (0x08080808u & ~m);   // pad -> garbage field
     const uint32_t q = qw & m;
-    const uint32_t codes = (s >> 1) & 0x07070707u;
+    const uint32_t codes = s & 0x07070707u;
     uint32_t sh = __builtin_amdgcn_perm(kShHi, kShLo, codes);
     const uint32_t ex = __builtin_amdgcn_perm(kExpHi, kExpLo, codes);
     if (__builtin_expect(s != ex, 0)) {   // bytes that are not exactly A/C/G/T/N
@@ -129,11 +129,16 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
   // raw-sum bounds: pass iff min_len <= n <= max_len and lo_r*n <= S <= hi_r*n
   const int lo_r = A.min_q + A.phred, hi_r = A.max_q + A.phred;
 
-  // LDS: pos_acc [6][lmax] u32 | hist [hlen] u32 | sc [8] u64
+  // LDS: pos_acc [6][lmax] u32 | hist [hlen] u32 | sc [8] u64 | per-wave tables
   uint32_t *pos_acc = reinterpret_cast<uint32_t *>(lds);
   uint32_t *hist = pos_acc + 6 * lmax;
   const int hist_words = (hlen + 1) & ~1;
   unsigned long long *sc = reinterpret_cast<unsigned long long *>(hist + hist_words);
+  // per wave: two read tables [64][4] u32 (os, oq, info, -) and the segment
+  // ends [64] u32; tables alternate between consecutive blocks
+  const int tab_words = (6 * lmax + hist_words + 2 * HPGQ_NUM_SCALARS + 3) & ~3;   // 16 B aligned
+  uint32_t *wtab = pos_acc + tab_words + wave * (2 * 256 + 64);
+  uint32_t *wends = wtab + 2 * 256;
   for (int i = tid; i < 6 * lmax + hist_words; i += kWG) pos_acc[i] = 0;
   for (int i = tid; i < HPGQ_NUM_SCALARS; i += kWG) sc[i] = 0;
   __syncthreads();
@@ -149,26 +154,29 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
   const int64_t gw = (int64_t)blockIdx.x * kWaves + wave;
   const int64_t nw = (int64_t)gridDim.x * kWaves;
 
-  // block prologue: lane j describes read r0 + j; lanes >= nr get length 0,
-  // so whatever gathers them contributes nothing
-  auto load_block = [&](int64_t blk, uint32_t &os, uint32_t &oq, uint32_t &inf) {
+  // block prologue: lane j describes read r0 + j in read table `tb`; lanes >=
+  // nr get length 0, so whatever gathers them contributes nothing.  Returns
+  // this lane's info word (the epilogue needs the lengths).
+  auto load_block = [&](int64_t blk, int tb) -> uint32_t {
     const int64_t r0 = blk * kTriBlock;
     const int nr = (int)min((int64_t)kTriBlock, A.num_reads - r0);
     const int l = min(lane, nr - 1);
     const int a = A.idx[0][r0 + l], e = A.idx[0][r0 + l + 1];
     const uint32_t xs = (uint32_t)(mb.bs + a), xq = (uint32_t)(mb.bq + a);
-    os = xs & ~3u;
-    oq = xq & ~3u;
-    inf = (lane < nr ? (uint32_t)(e - a) : 0u) | ((xs & 3u) << 16) | ((xq & 3u) << 20);
+    const uint32_t inf = (lane < nr ? (uint32_t)(e - a) : 0u) | ((xs & 3u) << 16) | ((xq & 3u) << 20);
+    typedef unsigned v4u __attribute__((ext_vector_type(4)));
+    v4u rec = {xs & ~3u, xq & ~3u, inf, 0u};
+    *reinterpret_cast<v4u *>(wtab + tb * 256 + 4 * lane) = rec;
+    __builtin_amdgcn_wave_barrier();   // other lanes read it (LDS is in order per wave)
+    return inf;
   };
-  // lane -> source lane (in the prologue registers) of its segment's read
-  auto gather = [&](uint32_t os, uint32_t oq, uint32_t inf, int src_lane, TriPending &pd) {
-    const int src = 4 * src_lane;
-    const uint32_t ros = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)os);
-    const uint32_t roq = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)oq);
-    pd.info = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)inf);
-    pd.s = __builtin_amdgcn_raw_buffer_load_b64(mb.rs, ros + lane8, 0, 0);
-    pd.q = __builtin_amdgcn_raw_buffer_load_b64(mb.rq, roq + lane8, 0, 0);
+  // lane -> its segment's read (entry `src` of read table tb): one ds_read_b128
+  auto gather = [&](int tb, int src, TriPending &pd) {
+    typedef unsigned v4u __attribute__((ext_vector_type(4)));
+    const v4u rec = *reinterpret_cast<const v4u *>(wtab + tb * 256 + 4 * src);
+    pd.info = rec.z;
+    pd.s = __builtin_amdgcn_raw_buffer_load_b64(mb.rs, rec.x + lane8, 0, 0);
+    pd.q = __builtin_amdgcn_raw_buffer_load_b64(mb.rq, rec.y + lane8, 0, 0);
   };
   // window-aligned words of a gathered triple
   auto unpack = [&](const TriPending &pd, uint32_t &s0, uint32_t &s1, uint32_t &q0, uint32_t &q1,
@@ -187,20 +195,21 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
   TriPending grp[2][kTriU];
   // issue group g (kTriU triples); triples past the block end gather lane 63
   // (length 0), so they add nothing
-  auto load_group = [&](uint32_t os, uint32_t oq, uint32_t inf, int nt, int g, int slot) {
+  auto load_group = [&](int tb, int nt, int g, int slot) {
 #pragma unroll
     for (int u = 0; u < kTriU; ++u) {
       const int t = g * kTriU + u;
-      gather(os, oq, inf, t < nt ? min(3 * t + seg, 63) : 63, grp[slot][u]);
+      gather(tb, t < nt ? min(3 * t + seg, 63) : 63, grp[slot][u]);
     }
   };
 
-  uint32_t os, oq, inf, osn, oqn, infn;
+  uint32_t inf = 0, infn = 0;
+  int tb = 0;   // read table of the current block
   int64_t blk = gw;
   if (blk < nblocks) {
-    load_block(blk, os, oq, inf);
+    inf = load_block(blk, tb);
     const int nr0 = (int)min((int64_t)kTriBlock, A.num_reads - blk * kTriBlock);
-    load_group(os, oq, inf, (nr0 + 2) / 3, 0, 0);
+    load_group(tb, (nr0 + 2) / 3, 0, 0);
   }
   const uint64_t not_seg_first = 0x6DB6DB6DB6DB6DB6ull;   // lanes j with j % 3 != 0
   for (; blk < nblocks; blk += nw) {
@@ -209,14 +218,11 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
     const int nt = (nr + 2) / 3;
     const int64_t nblk = blk + nw < nblocks ? blk + nw : blk;   // next block (or self)
     const int nnt = ((int)min((int64_t)kTriBlock, A.num_reads - nblk * kTriBlock) + 2) / 3;
-    load_block(nblk, osn, oqn, infn);
+    infn = load_block(nblk, tb ^ 1);
     if (stats && since_flush > kFlushEvery - kTriBlock / 3) {   // keep every field <= 63
       acc.flush(pos_acc, lmax, p0);
       since_flush = 0;
     }
-    // lane 3t+k <- inclusive prefix (over the wave) at the end of segment k of
-    // triple t, i.e. sum over segments <= k of (raw quality | G+C << 18)
-    uint32_t ends = 0;
 
     auto process_group = [&](int g, int slot) {
 #pragma unroll
@@ -230,10 +236,8 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
         const uint32_t g1 = zero_bytes((s1 | 0x04040404u) ^ 0x47474747u) & m1 & 0x80808080u;
         x += (uint32_t)(__builtin_popcount(g0) + __builtin_popcount(g1)) << 18;
         const uint32_t P = wave_scan(x);
-        // gather the three segment ends into lanes 3t, 3t+1, 3t+2
-        const int k = lane - 3 * t;
-        const uint32_t e = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * (kTriW * k + 20), (int)P);
-        if (t < nt && (unsigned)k < 3u) ends = e;
+        // segment ends (lanes 20, 41, 62) -> wends[3t + seg], no wait needed
+        if (ls == 20 && seg < 3 && t < nt) wends[3 * t + seg] = P;
         // every read is added; failed ones are subtracted in the block epilogue
         if (stats) {
           acc.add_word<false>(0, s0, q0, m0);
@@ -244,12 +248,12 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
 
     const int ngroups = (nt + kTriU - 1) / kTriU;
     for (int g = 0; g < ngroups; g += 2) {
-      if (g + 1 < ngroups) load_group(os, oq, inf, nt, g + 1, 1);
-      else load_group(osn, oqn, infn, nnt, 0, 1);
+      if (g + 1 < ngroups) load_group(tb, nt, g + 1, 1);
+      else load_group(tb ^ 1, nnt, 0, 1);
       process_group(g, 0);
       if (g + 1 < ngroups) {
-        if (g + 2 < ngroups) load_group(os, oq, inf, nt, g + 2, 0);
-        else load_group(osn, oqn, infn, nnt, 0, 0);
+        if (g + 2 < ngroups) load_group(tb, nt, g + 2, 0);
+        else load_group(tb ^ 1, nnt, 0, 0);
         process_group(g + 1, 1);
       }
     }
@@ -259,6 +263,9 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
     const bool valid = lane < nr;
     const int n = (int)(inf & 0xFFFFu);
     // per-read sums: difference of consecutive segment ends within a triple
+    // (wends[3t + k] = inclusive wave prefix at the end of segment k)
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t ends = lane < nr ? wends[lane] : 0u;
     const uint32_t prev = __builtin_amdgcn_mov_dpp(ends, 0x138, 0xF, 0xF, true);   // lane j-1
     const uint32_t r1 = ends - (((not_seg_first >> lane) & 1u) ? prev : 0u);
     const int sraw = (int)(r1 & 0x3FFFFu);
@@ -293,16 +300,15 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
         const uint32_t fbits = (uint32_t)(fl >> (3 * t)) & 7u;
         fl &= ~(7ull << (3 * t));
         TriPending pd;
-        gather(os, oq, inf, ((fbits >> (seg & 3)) & 1u) ? min(3 * t + seg, 63) : 63, pd);
+        gather(tb, ((fbits >> (seg & 3)) & 1u) ? min(3 * t + seg, 63) : 63, pd);
         uint32_t s0, s1, q0, q1, m0, m1;
         unpack(pd, s0, s1, q0, q1, m0, m1);
         acc.add_word<true>(0, s0, q0, m0);
         acc.add_word<true>(1, s1, q1, m1);
       }
     }
-    os = osn;
-    oq = oqn;
     inf = infn;
+    tb ^= 1;
   }
 
   // ---- workgroup epilogue ---------------------------------------------------
