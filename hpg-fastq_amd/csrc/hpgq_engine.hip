@@ -122,11 +122,13 @@ static const void *kernel_nch(int nch) {
 
 static const void *kernel_for(int nm, int nch, bool gen, bool tri) {
   if (tri) {
-    const char *w = std::getenv("HPGQ_TRI_WAVES");   // occupancy experiment knob
-    const int mw = w ? std::atoi(w) : 6;
-    if (mw <= 4) return (const void *)hpgq::engine_tri_kernel<4>;
-    if (mw == 5) return (const void *)hpgq::engine_tri_kernel<5>;
-    return (const void *)hpgq::engine_tri_kernel<6>;
+    const char *w = std::getenv("HPGQ_TRI_WAVES");      // occupancy experiment knob
+    const char *u = std::getenv("HPGQ_TRI_UNALIGNED");  // load-scheme experiment knob
+    const int mw = w ? std::atoi(w) : 5;
+    const bool un = u && std::atoi(u) != 0;
+    if (mw <= 4) return un ? (const void *)hpgq::engine_tri_kernel<4, true> : (const void *)hpgq::engine_tri_kernel<4, false>;
+    if (mw == 5) return un ? (const void *)hpgq::engine_tri_kernel<5, true> : (const void *)hpgq::engine_tri_kernel<5, false>;
+    return un ? (const void *)hpgq::engine_tri_kernel<6, true> : (const void *)hpgq::engine_tri_kernel<6, false>;
   }
   if (nm == 2) return gen ? kernel_nch<2, true>(nch) : kernel_nch<2, false>(nch);
   return gen ? kernel_nch<1, true>(nch) : kernel_nch<1, false>(nch);

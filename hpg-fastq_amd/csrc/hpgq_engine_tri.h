@@ -2,22 +2,34 @@
 //
 // Same contract and outputs as engine_kernel<1, *, false> (hpgq_engine_kernel.h)
 // for batches whose reads are at most 160 bases: the per-read fixed cost (the
-// DPP reduction, the scalar pass/fail decision, bookkeeping) is shared by three
-// reads and lane utilisation goes from 38/64 to 57/64 at 150 bp.
+// DPP reduction, the pass/fail decision, bookkeeping) is shared by three reads
+// and lane utilisation goes from 38/64 to 57/64 at 150 bp.  The kernel is
+// VALU-issue bound (PMC: ~80% VALU busy at 13.9 Greads/s with the previous
+// per-position field scheme), so everything below counts VALU instructions.
 //
-//   * the wave is cut into 3 segments of 21 lanes (lane 63 idle); segment k
-//     works on read 3t + k of the block.  Lane ls < 20 of a segment owns
-//     positions 8ls..8ls+7 (160 per read); lane 20 only donates its first dword
-//     to lane 19.
-//   * each lane fetches its segment's read offsets from the block prologue
-//     registers with ds_bpermute, then ONE buffer_load_dwordx2 per buffer
-//     (SRD bounds check), DPP wave_shl:1 for the neighbour's dword and two
-//     v_alignbyte per buffer realign the 8 bytes.
+//   * the wave is cut into 3 segments of 21 lanes (lanes 20, 41, 62, 63 own no
+//     positions); segment k works on read 3t + k of the block and lane ls < 20
+//     of a segment owns positions 8ls..8ls+7 (160 per read).
+//   * the block prologue writes one 16-byte record per read (seq offset, qual
+//     offset, length) into a per-wave LDS table; each lane fetches its
+//     segment's record with ONE ds_read_b128 and issues ONE unaligned
+//     buffer_load_dwordx2 per buffer at the read's byte offset + 8ls — no
+//     realignment.  The SRDs cover data_end + 8 bytes (the slack the C-ABI
+//     requires of device buffers, include/hpgq.h).
+//   * base classification: code = byte & 7 (one-to-one on A,C,G,T,N; masked
+//     bytes -> 0), then three v_perm_b32 LUTs: the expected byte (exact-match
+//     check; lowercase / IUPAC / other bytes take a rare path and count as
+//     "other"), C|G<<4 and A|T<<4 nibble one-hots.  G+C per read = popcount of
+//     the C|G word.  N is not counted: the workgroup epilogue derives it as
+//     count - A - C - G - T - other, count from the length histogram.
+//   * nibble counters (<= 15 triples) are widened into 8-bit per-base counters
+//     (<= 255 triples) and those flushed to LDS u32 arrays (ds_add); quality
+//     sums are 16-bit pairs.
 //   * per-read sums (raw quality | G+C << 18) use ONE inclusive DPP prefix scan
-//     for the three segments; segment totals are differences of the scan at
-//     lanes 20, 41, 62 (SALU).
-//   * per-position counters as in engine_kernel (6-bit base fields, 16-bit
-//     quality pairs), 8 positions per lane, segment masks from the pass bits.
+//     for the three segments; lanes 20, 41, 62 store the segment ends to LDS
+//     (no wait) and the block epilogue takes differences.
+//   * every read is accumulated; the epilogue decides pass/fail for the block
+//     vectorised over lanes and takes the failed reads back out.
 // The stats layout, histogram rules and workgroup epilogue are identical, so
 // the two kernels are interchangeable (the tests run both against the oracle).
 #pragma once
@@ -29,12 +41,24 @@ constexpr int kTriW = 21;       // lanes per segment
 constexpr int kTriPos = 160;    // positions per segment (20 owning lanes x 8)
 constexpr int kTriBlock = 54;   // reads per block (18 triples)
 constexpr int kTriU = 3;        // triples per pipeline group (6 groups per full block)
+constexpr int kTriSlack = 8;    // readable bytes past the data end the loads may touch
+constexpr int kNibbleEvery = 15;   // 4-bit counters
+constexpr int kByteEvery = 255;    // 8-bit counters
+
+// code = byte & 7: pad(masked)->0 'A'->1 'C'->3 'T'->4 'N'->6 'G'->7
+constexpr uint32_t kX7Lo = 0x43004101u;   // expected byte, codes 0..3 (0x01: no code-0 byte matches)
+constexpr uint32_t kX7Hi = 0x474E0054u;   // codes 4..7
+constexpr uint32_t kCGLo = 0x01000000u;   // C -> 0x01
+constexpr uint32_t kCGHi = 0x10000000u;   // G -> 0x10
+constexpr uint32_t kATLo = 0x00000100u;   // A -> 0x01
+constexpr uint32_t kATHi = 0x00000010u;   // T -> 0x10
 
 typedef unsigned v2u __attribute__((ext_vector_type(2)));
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
 struct TriPending {
-  v2u s, q;        // raw dword pairs
-  uint32_t info;   // this lane's read: n | als << 16 | alq << 20
+  v2u s, q;        // the lane's 8 bytes of seq / quality (raw dwords if aligned loads)
+  uint32_t n;      // its read's length (| als << 16 | alq << 20 if aligned loads)
 };
 
 __device__ __forceinline__ uint32_t next_lane0(uint32_t v) {   // lane i <- lane i+1, lane 63 <- 0
@@ -52,45 +76,44 @@ __device__ __forceinline__ uint32_t wave_scan(uint32_t v) {
   return v;
 }
 
+// masks of the lane's two words: bytes at positions < n (nv = n - p0)
+__device__ __forceinline__ void tri_masks(int nv, uint32_t &m0, uint32_t &m1) {
+  const int e = 32 - 8 * nv;   // right shift of 0x00000000FFFFFFFF giving m0
+  const uint64_t ones = 0xFFFFFFFFull;
+  m0 = (uint32_t)(ones >> min(max(e, 0), 32));
+  m1 = (uint32_t)(ones >> min(max(e + 32, 0), 32));
+}
+
+// 0xFF in every byte of d that is non-zero
+__device__ __forceinline__ uint32_t nonzero_bytes(uint32_t d) {
+  const uint32_t nz = (((d & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | d) & 0x80808080u;
+  return (nz >> 7) * 0xFFu;
+}
+
 struct TriAcc {
-  uint32_t pk[8];           // positions p0..p0+7, 6-bit base fields
-  uint32_t q02[2], q13[2];  // quality 16-bit pairs per dword
+  uint32_t n4[2][2];   // [word][C|G<<4, A|T<<4]: nibble per position
+  uint32_t c8[2][4];   // [word][A, C, G, T]: byte per position
+  uint32_t q02[2], q13[2];   // quality 16-bit pairs (positions 0,2 / 1,3 of the word)
   __device__ __forceinline__ void zero() {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) pk[i] = 0;
-    q02[0] = q02[1] = q13[0] = q13[1] = 0;
-  }
-  // SUB = true takes a read back out (it was added in the same flush window,
-  // so no field underflows)
-  template <bool SUB>
-  __device__ __forceinline__ void add_word(int w, uint32_t sw, uint32_t qw, uint32_t m) {
-    const uint32_t s = (sw & m) | (0x08080808u & ~m);   // pad -> garbage field
-    const uint32_t q = qw & m;
-    const uint32_t codes = s & 0x07070707u;
-    uint32_t sh = __builtin_amdgcn_perm(kShHi, kShLo, codes);
-    const uint32_t ex = __builtin_amdgcn_perm(kExpHi, kExpLo, codes);
-    if (__builtin_expect(s != ex, 0)) {   // bytes that are not exactly A/C/G/T/N
-      const uint32_t d = s ^ ex;
-      const uint32_t nz = (((d & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | d) & 0x80808080u;
-      const uint32_t ff = (nz >> 7) * 0xFFu;
-      sh = (sh & ~ff) | (0x1E1E1E1Eu & ff);
-    }
-    if (SUB) {
-      pk[4 * w + 0] -= 1u << (sh & 31u);
-      pk[4 * w + 1] -= 1u << ((sh >> 8) & 31u);
-      pk[4 * w + 2] -= 1u << ((sh >> 16) & 31u);
-      pk[4 * w + 3] -= 1u << ((sh >> 24) & 31u);
-      q02[w] -= q & 0x00FF00FFu;
-      q13[w] -= (q >> 8) & 0x00FF00FFu;
-    } else {
-      pk[4 * w + 0] += 1u << (sh & 31u);
-      pk[4 * w + 1] += 1u << ((sh >> 8) & 31u);
-      pk[4 * w + 2] += 1u << ((sh >> 16) & 31u);
-      pk[4 * w + 3] += 1u << ((sh >> 24) & 31u);
-      q02[w] += q & 0x00FF00FFu;
-      q13[w] += (q >> 8) & 0x00FF00FFu;
+    for (int w = 0; w < 2; ++w) {
+      n4[w][0] = n4[w][1] = 0;
+      c8[w][0] = c8[w][1] = c8[w][2] = c8[w][3] = 0;
+      q02[w] = q13[w] = 0;
     }
   }
+  // nibbles -> bytes (every <= 15 triples and before any subtraction)
+  __device__ __forceinline__ void widen() {
+#pragma unroll
+    for (int w = 0; w < 2; ++w) {
+      c8[w][1] += n4[w][0] & 0x0F0F0F0Fu;
+      c8[w][2] += (n4[w][0] >> 4) & 0x0F0F0F0Fu;
+      c8[w][0] += n4[w][1] & 0x0F0F0F0Fu;
+      c8[w][3] += (n4[w][1] >> 4) & 0x0F0F0F0Fu;
+      n4[w][0] = n4[w][1] = 0;
+    }
+  }
+  // bytes -> LDS (pos_acc [6][lmax]: qsum, A, C, G, T, N/other); nibbles empty
   __device__ __forceinline__ void flush(uint32_t *pos_acc, int lmax, int p0) {
 #pragma unroll
     for (int w = 0; w < 2; ++w) {
@@ -101,18 +124,49 @@ struct TriAcc {
         if (pos < lmax) {
           atomicAdd(&pos_acc[pos], qv[i]);
 #pragma unroll
-          for (int b = 0; b < 5; ++b)
-            atomicAdd(&pos_acc[(1 + b) * lmax + pos], (pk[4 * w + i] >> (6 * b)) & 63u);
+          for (int b = 0; b < 4; ++b)
+            atomicAdd(&pos_acc[(1 + b) * lmax + pos], (c8[w][b] >> (8 * i)) & 0xFFu);
         }
-        pk[4 * w + i] = 0;
       }
+      c8[w][0] = c8[w][1] = c8[w][2] = c8[w][3] = 0;
       q02[w] = q13[w] = 0;
     }
   }
 };
 
+// codes of a masked word; marks bytes that are not exactly A/C/G/T/N
+__device__ __forceinline__ uint32_t tri_codes(uint32_t s, uint32_t m, uint32_t &bad) {
+  const uint32_t codes = s & m & 0x07070707u;
+  const uint32_t ex = __builtin_amdgcn_perm(kX7Hi, kX7Lo, codes);
+  bad |= (s ^ ex) & m;
+  return codes;
+}
+
+// rare path: bytes that are not exactly A/C/G/T/N get code 0 (counted nowhere)
+// and one "other" count per position (sign: +1 add, -1 subtract)
+__device__ __forceinline__ uint32_t tri_fix(uint32_t s, uint32_t m, uint32_t codes, uint32_t *other,
+                                            int lmax, int pos0, uint32_t sign) {
+  const uint32_t ex = __builtin_amdgcn_perm(kX7Hi, kX7Lo, codes);
+  const uint32_t ff = nonzero_bytes((s ^ ex) & m);
+  if (ff) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (((ff >> (8 * i)) & 1u) && pos0 + i < lmax) atomicAdd(&other[pos0 + i], sign);
+  }
+  return codes & ~ff;
+}
+
+template <bool B>
+struct TriTag {
+  static constexpr bool value = B;
+};
+using AddTag = TriTag<false>;
+using SubTag = TriTag<true>;
+
 // MINW: minimum waves per SIMD the register allocation must allow (occupancy)
-template <int MINW>
+// UNAL: unaligned 8-byte loads at the read's byte offset; else dword-aligned
+// loads realigned with DPP wave_shl:1 + v_alignbyte
+template <int MINW, bool UNAL>
 __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x;
@@ -123,19 +177,21 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
   const int seg = lane / kTriW;                 // 0..2, lane 63 -> 3 (idle)
   const int ls = lane - seg * kTriW;            // 0..20
   const bool owner = seg < 3 && ls < 20;
-  const int p0 = owner ? 8 * ls : 0x40000000;   // first position of this lane
+  const int p0 = owner ? 8 * ls : (1 << 26);   // first position of this lane (8*p0 fits int32)
   const uint32_t lane8 = 8u * (uint32_t)ls;
   const bool stats = A.flags & F_STATS, filter = A.flags & F_FILTER;
   // raw-sum bounds: pass iff min_len <= n <= max_len and lo_r*n <= S <= hi_r*n
   const int lo_r = A.min_q + A.phred, hi_r = A.max_q + A.phred;
 
   // LDS: pos_acc [6][lmax] u32 | hist [hlen] u32 | sc [8] u64 | per-wave tables
+  // (pos_acc row 5 holds "other" counts until the epilogue turns it into N)
   uint32_t *pos_acc = reinterpret_cast<uint32_t *>(lds);
+  uint32_t *other = pos_acc + 5 * lmax;
   uint32_t *hist = pos_acc + 6 * lmax;
   const int hist_words = (hlen + 1) & ~1;
   unsigned long long *sc = reinterpret_cast<unsigned long long *>(hist + hist_words);
-  // per wave: two read tables [64][4] u32 (os, oq, info, -) and the segment
-  // ends [64] u32; tables alternate between consecutive blocks
+  // per wave: two read tables [64] x 16 B (seq offset, qual offset, length, -)
+  // alternating between consecutive blocks, and the segment ends [64] u32
   const int tab_words = (6 * lmax + hist_words + 2 * HPGQ_NUM_SCALARS + 3) & ~3;   // 16 B aligned
   uint32_t *wtab = pos_acc + tab_words + wave * (2 * 256 + 64);
   uint32_t *wends = wtab + 2 * 256;
@@ -143,10 +199,17 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
   for (int i = tid; i < HPGQ_NUM_SCALARS; i += kWG) sc[i] = 0;
   __syncthreads();
 
-  const MateBuf mb = make_mate(A.seq[0], A.qual[0], uni(A.idx[0][A.num_reads]));
+  // SRDs: the read bytes plus the load slack (unaligned 8-byte windows)
+  const int data_end = uni(A.idx[0][A.num_reads]);
+  const uintptr_t ps = reinterpret_cast<uintptr_t>(A.seq[0]), pq = reinterpret_cast<uintptr_t>(A.qual[0]);
+  const int bs = UNAL ? 0 : (int)(ps & 3), bq = UNAL ? 0 : (int)(pq & 3);   // base misalignment
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)(ps - bs), (short)0, bs + data_end + kTriSlack, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)(pq - bq), (short)0, bq + data_end + kTriSlack, 0x00020000);
   TriAcc acc;
   acc.zero();
-  int since_flush = 0;   // triples added since the last flush (a field grows <= 1 per triple)
+  int since_flush = 0;   // triples added since the last LDS flush (a byte grows <= 1 per triple)
   uint64_t fx16 = 0;
   uint32_t cnt[7] = {0, 0, 0, 0, 0, 0, 0};   // input, passed, failed, edited, stats, long, any-long
 
@@ -156,40 +219,27 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
 
   // block prologue: lane j describes read r0 + j in read table `tb`; lanes >=
   // nr get length 0, so whatever gathers them contributes nothing.  Returns
-  // this lane's info word (the epilogue needs the lengths).
+  // this lane's length (the epilogue needs it).
   auto load_block = [&](int64_t blk, int tb) -> uint32_t {
     const int64_t r0 = blk * kTriBlock;
     const int nr = (int)min((int64_t)kTriBlock, A.num_reads - r0);
     const int l = min(lane, nr - 1);
     const int a = A.idx[0][r0 + l], e = A.idx[0][r0 + l + 1];
-    const uint32_t xs = (uint32_t)(mb.bs + a), xq = (uint32_t)(mb.bq + a);
-    const uint32_t inf = (lane < nr ? (uint32_t)(e - a) : 0u) | ((xs & 3u) << 16) | ((xq & 3u) << 20);
-    typedef unsigned v4u __attribute__((ext_vector_type(4)));
-    v4u rec = {xs & ~3u, xq & ~3u, inf, 0u};
+    const uint32_t n = lane < nr ? (uint32_t)(e - a) : 0u;
+    const uint32_t xs = (uint32_t)(bs + a), xq = (uint32_t)(bq + a);
+    v4u rec;
+    if (UNAL) rec = v4u{xs, xq, n, 0u};
+    else rec = v4u{xs & ~3u, xq & ~3u, n | ((xs & 3u) << 16) | ((xq & 3u) << 20), 0u};
     *reinterpret_cast<v4u *>(wtab + tb * 256 + 4 * lane) = rec;
     __builtin_amdgcn_wave_barrier();   // other lanes read it (LDS is in order per wave)
-    return inf;
+    return n;
   };
-  // lane -> its segment's read (entry `src` of read table tb): one ds_read_b128
+  // lane -> its segment's read (entry `src` of read table tb)
   auto gather = [&](int tb, int src, TriPending &pd) {
-    typedef unsigned v4u __attribute__((ext_vector_type(4)));
     const v4u rec = *reinterpret_cast<const v4u *>(wtab + tb * 256 + 4 * src);
-    pd.info = rec.z;
-    pd.s = __builtin_amdgcn_raw_buffer_load_b64(mb.rs, rec.x + lane8, 0, 0);
-    pd.q = __builtin_amdgcn_raw_buffer_load_b64(mb.rq, rec.y + lane8, 0, 0);
-  };
-  // window-aligned words of a gathered triple
-  auto unpack = [&](const TriPending &pd, uint32_t &s0, uint32_t &s1, uint32_t &q0, uint32_t &q1,
-                    uint32_t &m0, uint32_t &m1) {
-    const int n = (int)(pd.info & 0xFFFFu);
-    const uint32_t als = (pd.info >> 16) & 3u, alq = (pd.info >> 20) & 3u;
-    s0 = __builtin_amdgcn_alignbyte(pd.s.y, pd.s.x, als);
-    s1 = __builtin_amdgcn_alignbyte(next_lane0(pd.s.x), pd.s.y, als);
-    q0 = __builtin_amdgcn_alignbyte(pd.q.y, pd.q.x, alq);
-    q1 = __builtin_amdgcn_alignbyte(next_lane0(pd.q.x), pd.q.y, alq);
-    const int nv = n - p0;
-    m0 = byte_mask(nv);
-    m1 = byte_mask(nv - 4);
+    pd.n = rec.z;
+    pd.s = __builtin_amdgcn_raw_buffer_load_b64(rs, rec.x + lane8, 0, 0);
+    pd.q = __builtin_amdgcn_raw_buffer_load_b64(rq, rec.y + lane8, 0, 0);
   };
 
   TriPending grp[2][kTriU];
@@ -203,11 +253,70 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
     }
   };
 
-  uint32_t inf = 0, infn = 0;
+  // one triple: per-lane partial (raw quality | G+C << 18); adds (SUB = false)
+  // or removes (SUB = true) the lane's positions from the counters
+  auto account = [&](const TriPending &pd, bool count, auto sub_tag) -> uint32_t {
+    constexpr bool SUB = decltype(sub_tag)::value;
+    uint32_t s0 = pd.s.x, s1 = pd.s.y, q0 = pd.q.x, q1 = pd.q.y;
+    if (!UNAL) {
+      const uint32_t als = (pd.n >> 16) & 3u, alq = (pd.n >> 20) & 3u;
+      s0 = __builtin_amdgcn_alignbyte(pd.s.y, pd.s.x, als);
+      s1 = __builtin_amdgcn_alignbyte(next_lane0(pd.s.x), pd.s.y, als);
+      q0 = __builtin_amdgcn_alignbyte(pd.q.y, pd.q.x, alq);
+      q1 = __builtin_amdgcn_alignbyte(next_lane0(pd.q.x), pd.q.y, alq);
+    }
+    uint32_t m0, m1;
+    tri_masks((int)(pd.n & 0xFFFFu) - p0, m0, m1);
+    const uint32_t qm0 = q0 & m0, qm1 = q1 & m1;
+    uint32_t bad = 0;
+    uint32_t c0 = tri_codes(s0, m0, bad);
+    uint32_t c1 = tri_codes(s1, m1, bad);
+    if (__builtin_expect(bad != 0, 0)) {
+      const uint32_t sign = SUB ? 0xFFFFFFFFu : 1u;
+      c0 = tri_fix(s0, m0, c0, other, count ? lmax : 0, p0, sign);
+      c1 = tri_fix(s1, m1, c1, other, count ? lmax : 0, p0 + 4, sign);
+    }
+    const uint32_t cg0 = __builtin_amdgcn_perm(kCGHi, kCGLo, c0);
+    const uint32_t cg1 = __builtin_amdgcn_perm(kCGHi, kCGLo, c1);
+    if (count) {
+      const uint32_t at0 = __builtin_amdgcn_perm(kATHi, kATLo, c0);
+      const uint32_t at1 = __builtin_amdgcn_perm(kATHi, kATLo, c1);
+      const uint32_t h0 = __builtin_amdgcn_perm(0u, qm0, 0x0C030C01u);   // bytes 1, 3
+      const uint32_t h1 = __builtin_amdgcn_perm(0u, qm1, 0x0C030C01u);
+      if (SUB) {
+        acc.c8[0][1] -= cg0 & 0x0F0F0F0Fu;
+        acc.c8[0][2] -= (cg0 >> 4) & 0x0F0F0F0Fu;
+        acc.c8[0][0] -= at0 & 0x0F0F0F0Fu;
+        acc.c8[0][3] -= (at0 >> 4) & 0x0F0F0F0Fu;
+        acc.c8[1][1] -= cg1 & 0x0F0F0F0Fu;
+        acc.c8[1][2] -= (cg1 >> 4) & 0x0F0F0F0Fu;
+        acc.c8[1][0] -= at1 & 0x0F0F0F0Fu;
+        acc.c8[1][3] -= (at1 >> 4) & 0x0F0F0F0Fu;
+        acc.q02[0] -= qm0 & 0x00FF00FFu;
+        acc.q13[0] -= h0;
+        acc.q02[1] -= qm1 & 0x00FF00FFu;
+        acc.q13[1] -= h1;
+      } else {
+        acc.n4[0][0] += cg0;
+        acc.n4[0][1] += at0;
+        acc.n4[1][0] += cg1;
+        acc.n4[1][1] += at1;
+        acc.q02[0] += qm0 & 0x00FF00FFu;
+        acc.q13[0] += h0;
+        acc.q02[1] += qm1 & 0x00FF00FFu;
+        acc.q13[1] += h1;
+      }
+    }
+    const uint32_t gc = (uint32_t)__builtin_popcount(cg1) + (uint32_t)__builtin_popcount(cg0);
+    const uint32_t qs = __builtin_amdgcn_sad_u8(qm1, 0u, __builtin_amdgcn_sad_u8(qm0, 0u, 0u));
+    return qs + (gc << 18);
+  };
+
+  uint32_t len = 0, lenn = 0;
   int tb = 0;   // read table of the current block
   int64_t blk = gw;
   if (blk < nblocks) {
-    inf = load_block(blk, tb);
+    len = load_block(blk, tb);
     const int nr0 = (int)min((int64_t)kTriBlock, A.num_reads - blk * kTriBlock);
     load_group(tb, (nr0 + 2) / 3, 0, 0);
   }
@@ -218,8 +327,8 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
     const int nt = (nr + 2) / 3;
     const int64_t nblk = blk + nw < nblocks ? blk + nw : blk;   // next block (or self)
     const int nnt = ((int)min((int64_t)kTriBlock, A.num_reads - nblk * kTriBlock) + 2) / 3;
-    infn = load_block(nblk, tb ^ 1);
-    if (stats && since_flush > kFlushEvery - kTriBlock / 3) {   // keep every field <= 63
+    lenn = load_block(nblk, tb ^ 1);
+    if (stats && since_flush > kByteEvery - kTriBlock / 3) {   // keep every byte <= 255
       acc.flush(pos_acc, lmax, p0);
       since_flush = 0;
     }
@@ -228,21 +337,11 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
 #pragma unroll
       for (int u = 0; u < kTriU; ++u) {
         const int t = g * kTriU + u;
-        uint32_t s0, s1, q0, q1, m0, m1;
-        unpack(grp[slot][u], s0, s1, q0, q1, m0, m1);
-        // packed per-lane partial: raw quality | G+C << 18
-        uint32_t x = __builtin_amdgcn_sad_u8(q1 & m1, 0u, __builtin_amdgcn_sad_u8(q0 & m0, 0u, 0u));
-        const uint32_t g0 = zero_bytes((s0 | 0x04040404u) ^ 0x47474747u) & m0 & 0x80808080u;
-        const uint32_t g1 = zero_bytes((s1 | 0x04040404u) ^ 0x47474747u) & m1 & 0x80808080u;
-        x += (uint32_t)(__builtin_popcount(g0) + __builtin_popcount(g1)) << 18;
+        // every read is added; failed ones are taken out in the block epilogue
+        const uint32_t x = account(grp[slot][u], stats, AddTag{});
         const uint32_t P = wave_scan(x);
         // segment ends (lanes 20, 41, 62) -> wends[3t + seg], no wait needed
         if (ls == 20 && seg < 3 && t < nt) wends[3 * t + seg] = P;
-        // every read is added; failed ones are subtracted in the block epilogue
-        if (stats) {
-          acc.add_word<false>(0, s0, q0, m0);
-          acc.add_word<false>(1, s1, q1, m1);
-        }
       }
     };
 
@@ -256,12 +355,16 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
         else load_group(tb ^ 1, nnt, 0, 0);
         process_group(g + 1, 1);
       }
+      // nibbles hold at most 15 triples: widen after groups 0-3 and at block end
+      static_assert(4 * kTriU <= kNibbleEvery && kTriBlock / 3 - 4 * kTriU <= kNibbleEvery, "");
+      if (stats && g == 2) acc.widen();
     }
+    if (stats) acc.widen();
     since_flush += nt;
 
     // ---- block epilogue (lane j = read r0 + j) ----------------------------
     const bool valid = lane < nr;
-    const int n = (int)(inf & 0xFFFFu);
+    const int n = (int)len;
     // per-read sums: difference of consecutive segment ends within a triple
     // (wends[3t + k] = inclusive wave prefix at the end of segment k)
     __builtin_amdgcn_wave_barrier();
@@ -301,17 +404,15 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
         fl &= ~(7ull << (3 * t));
         TriPending pd;
         gather(tb, ((fbits >> (seg & 3)) & 1u) ? min(3 * t + seg, 63) : 63, pd);
-        uint32_t s0, s1, q0, q1, m0, m1;
-        unpack(pd, s0, s1, q0, q1, m0, m1);
-        acc.add_word<true>(0, s0, q0, m0);
-        acc.add_word<true>(1, s1, q1, m1);
+        (void)account(pd, true, SubTag{});
       }
     }
-    inf = infn;
+    len = lenn;
     tb ^= 1;
   }
 
   // ---- workgroup epilogue ---------------------------------------------------
+  acc.widen();
   acc.flush(pos_acc, lmax, p0);
   {
     const uint32_t lo = (uint32_t)fx16, hi = (uint32_t)(fx16 >> 32);
@@ -326,6 +427,14 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
       if (tot) atomicAdd(&sc[HPGQ_S_ACC_MEANQ_FX16], (unsigned long long)tot);
       if (cnt[6] && A.err) atomicOr(A.err, 1);
     }
+  }
+  __syncthreads();
+  // N at position p = (stats reads longer than p) - A - C - G - T - other
+  for (int p = tid; p < lmax; p += kWG) {
+    uint32_t c = 0;
+    for (int L = p + 1; L <= lmax; ++L) c += hist[L];
+    other[p] = c - pos_acc[lmax + p] - pos_acc[2 * lmax + p] - pos_acc[3 * lmax + p] -
+               pos_acc[4 * lmax + p] - other[p];
   }
   __syncthreads();
   uint64_t *row = A.slab + (size_t)blockIdx.x * A.clen;

@@ -8,6 +8,7 @@ LIB_PATH = os.path.join(os.path.dirname(_HERE), "libhpgq.so")
 
 NO_VALUE, MIN_VALUE, MAX_VALUE = -1, 0, 100000
 LMAX_LIMIT = 1024
+DEVICE_SLACK = 8   # readable bytes past the data end of device seq/quality buffers
 NUM_SCALARS = 8
 (S_NUM_INPUT, S_NUM_PASSED, S_NUM_FAILED, S_NUM_EDITED,
  S_NUM_STATS, S_ACC_MEANQ_FX16, S_LONG_READS) = range(7)

@@ -48,6 +48,10 @@ extern "C" {
 
 /* longest read the per-position counters can hold (dense arrays) */
 #define HPGQ_LMAX_LIMIT 1024
+/* Device sequence / quality buffers must stay readable for this many bytes
+ * past their last read (seq + data_indices[num_reads]): the engine fetches
+ * unaligned 8-byte windows.  The bytes are never used. */
+#define HPGQ_DEVICE_SLACK 8
 
 /* error codes */
 #define HPGQ_OK                  0
@@ -194,7 +198,8 @@ void hpgq_close(hpgq_ctx_t *ctx);
  * passed, 0 otherwise; trim_out[i] = trim_start | trim_end << 16 when edit
  * is on (for pairs: mate 1 in trim_out[i], mate 2 in trim_out[num_reads+i]).
  * Either output may be NULL.  For paired ctxs b2 is mate 2 (same num_reads),
- * else it must be NULL.
+ * else it must be NULL.  seq / quality must be readable HPGQ_DEVICE_SLACK bytes
+ * past the data end (hpgq_run_host pads its own staging copy).
  */
 int  hpgq_run_device(hpgq_ctx_t *ctx, const hpgq_batch_t *b, const hpgq_batch_t *b2,
                      uint8_t *mask_out, uint32_t *trim_out);

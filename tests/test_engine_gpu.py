@@ -193,8 +193,9 @@ def test_device_path_torch_buffers(kernel_choice):
     reads = O.synth(50000, seed=11, L=150, trunc_pct=5)
     p = H.stats_params(lmax=150, read_quality_range="20,", read_length_range="50,")
     dev = torch.device("cuda", 0)
-    seq = torch.from_numpy(reads.seq).to(dev)
-    qual = torch.from_numpy(reads.qual).to(dev)
+    pad = np.zeros(H.DEVICE_SLACK, np.uint8)   # the C-ABI's readable slack
+    seq = torch.from_numpy(np.concatenate([reads.seq, pad])).to(dev)
+    qual = torch.from_numpy(np.concatenate([reads.qual, pad])).to(dev)
     idx = torch.from_numpy(reads.idx).to(dev)
     mask = torch.zeros(reads.n, dtype=torch.uint8, device=dev)
     torch.cuda.synchronize()
