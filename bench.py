@@ -182,11 +182,16 @@ def main():
     achieved = bytes_per_launch / avg_launch_s / 1e9
 
     traffic = None
+    # HBM bytes per launch from the committed PMC passes of the same kernel and
+    # batch (tools/gpu_profile.sh -> tools/profile_report.py); only used when
+    # they were taken on the kernel this run launched
     pmc = os.path.join(ROOT, "profiles", "pmc_engine_c2.json")
     if os.path.exists(pmc):
         try:
-            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
-        except Exception:
+            rec = json.load(open(pmc))
+            if rec.get("kernel") == eng.kernel_name and rec.get("batch_reads") == args.batch_reads:
+                traffic = rec.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
             traffic = None
 
     out = {
@@ -208,7 +213,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic,
-                     "kernel": "hpgq::engine_kernel<1>",
+                     "kernel": eng.kernel_name,
                      "avg_launch_us": round(avg_launch_s * 1e6, 1),
                      "alg_bytes_per_launch": int(bytes_per_launch)},
     }

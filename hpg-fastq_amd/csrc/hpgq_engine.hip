@@ -8,6 +8,7 @@
 // C-ABI
 // ===========================================================================
 
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <rccl/rccl.h>
@@ -21,6 +22,8 @@ struct hpgq_ctx {
   uint64_t *d_counters = nullptr;
   int32_t *d_err = nullptr;
   size_t lds_bytes = 0;
+  char kname[64] = {0};   // the engine kernel instance hpgq_open chose
+  const void *kfn = nullptr;
   int nch = 1;
   bool gen = false;               // generic (edit / N / OOR / left-right) kernel variant
   bool tri = false;               // three-reads-per-wave FAST kernel (SE, lmax <= 160)
@@ -120,16 +123,20 @@ static const void *kernel_nch(int nch) {
   }
 }
 
-static const void *kernel_for(int nm, int nch, bool gen, bool tri) {
+static const void *kernel_for(int nm, int nch, bool gen, bool tri, char *name, size_t cap) {
   if (tri) {
     const char *w = std::getenv("HPGQ_TRI_WAVES");      // occupancy experiment knob
     const char *u = std::getenv("HPGQ_TRI_UNALIGNED");  // load-scheme experiment knob
-    const int mw = w ? std::atoi(w) : 5;
+    int mw = w ? std::atoi(w) : 5;
+    mw = mw <= 4 ? 4 : (mw == 5 ? 5 : 6);
     const bool un = u && std::atoi(u) != 0;
+    std::snprintf(name, cap, "hpgq::engine_tri_kernel<%d, %s>", mw, un ? "true" : "false");
     if (mw <= 4) return un ? (const void *)hpgq::engine_tri_kernel<4, true> : (const void *)hpgq::engine_tri_kernel<4, false>;
     if (mw == 5) return un ? (const void *)hpgq::engine_tri_kernel<5, true> : (const void *)hpgq::engine_tri_kernel<5, false>;
     return un ? (const void *)hpgq::engine_tri_kernel<6, true> : (const void *)hpgq::engine_tri_kernel<6, false>;
   }
+  std::snprintf(name, cap, "hpgq::engine_kernel<%d, %d, %s>", nm, nch == 1 ? 1 : (nch == 2 ? 2 : 5),
+                gen ? "true" : "false");
   if (nm == 2) return gen ? kernel_nch<2, true>(nch) : kernel_nch<2, false>(nch);
   return gen ? kernel_nch<1, true>(nch) : kernel_nch<1, false>(nch);
 }
@@ -176,6 +183,8 @@ const char *hpgq_strerror(int code) {
 }
 
 const char *hpgq_version(void) { return "hpgq 0.1 (gfx950)"; }
+
+const char *hpgq_kernel_name(const hpgq_ctx_t *ctx) { return ctx ? ctx->kname : ""; }
 
 int hpgq_device_count(void) {
   int n = 0;
@@ -233,7 +242,8 @@ int hpgq_open(hpgq_ctx_t **out, int device, const hpgq_params_t *p) {
   HPGQ_HIP_TRY(hipMemsetAsync(c->d_err, 0, sizeof(int32_t), c->stream));
   int cus = 0;
   HPGQ_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-  const void *kfn = kernel_for(c->nm, c->nch, c->gen, c->tri);
+  const void *kfn = kernel_for(c->nm, c->nch, c->gen, c->tri, c->kname, sizeof(c->kname));
+  c->kfn = kfn;
   if (c->lds_bytes > 64 * 1024)
     HPGQ_HIP_TRY(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)c->lds_bytes));
@@ -280,7 +290,7 @@ static int launch(hpgq_ctx *c, hpgq::EngineArgs &A) {
   const int64_t need = (nblocks + hpgq::kWaves - 1) / hpgq::kWaves;
   const int grid = (int)std::min<int64_t>(need, c->grid);
   void *args[] = {&A};
-  HPGQ_HIP_TRY(hipLaunchKernel(kernel_for(c->nm, c->nch, c->gen, c->tri), dim3(grid), dim3(hpgq::kWG), args,
+  HPGQ_HIP_TRY(hipLaunchKernel(c->kfn, dim3(grid), dim3(hpgq::kWG), args,
                                c->lds_bytes, c->stream));
   c->dirty = true;
   return HPGQ_OK;

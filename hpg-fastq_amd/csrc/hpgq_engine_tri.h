@@ -5,17 +5,19 @@
 // DPP reduction, the pass/fail decision, bookkeeping) is shared by three reads
 // and lane utilisation goes from 38/64 to 57/64 at 150 bp.  The kernel is
 // VALU-issue bound (PMC: ~80% VALU busy at 13.9 Greads/s with the previous
-// per-position field scheme), so everything below counts VALU instructions.
+// per-position field scheme), so everything below counts VALU instructions
+// (15.3 Greads/s with this one at 5 waves/SIMD).
 //
 //   * the wave is cut into 3 segments of 21 lanes (lanes 20, 41, 62, 63 own no
 //     positions); segment k works on read 3t + k of the block and lane ls < 20
 //     of a segment owns positions 8ls..8ls+7 (160 per read).
-//   * the block prologue writes one 16-byte record per read (seq offset, qual
-//     offset, length) into a per-wave LDS table; each lane fetches its
-//     segment's record with ONE ds_read_b128 and issues ONE unaligned
-//     buffer_load_dwordx2 per buffer at the read's byte offset + 8ls — no
-//     realignment.  The SRDs cover data_end + 8 bytes (the slack the C-ABI
-//     requires of device buffers, include/hpgq.h).
+//   * the block prologue writes one 16-byte record per read (dword-aligned seq
+//     and qual offsets, length | alignments) into a per-wave LDS table; each
+//     lane fetches its segment's record with ONE ds_read_b128, issues ONE
+//     buffer_load_dwordx2 per buffer and realigns with DPP wave_shl:1 +
+//     v_alignbyte (UNAL = true loads unaligned windows instead: fewer VALU,
+//     but measured ~15% slower in the address/data path).  The SRDs cover
+//     data_end + 8 bytes (the slack the C-ABI requires of device buffers).
 //   * base classification: code = byte & 7 (one-to-one on A,C,G,T,N; masked
 //     bytes -> 0), then three v_perm_b32 LUTs: the expected byte (exact-match
 //     check; lowercase / IUPAC / other bytes take a rare path and count as

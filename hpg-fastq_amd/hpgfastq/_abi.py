@@ -120,6 +120,7 @@ _SIGS = [
     ("hpgq_device_count", C.c_int, []),
     ("hpgq_strerror", C.c_char_p, [C.c_int]),
     ("hpgq_version", C.c_char_p, []),
+    ("hpgq_kernel_name", C.c_char_p, [C.c_void_p]),
 ]
 
 

@@ -61,6 +61,11 @@ class Engine:
     def stream(self):
         return lib.hpgq_stream(self._h)
 
+    @property
+    def kernel_name(self):
+        """The engine kernel instance this ctx launches."""
+        return lib.hpgq_kernel_name(self._h).decode()
+
     def run_host(self, batch, batch2=None, mask=None, trim=None):
         """Host numpy batch; mask/trim are numpy outputs valid after sync()."""
         check(lib.hpgq_run_host(self._h, C.byref(batch), C.byref(batch2) if batch2 else None,

@@ -307,6 +307,8 @@ int  hpgq_device_count(void);
 
 const char *hpgq_strerror(int code);
 const char *hpgq_version(void);
+/* the engine kernel instance a ctx runs (for profiles / bench reports) */
+const char *hpgq_kernel_name(const hpgq_ctx_t *ctx);
 
 #ifdef __cplusplus
 }
