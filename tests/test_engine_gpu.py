@@ -225,3 +225,48 @@ def test_synth_device_matches_oracle_generator():
     torch.cuda.synchronize()
     np.testing.assert_array_equal(seq.cpu().numpy(), ref.seq)
     np.testing.assert_array_equal(qual.cpu().numpy(), ref.qual)
+
+
+# ---- golden vectors: hand-derived KATs and the committed synthetic vectors ----
+def _gold():
+    import os
+    return os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.mark.parametrize("section", ["stats", "filter", "edit"])
+def test_kat_gpu(section, kernel_choice):
+    import json
+    import os
+    from fastq_io import read_fastq, check_partial
+    kat = json.load(open(os.path.join(_gold(), "kat_expected.json")))
+    reads = read_fastq(os.path.join(_gold(), kat["reads"]))
+    lmax = kat["lmax"]
+    if section == "stats":
+        p = H.stats_params(lmax=lmax)
+    elif section == "filter":
+        p = H.stats_params(lmax=lmax, **kat["filter"]["flags"])
+    else:
+        p = H.edit_params(lmax=lmax, stats=True, **kat["edit"]["flags"])
+    mask, trim, ctr = gpu_host_path(p, reads)
+    exp = kat[section]
+    check_partial(ctr, exp, lmax, H.layout(lmax))
+    if "mask" in exp:
+        np.testing.assert_array_equal(mask, exp["mask"])
+    if "trim" in exp:
+        np.testing.assert_array_equal(trim, exp["trim"])
+
+
+@pytest.mark.parametrize("name", ["synth_c2_filter.npz", "synth_c4_edit.npz", "synth_c3_pe.npz",
+                                  "synth_filter_all_250.npz"])
+def test_committed_vectors_gpu(name, kernel_choice):
+    import json
+    import os
+    z = np.load(os.path.join(_gold(), name))
+    p = H.params_default(**json.loads(str(z["params"])))
+    r1 = O.Reads(z["seq"], z["qual"], z["idx"])
+    r2 = O.Reads(z["seq2"], z["qual2"], z["idx2"]) if p.paired else None
+    mask, trim, ctr = gpu_host_path(p, r1, r2)
+    np.testing.assert_array_equal(mask, z["mask"])
+    np.testing.assert_array_equal(ctr, z["counters"])
+    if p.edit_on:
+        np.testing.assert_array_equal(trim, z["trim"])
