@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""bench.py — hpg-fastq hot path on MI355X: stats+filter Mreads/s.
+"""bench.py — hpg-fastq hot path on MI355X.
 
-Workload (BASELINE.json configs[1]): `hpg-fastq stats
+Default workload (BASELINE.json configs[1]): `hpg-fastq stats
 --read-quality-range 20, --read-length-range 50,` over 100 M synthetic 150 bp
 single-end reads PER GPU, resident in HBM (10 batches of 10 M reads, the
 reference's fastq_batch_t layout).  One step = reset counters + the fused
@@ -9,10 +9,16 @@ edit->filter->stats kernel over every batch (+ one RCCL all-reduce of the
 packed counters when N > 1).  Reads shard by index across ranks with no
 data-path collective: weak scaling.
 
-  python bench.py [--gpus N --steps K --warmup W]
+Other configs (--config; parity cases of BASELINE.json, reported in DESIGN.md,
+not the driver's line):
+  c3  paired-end 2x150, pair-consistent filter, 100 M pairs per GPU
+  c4  edit (5'/3' Q20 trim) + stats, 500 M x 150 over 8 GPUs = 62.5 M per GPU
+  c5  chaos game k=7, 200 M x 250 over 8 GPUs = 25 M per GPU
+
+  python bench.py [--gpus N --steps K --warmup W] [--config c2|c3|c4|c5]
   python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 
-Prints ONE JSON line (rank 0) with `roofline` (engine kernel, HIP events on
+Prints ONE JSON line (rank 0) with `roofline` (the hot kernel, HIP events on
 the engine's own stream) and `cpu_baseline` (oracle/liboracle.so, C+OpenMP,
 timed on this host's cores on a bounded sample, rank 0 at N=1 only).
 """
@@ -30,9 +36,24 @@ sys.path.insert(0, os.path.join(ROOT, "hpg-fastq_amd"))
 
 import hpgfastq as H  # noqa: E402
 
-METRIC = "Mreads/s (150 bp) stats+filter at 1/2/4/8 MI355X; achieved HBM GB/s vs peak"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
-FILTER_FLAGS = dict(read_quality_range="20,", read_length_range="50,")
+
+CONFIGS = {
+    "c2": dict(metric="Mreads/s (150 bp) stats+filter at 1/2/4/8 MI355X; achieved HBM GB/s vs peak",
+               unit="Mreads/s", reads=100_000_000, batch=10_000_000, L=150, seed=2,
+               workload="C2: stats+filter --read-quality-range 20, --read-length-range 50,"),
+    "c3": dict(metric="Mpairs/s (2x150 bp) paired-end stats+filter, pair-consistent",
+               unit="Mpairs/s", reads=100_000_000, batch=10_000_000, L=150, seed=3,
+               workload="C3: PE 2x150 stats+filter --read-quality-range 20, "
+                        "--read-length-range 50, (pair passes iff both mates pass)"),
+    "c4": dict(metric="Mreads/s (150 bp) edit Q20 trim + stats",
+               unit="Mreads/s", reads=62_500_000, batch=12_500_000, L=150, seed=4,
+               workload="C4: edit --left-length 10 --left-quality-range 20, --right-length 30 "
+                        "--right-quality-range 20, + stats (500 M reads over 8 GPUs)"),
+    "c5": dict(metric="Mreads/s (250 bp) chaos game k=7 tables",
+               unit="Mreads/s", reads=25_000_000, batch=5_000_000, L=250, seed=5,
+               workload="C5: chaos game k=7 feature tables (200 M x 250 bp over 8 GPUs)"),
+}
 
 
 def parse():
@@ -40,52 +61,122 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--reads", type=int, default=100_000_000, help="reads per GPU")
-    ap.add_argument("--batch-reads", type=int, default=10_000_000)
-    ap.add_argument("--read-length", type=int, default=150)
-    ap.add_argument("--seed", type=int, default=2)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--reads", type=int, default=None, help="reads (pairs) per GPU")
+    ap.add_argument("--batch-reads", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    return ap.parse_args()
+    a = ap.parse_args()
+    cfg = CONFIGS[a.config]
+    a.reads = a.reads or cfg["reads"]
+    a.batch_reads = a.batch_reads or cfg["batch"]
+    a.read_length, a.seed = cfg["L"], cfg["seed"]
+    return a
 
 
+def params_for(cfg, L):
+    if cfg == "c4":
+        return H.edit_params(lmax=L, stats=True, left_length=10, left_quality_range="20,",
+                             right_length=30, right_quality_range="20,")
+    p = H.stats_params(lmax=L, read_quality_range="20,", read_length_range="50,")
+    if cfg == "c3":
+        p.paired = 1
+    return p
+
+
+# ---- CPU baseline: the oracle (C + OpenMP) on a bounded sample --------------
 def cpu_baseline(args, params):
-    """Oracle (C + OpenMP) on a bounded sample of the same workload."""
     lib = C.CDLL(os.path.join(ROOT, "oracle", "liboracle.so"))
     lib.oracle_run.restype = C.c_int
     lib.oracle_run.argtypes = [C.POINTER(H.Params), C.POINTER(H.Batch), C.POINTER(H.Batch),
                                C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
     lib.oracle_synth.argtypes = [C.POINTER(H.Synth), C.c_int64, C.c_int64, C.c_void_p,
                                  C.c_void_p, C.c_void_p]
+    lib.oracle_cgr_fill_batches.restype = C.c_int
+    lib.oracle_cgr_fill_batches.argtypes = [C.c_int, C.c_int, C.POINTER(H.Batch), C.c_int,
+                                            C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
     ncores = len(os.sched_getaffinity(0))
     threads = max(1, min(16, ncores))
-    n = 2_000_000
-    s = H.Synth(args.seed, args.read_length, 5, 5, 1, 33, 0)
-    idx = np.zeros(n + 1, np.int32)
-    seq = np.zeros(n * args.read_length, np.uint8)
-    qual = np.zeros(n * args.read_length, np.uint8)
-    lib.oracle_synth(C.byref(s), 0, n, seq.ctypes.data, qual.ctypes.data, idx.ctypes.data)
-    b = H.Batch(n, seq.ctypes.data, qual.ctypes.data, idx.ctypes.data)
-    mask = np.zeros(n, np.uint8)
-    ctr = np.zeros(H.counters_len(params.lmax), np.uint64)
+    L = args.read_length
+    n = 2_000_000 if args.config != "c5" else 400_000
+    mates = 2 if args.config == "c3" else 1
+    bufs = []
+    for m in range(mates):
+        s = H.Synth(args.seed, L, 5, 5, 1, 33, m)
+        idx = np.zeros(n + 1, np.int32)
+        seq = np.zeros(n * L, np.uint8)
+        qual = np.zeros(n * L, np.uint8)
+        lib.oracle_synth(C.byref(s), 0, n, seq.ctypes.data, qual.ctypes.data, idx.ctypes.data)
+        bufs.append((seq, qual, idx))
+    bs = [H.Batch(n, sq.ctypes.data, ql.ctypes.data, ix.ctypes.data) for sq, ql, ix in bufs]
+    if args.config == "c5":
+        # independent fill calls (one per batch of 20 k reads) spread over the threads
+        nb = 20
+        per = n // nb
+        sub = (H.Batch * nb)()
+        sq, ql, ix = bufs[0]
+        for i in range(nb):
+            sub[i] = H.Batch(per, sq.ctypes.data, ql.ctypes.data, ix[i * per:].ctypes.data)
+        ts = np.zeros(128 * 128, np.uint32)
+        tq = np.zeros(128 * 128, np.uint32)
+        wc = np.zeros(1, np.uint32)
+        run = lambda: lib.oracle_cgr_fill_batches(7, 33, sub, nb, ts.ctypes.data,  # noqa: E731
+                                                  tq.ctypes.data, wc.ctypes.data, threads)
+        what = f"oracle_cgr_fill_batches (old/chaos_game.c restated), {nb} fill calls"
+    else:
+        mask = np.zeros(n, np.uint8)
+        trim = np.zeros(n * mates, np.uint32)
+        ctr = np.zeros(H.counters_len(params.lmax) * mates, np.uint64)
+        run = lambda: lib.oracle_run(C.byref(params), C.byref(bs[0]),  # noqa: E731
+                                     C.byref(bs[1]) if mates == 2 else None, mask.ctypes.data,
+                                     trim.ctypes.data, ctr.ctypes.data, threads)
+        what = "oracle_run (hpgq_oracle.c)"
     done, t0 = 0, time.perf_counter()
     while True:
-        rc = lib.oracle_run(C.byref(params), C.byref(b), None, mask.ctypes.data, None,
-                            ctr.ctypes.data, threads)
-        assert rc == 0
+        assert run() == 0
         done += n
         el = time.perf_counter() - t0
         if el >= args.cpu_seconds:
             break
-    return {"value": round(done / el / 1e6, 3), "unit": "Mreads/s", "cores": threads,
-            "kind": "port",
-            "sample": f"{n} synthetic {args.read_length} bp reads (seed {args.seed}, same "
-                      f"generator and filter), {done // n} passes in {el:.1f} s; "
-                      f"oracle/hpgq_oracle.c -O3 OpenMP, {threads} threads of {ncores} visible"}
+    return {"value": round(done / el / 1e6, 3), "unit": CONFIGS[args.config]["unit"],
+            "cores": threads, "kind": "port",
+            "sample": f"{n} synthetic {L} bp {'pairs' if mates == 2 else 'reads'} (seed "
+                      f"{args.seed}, same generator and options), {done // n} passes in "
+                      f"{el:.1f} s; {what} -O3 OpenMP, {threads} threads of {ncores} visible"}
+
+
+# ---- resident synthetic shard ----------------------------------------------
+def make_batches(args, rank, dev, mates):
+    import torch
+    L = args.read_length
+    out = []   # per batch: (n, [(seq, qual, idx) per mate], alg bytes)
+    first = rank * args.reads
+    for lo in range(0, args.reads, args.batch_reads):
+        n = min(args.batch_reads, args.reads - lo)
+        per_mate = []
+        nbytes = 0
+        for m in range(mates):
+            s = H.Synth(args.seed, L, 5, 5, 1, 33, m)
+            idx = np.zeros(n + 1, np.int32)
+            H.check(H.lib.hpgq_synth_indices_host(C.byref(s), first + lo, n, idx.ctypes.data),
+                    "idx")
+            nb = int(idx[-1])
+            d_seq = torch.empty(nb + 64, dtype=torch.uint8, device=dev)
+            d_qual = torch.empty(nb + 64, dtype=torch.uint8, device=dev)
+            d_idx = torch.from_numpy(idx).to(dev)
+            torch.cuda.synchronize()
+            H.check(H.lib.hpgq_synth_device(C.byref(s), first + lo, n, d_seq.data_ptr(),
+                                            d_qual.data_ptr(), d_idx.data_ptr(), None), "synth")
+            torch.cuda.synchronize()
+            per_mate.append((d_seq, d_qual, d_idx))
+            nbytes += 2 * nb + 4 * (n + 1)   # seq + quality + 4-byte offsets
+        out.append((n, per_mate, nbytes))
+    return out
 
 
 def main():
     args = parse()
+    cfg = CONFIGS[args.config]
     import torch
     import torch.distributed as dist
 
@@ -98,54 +189,58 @@ def main():
     dev = torch.device("cuda", local)
 
     L = args.read_length
-    params = H.stats_params(lmax=L, **FILTER_FLAGS)
-    eng = H.Engine(params, device=local)
-    if world > 1:
-        uid = H.engine.comm_unique_id() if rank == 0 else b"\0" * 128
-        obj = [uid]
-        dist.broadcast_object_list(obj, src=0)
-        eng.comm_init(world, rank, obj[0])
-
-    # ---- resident synthetic shard: reads [rank*R, (rank+1)*R) -------------
-    stream_ptr = eng.stream
-    ext = torch.cuda.ExternalStream(stream_ptr, device=dev)
-    batches = []
-    total_bytes_alg = 0
-    first = rank * args.reads
-    s = H.Synth(args.seed, L, 5, 5, 1, 33, 0)
-    for lo in range(0, args.reads, args.batch_reads):
-        n = min(args.batch_reads, args.reads - lo)
-        idx = np.zeros(n + 1, np.int32)
-        H.check(H.lib.hpgq_synth_indices_host(C.byref(s), first + lo, n, idx.ctypes.data), "idx")
-        nb = int(idx[-1])
-        d_seq = torch.empty(nb + 64, dtype=torch.uint8, device=dev)
-        d_qual = torch.empty(nb + 64, dtype=torch.uint8, device=dev)
-        d_idx = torch.from_numpy(idx).to(dev)
-        torch.cuda.synchronize()
-        H.check(H.lib.hpgq_synth_device(C.byref(s), first + lo, n, d_seq.data_ptr(),
-                                        d_qual.data_ptr(), d_idx.data_ptr(), None), "synth")
-        torch.cuda.synchronize()
-        batches.append((n, d_seq, d_qual, d_idx))
-        # algorithmic bytes: seq + quality + 4-byte offset per read, 1-byte mask out
-        total_bytes_alg += 2 * nb + 4 * (n + 1) + n
+    cgr = args.config == "c5"
+    params = params_for(args.config, L)
+    mates = 2 if params.paired else 1
+    batches = make_batches(args, rank, dev, mates)
     d_mask = torch.empty(args.reads, dtype=torch.uint8, device=dev)
-    hb = [H.engine.device_batch(n, sq.data_ptr(), ql.data_ptr(), ix.data_ptr())
-          for (n, sq, ql, ix) in batches]
-    offs = np.cumsum([0] + [n for (n, *_r) in batches])
+    d_trim = torch.empty(args.reads * mates, dtype=torch.int32, device=dev)
+    offs = np.cumsum([0] + [b[0] for b in batches])
 
+    if cgr:
+        eng = H.ChaosGame(7, 33, device=local)
+        kernel_name = "hpgq::cgr::cgr_fill_kernel<7> (+check, fix)"
+        # algorithmic bytes per read: seq + quality + offset (tables stay in LDS)
+        alg = [nb for (_n, _m, nb) in batches]
+        red = torch.zeros(2 * 128 * 128 + 1, dtype=torch.int64, device=dev) if world > 1 else None
+    else:
+        eng = H.Engine(params, device=local)
+        kernel_name = eng.kernel_name
+        if world > 1:
+            uid = H.engine.comm_unique_id() if rank == 0 else b"\0" * 128
+            obj = [uid]
+            dist.broadcast_object_list(obj, src=0)
+            eng.comm_init(world, rank, obj[0])
+        # + 1 B mask per read (pair), + 4 B trim per read when editing
+        alg = [nb + n + (4 * n * mates if params.edit_on else 0) for (n, _m, nb) in batches]
+    ext = torch.cuda.ExternalStream(eng.stream, device=dev)
+    hb = [[H.engine.device_batch(n, sq.data_ptr(), ql.data_ptr(), ix.data_ptr())
+           for (sq, ql, ix) in mm] for (n, mm, _nb) in batches]
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in batches]
 
-    def step(timed_events):
+    def step(timed):
         eng.reset()
         for i, b in enumerate(hb):
-            if timed_events:
+            if timed:
                 ev[i][0].record(ext)
-            eng.run_device(b, None, d_mask.data_ptr() + int(offs[i]), None)
-            if timed_events:
+            if cgr:
+                eng.fill_device(b[0])
+            else:
+                eng.run_device(b[0], b[1] if mates == 2 else None,
+                               d_mask.data_ptr() + int(offs[i]),
+                               d_trim.data_ptr() + 4 * int(offs[i]) if params.edit_on else None)
+            if timed:
                 ev[i][1].record(ext)
         if world > 1:
-            eng.allreduce()
+            if cgr:   # the one exchange step: sum the tables (RCCL via torch.distributed)
+                ts, tq, wc = eng.tables()
+                red.copy_(torch.from_numpy(np.concatenate(
+                    [ts.reshape(-1).astype(np.int64), tq.reshape(-1).astype(np.int64),
+                     np.array([wc], np.int64)])))
+                dist.all_reduce(red)
+            else:
+                eng.allreduce()
 
     for _ in range(args.warmup):
         step(False)
@@ -170,34 +265,35 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t.item())
 
-    # correctness sanity: every read accounted for in the final counters
-    ctr = eng.counters()
-    expect = args.reads * (world if world > 1 else 1)
-    assert int(ctr[H.S_NUM_INPUT]) == expect, (int(ctr[H.S_NUM_INPUT]), expect)
+    # sanity: every read accounted for
+    if cgr:
+        _ts, _tq, wc = eng.tables()
+        assert wc > 0
+    else:
+        ctr = eng.counters()
+        expect = args.reads * (world if world > 1 else 1)
+        assert int(ctr[H.S_NUM_INPUT]) == expect, (int(ctr[H.S_NUM_INPUT]), expect)
 
-    total_reads = args.reads * world * args.steps
-    value = total_reads / el / 1e6
+    total = args.reads * world * args.steps
+    value = total / el / 1e6
     avg_launch_s = float(np.mean(kern_ms)) / 1e3
-    bytes_per_launch = total_bytes_alg / len(batches)
+    bytes_per_launch = float(np.mean(alg))
     achieved = bytes_per_launch / avg_launch_s / 1e9
 
     traffic = None
-    # HBM bytes per launch from the committed PMC passes of the same kernel and
-    # batch (tools/gpu_profile.sh -> tools/profile_report.py); only used when
-    # they were taken on the kernel this run launched
-    pmc = os.path.join(ROOT, "profiles", "pmc_engine_c2.json")
+    pmc = os.path.join(ROOT, "profiles", f"pmc_engine_{args.config}.json")
     if os.path.exists(pmc):
         try:
             rec = json.load(open(pmc))
-            if rec.get("kernel") == eng.kernel_name and rec.get("batch_reads") == args.batch_reads:
+            if rec.get("kernel") == kernel_name and rec.get("batch_reads") == args.batch_reads:
                 traffic = rec.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
 
     out = {
-        "metric": METRIC,
+        "metric": cfg["metric"],
         "value": round(value, 2),
-        "unit": "Mreads/s",
+        "unit": cfg["unit"],
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
@@ -205,15 +301,14 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u8",
+        "dtype": "f64" if cgr else "u8",
         "data": "synthetic (counter-based generator, resident in HBM)",
-        "config": {"workload": "C2: stats+filter --read-quality-range 20, --read-length-range 50,",
-                   "reads_per_gpu": args.reads, "read_length": L, "batch_reads": args.batch_reads,
+        "config": {"workload": cfg["workload"], "reads_per_gpu": args.reads, "read_length": L,
+                   "batch_reads": args.batch_reads,
                    "parallelism": f"read-sharded x{world}, RCCL all-reduce of counters"},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic,
-                     "kernel": eng.kernel_name,
+                     "traffic": traffic, "kernel": kernel_name,
                      "avg_launch_us": round(avg_launch_s * 1e6, 1),
                      "alg_bytes_per_launch": int(bytes_per_launch)},
     }

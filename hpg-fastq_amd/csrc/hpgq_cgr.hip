@@ -40,7 +40,7 @@ namespace hpgq {
 namespace cgr {
 
 constexpr double kEps = 0.00001;   // old/chaos_game.h:41
-constexpr int kWG = 256;
+constexpr int kWG = 1024;       // 16 waves share one set of LDS tables (128 KB at k = 7)
 constexpr int kWarm = 128;         // bytes of context replayed to guess a read's entry state
 constexpr int kLdsMaxK = 7;        // 2 x 4^7 x 4 B = 128 KB of LDS tables
 
