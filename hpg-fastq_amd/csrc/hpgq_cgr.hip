@@ -89,87 +89,170 @@ struct State {
   double fx, fy;
 };
 
-// One base of chaos_game_fill_tables (:197-260).  FULL adds the word to the
-// tables (sign = 1 adds, 0xFFFFFFFF takes it back out); !FULL only advances
-// f, the word counter and the boundary clamp (context replay).
-template <int K, bool FULL>
-__device__ __forceinline__ void step(uint32_t sb, uint32_t qb, uint32_t qold, State &st, int &cnt,
+// Byte classes (exact byte match, as the reference's switch, :197-233), kept
+// in a 256-entry LDS table: bit0 moves f (A/C/G/T), bit1 x half (A/T), bit2
+// y half (G/T), bit3 'N'.  Every other byte — and the zero bytes the loads
+// mask in past a read's end — is class 0, an exact no-op of `step`.
+constexpr uint32_t F_MV = 1, F_BX = 2, F_BY = 4, F_N = 8;
+// the same classes in registers, 4 bytes at a time: code = byte & 7 is
+// one-to-one on A(1) C(3) T(4) N(6) G(7); v_perm_b32 looks up the class and
+// the expected byte per code, and bytes that are not exactly that byte
+// (lowercase, IUPAC, anything else) get class 0
+constexpr uint32_t kClsLo = 0x01000300u;   // codes 0..3: -, A, -, C
+constexpr uint32_t kClsHi = 0x05080007u;   // codes 4..7: T, -, N, G
+constexpr uint32_t kExLo = 0x43004101u;    // expected byte per code (code 0: 0x01 never matches)
+constexpr uint32_t kExHi = 0x474E0054u;
+
+__device__ __forceinline__ uint32_t classes4(uint32_t w) {
+  const uint32_t code = w & 0x07070707u;
+  const uint32_t d = w ^ __builtin_amdgcn_perm(kExHi, kExLo, code);
+  const uint32_t nz = (((d & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | d) & 0x80808080u;   // inexact bytes
+  return __builtin_amdgcn_perm(kClsHi, kClsLo, code) & ~((nz >> 7) * 0xFFu);
+}
+
+__device__ __forceinline__ void fill_classes(uint8_t *cls, int tid, int nthreads) {
+  for (int i = tid; i < 256; i += nthreads) {
+    uint32_t f = 0;
+    if (i == 'A') f = F_MV | F_BX;
+    if (i == 'C') f = F_MV;
+    if (i == 'G') f = F_MV | F_BY;
+    if (i == 'T') f = F_MV | F_BX | F_BY;
+    if (i == 'N') f = F_N;
+    cls[i] = (uint8_t)f;
+  }
+}
+
+// One base of chaos_game_fill_tables (:197-260), branch-free.  FULL adds the
+// word to the tables (sign = 1 adds, 0xFFFFFFFF takes it back out); !FULL only
+// advances f, the word counter and the boundary clamp (context replay).
+// UNCOND: the tables have a spare row + cell, so the add is issued for every
+// base (adding 0 when no word completes) instead of under a divergent branch.
+template <int K, bool FULL, bool UNCOND>
+__device__ __forceinline__ void step(uint32_t fl, uint32_t qb, uint32_t qold, State &st, int &cnt,
                                      uint32_t &acc, uint32_t *ts, uint32_t *tq, uint32_t sign,
                                      uint32_t sub, uint32_t &words) {
   constexpr int dim = 1 << K;
-  const bool isA = sb == 65u, isC = sb == 67u, isG = sb == 71u, isT = sb == 84u;
-  if (sb == 78u) {   // 'N' (:229-233)
-    cnt = 0;
-    acc = 0;
-  }
-  if (isA | isC | isG | isT) {
-    const bool bx = isA | isT, by = isG | isT;
-    st.fx = bx ? st.fx + (((double)dim - st.fx) * 0.5) : st.fx * 0.5;
-    st.fy = by ? st.fy + (((double)dim - st.fy) * 0.5) : st.fy * 0.5;
-    ++cnt;
-    if (FULL) acc += qb;
-  }
-  if (cnt == K) {   // :236-260
-    int cx = (int)st.fx, cy = (int)st.fy;
-    if (cx == dim) {
+  const bool mv = fl & F_MV, bx = fl & F_BX, by = fl & F_BY, isN = fl & F_N;
+  const double hx = st.fx * 0.5, hy = st.fy * 0.5;
+  // f + (dim - f) * 0.5 with the product exact: one fma rounds identically
+  const double gx = __builtin_fma((double)dim - st.fx, 0.5, st.fx);
+  const double gy = __builtin_fma((double)dim - st.fy, 0.5, st.fy);
+  // keep both candidates computed unconditionally (else hipcc sinks them under
+  // an exec-mask branch per base, which costs more than the arithmetic)
+  asm volatile("" ::"v"(hx), "v"(gx), "v"(hy), "v"(gy));
+  st.fx = mv ? (bx ? gx : hx) : st.fx;
+  st.fy = mv ? (by ? gy : hy) : st.fy;
+  cnt = isN ? 0 : cnt + (mv ? 1 : 0);
+  if (FULL) acc = isN ? 0u : acc + (mv ? qb : 0u);
+  const bool word = cnt == K;
+  int cx = (int)st.fx, cy = (int)st.fy;
+  // boundary clamp (:241-251): f == dim only after ~50 A/T (x) or G/T (y) in a row
+  if (__builtin_expect(__ballot(word && (cx == dim || cy == dim)) != 0, 0)) {
+    if (word && cx == dim) {
       cx = dim - 1;
       st.fx = st.fx - kEps;
     }
-    if (cy == dim) {
+    if (word && cy == dim) {
       cy = dim - 1;
       st.fy = st.fy - kEps;
     }
-    --cnt;
-    if (FULL) {
-      const int cell = cx * dim + cy;
+  }
+  cnt -= word ? 1 : 0;
+  if (FULL) {
+    const int cell = cx * dim + cy;   // <= dim*dim + dim only when !word (spare cells)
+    if (UNCOND) {
+      atomicAdd(&ts[cell], word ? sign : 0u);
+      atomicAdd(&tq[cell], word ? sign * (acc - sub) : 0u);
+    } else if (word) {
       atomicAdd(&ts[cell], sign);
       atomicAdd(&tq[cell], sign * (acc - sub));
-      ++words;
-      acc -= qold;   // quality[quality_position - word_size] (:259), raw position
     }
+    words += word ? 1u : 0u;
+    acc -= word ? qold : 0u;   // quality[quality_position - word_size] (:259), raw position
   }
 }
 
 // word counter at byte p of a read: moving bases since the last reset
-// (read start or 'N'), capped at K-1 (a completed word drops it to K-1)
+// (read start or 'N'), capped at K-1 (a completed word drops it to K-1).
+// The 16 bytes before p are scanned in registers; only when they hold fewer
+// than K-1 A/C/G/T and no 'N' (other bytes in between) does it walk further.
 template <int K>
-__device__ int count_before(const char *seq, int a, int p) {
+__device__ int count_before(const Args &A, const Src &S, const uint8_t *cls, int a, int p) {
+  const int lo = p >= 16 ? p - 16 : 0;
+  const v2u w0 = __builtin_amdgcn_raw_buffer_load_b64(S.rs, (uint32_t)(a + lo), 0, 0);
+  const v2u w1 = __builtin_amdgcn_raw_buffer_load_b64(S.rs, (uint32_t)(a + lo + 8), 0, 0);
+  const v2u c0 = {classes4(w0.x), classes4(w0.y)}, c1 = {classes4(w1.x), classes4(w1.y)};
   int m = 0;
-  for (int i = p - 1; i >= 0 && m < K - 1; --i) {
-    const char c = seq[a + i];
-    if (c == 'N') break;
-    if (c == 'A' || c == 'C' || c == 'G' || c == 'T') ++m;
+  bool alive = true;
+#pragma unroll
+  for (int i = 15; i >= 0; --i) {
+    const int pos = lo + i;
+    const uint32_t f = i >= 8 ? byte_of(c1, i - 8) : byte_of(c0, i);
+    const bool in = pos < p;
+    alive = alive && !(in && (f & F_N));
+    m += (alive && in && (f & F_MV)) ? 1 : 0;
+  }
+  if (m >= K - 1) return K - 1;
+  if (!alive || lo == 0) return m;
+  for (int i = lo - 1; i >= 0 && m < K - 1; --i) {   // rare: other bytes in the window
+    const uint32_t f = cls[(uint8_t)A.seq[a + i]];
+    if (f & F_N) break;
+    if (f & F_MV) ++m;
   }
   return m;
 }
 
-// Run read r from byte p0 (word counter cnt0) with state st.
-template <int K, bool FULL>
-__device__ void run_read(const Args &A, const Src &S, int64_t r, int p0, int cnt0, State &st,
+// One 8-byte chunk of a read at byte c (< n).  h1/h2: the two previous
+// quality chunks (for quality[qpos - K]), rotated here.
+template <int K, bool FULL, bool UNCOND>
+__device__ __forceinline__ void run_chunk(v2u sv, v2u qv, v2u &h1, v2u &h2, int left, State &st,
+                                          int &cnt, uint32_t &acc, uint32_t *ts, uint32_t *tq,
+                                          uint32_t sign, uint32_t sub, uint32_t &words) {
+  // bytes past the read end -> 0 (class 0: no-op); left <= 0 masks all
+  const uint64_t m = left >= 8 ? ~0ull : ((1ull << (8 * max(left, 0))) - 1);
+  sv.x &= (uint32_t)m;
+  sv.y &= (uint32_t)(m >> 32);
+  const v2u cl = {classes4(sv.x), classes4(sv.y)};
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    uint32_t qold = 0;
+    if (FULL) {
+      const int o = u + 1 - K;   // raw byte j+1-K relative to this chunk
+      qold = o >= 0 ? sbyte_of(qv, o) : (o >= -8 ? sbyte_of(h1, o + 8) : sbyte_of(h2, o + 16));
+    }
+    step<K, FULL, UNCOND>(byte_of(cl, u), FULL ? sbyte_of(qv, u) : 0u, qold, st, cnt, acc, ts, tq,
+                          sign, sub, words);
+  }
+  if (FULL) {
+    h2 = h1;
+    h1 = qv;
+  }
+}
+
+// Run read [a, a+n) from byte p0 (word counter cnt0) with state st.  The
+// next two chunks' loads are issued before a chunk is processed; each buffer
+// register is reloaded right after its chunk is consumed.
+template <int K, bool FULL, bool UNCOND>
+__device__ void run_read(const Args &A, const Src &S, int a, int n, int p0, int cnt0, State &st,
                          uint32_t *ts, uint32_t *tq, uint32_t sign, uint32_t &words) {
-  const int a = A.idx[r], n = A.idx[r + 1] - a;
   const uint32_t sub = A.base_quality * (uint32_t)K;
   int cnt = cnt0;
   uint32_t acc = 0;
-  v2u q1 = {0u, 0u}, q2 = {0u, 0u};   // the two previous quality chunks
-  for (int c = p0; c < n; c += 8) {
-    const v2u sv = __builtin_amdgcn_raw_buffer_load_b64(S.rs, (uint32_t)(a + c), 0, 0);
-    v2u qv = {0u, 0u};
-    if (FULL) qv = __builtin_amdgcn_raw_buffer_load_b64(S.rq, (uint32_t)(a + c), 0, 0);
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      if (c + u < n) {
-        uint32_t qold = 0;
-        if (FULL) {
-          const int o = u + 1 - K;   // raw byte j+1-K relative to this chunk
-          qold = o >= 0 ? sbyte_of(qv, o) : (o >= -8 ? sbyte_of(q1, o + 8) : sbyte_of(q2, o + 16));
-        }
-        step<K, FULL>(byte_of(sv, u), FULL ? sbyte_of(qv, u) : 0u, qold, st, cnt, acc, ts, tq, sign,
-                      sub, words);
-      }
-    }
-    q2 = q1;
-    q1 = qv;
+  const v2u z = {0u, 0u};
+  v2u h1 = z, h2 = z;
+  auto ld_s = [&](int c) { return __builtin_amdgcn_raw_buffer_load_b64(S.rs, (uint32_t)(a + c), 0, 0); };
+  auto ld_q = [&](int c) {
+    return FULL ? __builtin_amdgcn_raw_buffer_load_b64(S.rq, (uint32_t)(a + c), 0, 0) : z;
+  };
+  v2u sA = ld_s(p0), qA = ld_q(p0), sB = ld_s(p0 + 8), qB = ld_q(p0 + 8);
+  // one exit (a second chunk past the end is all class 0)
+  for (int c = p0; c < n; c += 16) {
+    run_chunk<K, FULL, UNCOND>(sA, qA, h1, h2, n - c, st, cnt, acc, ts, tq, sign, sub, words);
+    sA = ld_s(c + 16);
+    qA = ld_q(c + 16);
+    run_chunk<K, FULL, UNCOND>(sB, qB, h1, h2, n - c - 8, st, cnt, acc, ts, tq, sign, sub, words);
+    sB = ld_s(c + 24);
+    qB = ld_q(c + 24);
   }
 }
 
@@ -177,22 +260,33 @@ __device__ void run_read(const Args &A, const Src &S, int64_t r, int p0, int cnt
 // before it from the fixed start state; exact when the context reaches the
 // batch start
 template <int K>
-__device__ State guess_entry(const Args &A, const Src &S, int64_t r) {
+__device__ State guess_entry(const Args &A, const Src &S, const uint8_t *cls, int64_t r) {
   constexpr double half = (double)(1 << K) * 0.5;   // :107-108
   State st = {half, half};
-  int need = kWarm;
-  int64_t t = r;
-  int p = 0;
-  while (need > 0 && t > 0) {
-    --t;
-    if (!valid_read(A, t)) continue;
-    const int L = A.idx[t + 1] - A.idx[t];
-    if (L >= need) {
-      p = L - need;
-      need = 0;
-    } else {
-      need -= L;
-      p = 0;
+  if (r == 0) return st;
+  // common case: the previous read alone holds kWarm bytes
+  const int ap = A.idx[r - 1], ar = A.idx[r];
+  int64_t t;
+  int p, need;
+  if (ar - ap >= kWarm && valid_read(A, r - 1)) {
+    t = r - 1;
+    p = ar - ap - kWarm;
+    need = 0;
+  } else {
+    need = kWarm;
+    t = r;
+    p = 0;
+    while (need > 0 && t > 0) {
+      --t;
+      if (!valid_read(A, t)) continue;
+      const int L = A.idx[t + 1] - A.idx[t];
+      if (L >= need) {
+        p = L - need;
+        need = 0;
+      } else {
+        need -= L;
+        p = 0;
+      }
     }
   }
   if (need > 0) {   // context reaches the batch start: replay it all, exactly
@@ -202,8 +296,9 @@ __device__ State guess_entry(const Args &A, const Src &S, int64_t r) {
   uint32_t w = 0;
   for (; t < r; ++t) {
     if (!valid_read(A, t)) continue;
-    const int cnt0 = p > 0 ? count_before<K>(A.seq, A.idx[t], p) : 0;
-    run_read<K, false>(A, S, t, p, cnt0, st, nullptr, nullptr, 0u, w);
+    const int a = A.idx[t], n = A.idx[t + 1] - a;
+    const int cnt0 = p > 0 ? count_before<K>(A, S, cls, a, p) : 0;
+    run_read<K, false, false>(A, S, a, n, p, cnt0, st, nullptr, nullptr, 0u, w);
     p = 0;
   }
   return st;
@@ -213,20 +308,25 @@ template <int K>
 __global__ void __launch_bounds__(kWG) cgr_fill_kernel(Args A) {
   constexpr int dim = 1 << K;
   constexpr bool kLds = K <= kLdsMaxK;
+  constexpr int cells = dim * dim + dim + 1;   // + the spare row/cell of the unconditional adds
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  __shared__ uint8_t cls[256];
   uint32_t *ts = kLds ? lds : A.ts;
-  uint32_t *tq = kLds ? lds + dim * dim : A.tq;
-  if (kLds) {
-    for (int i = threadIdx.x; i < 2 * dim * dim; i += kWG) lds[i] = 0;
-    __syncthreads();
-  }
+  uint32_t *tq = kLds ? lds + cells : A.tq;
+  if (kLds)
+    for (int i = threadIdx.x; i < 2 * cells; i += kWG) lds[i] = 0;
+  fill_classes(cls, threadIdx.x, kWG);
+  __syncthreads();
   const Src S = make_src(A);
   uint32_t words = 0;
   const int64_t stride = (int64_t)gridDim.x * kWG;
   for (int64_t r = (int64_t)blockIdx.x * kWG + threadIdx.x; r < A.num_reads; r += stride) {
-    State st = guess_entry<K>(A, S, r);
+    State st = guess_entry<K>(A, S, cls, r);
     A.g[r] = make_double2(st.fx, st.fy);
-    if (valid_read(A, r)) run_read<K, true>(A, S, r, 0, 0, st, ts, tq, 1u, words);
+    if (valid_read(A, r)) {
+      const int a = A.idx[r];
+      run_read<K, true, kLds>(A, S, a, A.idx[r + 1] - a, 0, 0, st, ts, tq, 1u, words);
+    }
     A.e[r] = make_double2(st.fx, st.fy);
   }
   // fq_word_count: wave sum, one atomic per wave
@@ -237,7 +337,7 @@ __global__ void __launch_bounds__(kWG) cgr_fill_kernel(Args A) {
     __syncthreads();
     for (int i = threadIdx.x; i < dim * dim; i += kWG) {
       if (lds[i]) atomicAdd(&A.ts[i], lds[i]);
-      if (lds[dim * dim + i]) atomicAdd(&A.tq[i], lds[dim * dim + i]);
+      if (lds[cells + i]) atomicAdd(&A.tq[i], lds[cells + i]);
     }
   }
 }
@@ -262,6 +362,9 @@ __global__ void __launch_bounds__(256) cgr_check_kernel(Args A) {
 // one lane: replay flagged reads in order with their true entry states
 template <int K>
 __global__ void __launch_bounds__(64) cgr_fix_kernel(Args A) {
+  __shared__ uint8_t cls[256];
+  fill_classes(cls, threadIdx.x, 64);
+  __syncthreads();
   if (threadIdx.x != 0) return;
   const Src S = make_src(A);
   const int64_t nw = (A.num_reads + 63) >> 6;
@@ -284,10 +387,13 @@ __global__ void __launch_bounds__(64) cgr_fix_kernel(Args A) {
           if (valid_read(A, r)) {
             const double2 g = A.g[r];
             State s1 = {g.x, g.y};
-            run_read<K, true>(A, S, r, 0, 0, s1, A.ts, A.tq, 0xFFFFFFFFu, dummy);   // undo
+            run_read<K, true, false>(A, S, A.idx[r], A.idx[r + 1] - A.idx[r], 0, 0, s1,
+                                     A.ts, A.tq, 0xFFFFFFFFu, dummy);   // undo
           }
           State s2 = {entry.x, entry.y};
-          if (valid_read(A, r)) run_read<K, true>(A, S, r, 0, 0, s2, A.ts, A.tq, 1u, dummy);
+          if (valid_read(A, r))
+            run_read<K, true, false>(A, S, A.idx[r], A.idx[r + 1] - A.idx[r], 0, 0, s2,
+                                     A.ts, A.tq, 1u, dummy);
           const double2 ex = make_double2(s2.fx, s2.fy);
           A.e[r] = ex;
           ++replays;
@@ -405,7 +511,7 @@ int hpgq_cgr_open(hpgq_cgr_t **cg, int device, int k, int base_quality) {
   HPGQ_HIP_TRY(hipMemsetAsync(c->d_tq, 0, cells * 4, c->stream));
   HPGQ_HIP_TRY(hipMemsetAsync(c->d_words, 0, 8, c->stream));
   HPGQ_HIP_TRY(hipMemsetAsync(c->d_replays, 0, 8, c->stream));
-  c->lds = k <= hpgq::cgr::kLdsMaxK ? 2 * cells * 4 : 0;
+  c->lds = k <= hpgq::cgr::kLdsMaxK ? 2 * (cells + c->dim + 1) * 4 : 0;
   const void *kfn = hpgq::cgr::fill_for(k);
   if (c->lds > 64 * 1024)
     HPGQ_HIP_TRY(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds));

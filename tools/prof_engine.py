@@ -24,6 +24,26 @@ args = ap.parse_args()
 
 dev = torch.device("cuda", 0)
 n, L = args.reads, args.L
+if args.mode == "cgr":
+    s = H.Synth(5, L, 5, 5, 1, 33, 0)
+    idx = np.zeros(n + 1, np.int32)
+    H.check(H.lib.hpgq_synth_indices_host(C.byref(s), 0, n, idx.ctypes.data), "idx")
+    nb = int(idx[-1])
+    sq = torch.empty(nb + 64, dtype=torch.uint8, device=dev)
+    ql = torch.empty(nb + 64, dtype=torch.uint8, device=dev)
+    ix = torch.from_numpy(idx).to(dev)
+    torch.cuda.synchronize()
+    H.check(H.lib.hpgq_synth_device(C.byref(s), 0, n, sq.data_ptr(), ql.data_ptr(),
+                                    ix.data_ptr(), None), "synth")
+    torch.cuda.synchronize()
+    cg = H.ChaosGame(7)
+    b = H.engine.device_batch(n, sq.data_ptr(), ql.data_ptr(), ix.data_ptr())
+    for _ in range(args.iters):
+        cg.fill_device(b)
+    cg.sync()
+    print("cgr reads", n, "replays", cg.last_replays(), "words", cg.tables()[2])
+    cg.close()
+    sys.exit(0)
 if args.mode == "c2":
     p = H.stats_params(lmax=L, read_quality_range="20,", read_length_range="50,")
 elif args.mode == "stats":
