@@ -178,6 +178,7 @@ const char *hpgq_strerror(int code) {
     case HPGQ_E_NO_DEVICE: return "no HIP device";
     case HPGQ_E_RCCL: return "RCCL error";
     case HPGQ_E_STATE: return "invalid ctx state";
+    case HPGQ_E_FORMAT: return "malformed FASTQ text";
     default: return "unknown error";
   }
 }

@@ -17,7 +17,7 @@ CGR_ALL_READS, CGR_ONLY_VALID_READS = 0, 1
 
 ERRORS = {0: "ok", -1: "invalid argument", -2: "HIP runtime error", -3: "out of memory",
           -4: "read longer than lmax", -5: "no HIP device", -6: "RCCL error",
-          -7: "invalid ctx state"}
+          -7: "invalid ctx state", -8: "malformed FASTQ text"}
 
 
 class HpgqError(RuntimeError):
@@ -117,6 +117,13 @@ _SIGS = [
     ("hpgq_synth_indices_host", C.c_int, [C.POINTER(Synth), C.c_int64, C.c_int64, C.c_void_p]),
     ("hpgq_synth_device", C.c_int, [C.POINTER(Synth), C.c_int64, C.c_int64, C.c_void_p,
                                     C.c_void_p, C.c_void_p, C.c_void_p]),
+    ("hpgq_fastq_complete_prefix", C.c_int64, [C.c_char_p, C.c_int64, C.c_int]),
+    ("hpgq_parser_open", C.c_int, [C.POINTER(C.c_void_p), C.c_int, C.c_void_p]),
+    ("hpgq_parser_close", None, [C.c_void_p]),
+    ("hpgq_parse_host", C.c_int, [C.c_void_p, C.c_char_p, C.c_int64, C.POINTER(Batch)]),
+    ("hpgq_parse_device", C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(Batch)]),
+    ("hpgq_parse_records", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    ("hpgq_parser_stream", C.c_void_p, [C.c_void_p]),
     ("hpgq_device_count", C.c_int, []),
     ("hpgq_strerror", C.c_char_p, [C.c_int]),
     ("hpgq_version", C.c_char_p, []),

@@ -166,3 +166,50 @@ class ChaosGame:
         wc = np.zeros(1, dtype=np.uint32)
         check(lib.hpgq_cgr_read(self._h, _ptr(ts), _ptr(tq), _ptr(wc)), "hpgq_cgr_read")
         return ts.reshape(self.dim, self.dim), tq.reshape(self.dim, self.dim), int(wc[0])
+
+
+def complete_prefix(buf, at_eof=False):
+    """hpgq_fastq_complete_prefix: bytes of `buf` holding whole FASTQ records."""
+    return int(lib.hpgq_fastq_complete_prefix(buf, len(buf), 1 if at_eof else 0))
+
+
+class Parser:
+    """hpgq_parser: FASTQ text -> device batch (parsing half of fastq_fread_se,
+    src/stats_fastq.c:183, on the GPU)."""
+
+    def __init__(self, device=0, stream=None):
+        h = C.c_void_p()
+        check(lib.hpgq_parser_open(C.byref(h), device, stream), "hpgq_parser_open")
+        self._h = h
+        self.num_reads = 0
+
+    def close(self):
+        if self._h:
+            lib.hpgq_parser_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def parse(self, text):
+        """Host bytes (whole records) -> device Batch (valid until the next parse)."""
+        b = Batch()
+        check(lib.hpgq_parse_host(self._h, text, len(text), C.byref(b)), "hpgq_parse_host")
+        self.num_reads = int(b.num_reads)
+        return b
+
+    def records(self):
+        n = self.num_reads
+        out = {k: np.zeros(n, np.uint32) for k in ("start", "seq", "plus", "qual")}
+        check(lib.hpgq_parse_records(self._h, _ptr(out["start"]), _ptr(out["seq"]),
+                                     _ptr(out["plus"]), _ptr(out["qual"])), "hpgq_parse_records")
+        return out

@@ -62,6 +62,7 @@ extern "C" {
 #define HPGQ_E_NO_DEVICE       (-5)   /* no HIP device                        */
 #define HPGQ_E_RCCL            (-6)   /* RCCL communicator / collective error */
 #define HPGQ_E_STATE           (-7)   /* call not valid in this ctx state     */
+#define HPGQ_E_FORMAT          (-8)   /* malformed FASTQ text                 */
 
 /* ---------------------------------------------------------------------- */
 /* batch                                                                  */
@@ -278,6 +279,38 @@ int  hpgq_cgr_read(hpgq_cgr_t *cg, uint32_t *table_seq, uint32_t *table_q, uint3
 void *hpgq_cgr_stream(hpgq_cgr_t *cg);
 /* reads the last fill call had to replay sequentially (diagnostic) */
 int64_t hpgq_cgr_last_replays(hpgq_cgr_t *cg);
+
+/* ---------------------------------------------------------------------- */
+/* FASTQ text -> device batch (the parsing half of the producer's          */
+/* fastq_fread_se, src/stats_fastq.c:183, moved onto the GPU)              */
+/* ---------------------------------------------------------------------- */
+
+/*
+ * Records are 4 lines: "@header", sequence, "+[header]", quality (as long as
+ * the sequence); "\n" or "\r\n" line ends.  A parse unit is whole records,
+ * the last one ending in a newline.
+ */
+typedef struct hpgq_parser hpgq_parser_t;
+
+/* Bytes of buf[0, n) that form whole records; the rest starts the next unit.
+ * at_eof: the data ends at n (returns n; the caller appends a final newline
+ * when the file lacks one).  0: no complete record yet.  Host-only. */
+int64_t hpgq_fastq_complete_prefix(const char *buf, int64_t n, int at_eof);
+
+/* stream: the stream to parse on (e.g. hpgq_stream(ctx), so the engine runs
+ * after it), or NULL for a stream of its own */
+int  hpgq_parser_open(hpgq_parser_t **ps, int device, void *stream);
+void hpgq_parser_close(hpgq_parser_t *ps);
+/* Parse text[0, n) (n < 2^31) into a device batch owned by the parser, valid
+ * until its next parse; `out` gets device pointers and num_reads.  _host
+ * copies the text to the device first.  HPGQ_E_FORMAT on malformed records. */
+int  hpgq_parse_host(hpgq_parser_t *ps, const char *text, int64_t n, hpgq_batch_t *out);
+int  hpgq_parse_device(hpgq_parser_t *ps, const char *text_dev, int64_t n, hpgq_batch_t *out);
+/* offsets into the last parsed text, num_reads u32 each (any may be NULL):
+ * record start ('@'), sequence, '+' line, quality */
+int  hpgq_parse_records(hpgq_parser_t *ps, uint32_t *rec_start, uint32_t *seq_start,
+                        uint32_t *plus_start, uint32_t *qual_start);
+void *hpgq_parser_stream(hpgq_parser_t *ps);
 
 /* ---------------------------------------------------------------------- */
 /* synthetic input (bench / tests): counter-based, identical on host & GPU */

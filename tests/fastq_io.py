@@ -51,3 +51,31 @@ def check_partial(got, exp, lmax, lay):
         if p in exp:
             np.testing.assert_array_equal(got[lay[p]:lay[p] + lmax], np.array(exp[p], np.uint64),
                                           err_msg=p)
+
+
+def to_fastq(reads, crlf=False, plus_header=False, prefix="r"):
+    """Reads -> FASTQ text; returns (bytes, list of record end offsets)."""
+    nl = b"\r\n" if crlf else b"\n"
+    out, ends, pos = [], [], 0
+    for i in range(reads.n):
+        s, q = reads.read(i)
+        h = f"{prefix}{i} extra:{i % 7}".encode()
+        rec = b"@" + h + nl + s + nl + (b"+" + h if plus_header else b"+") + nl + q + nl
+        out.append(rec)
+        pos += len(rec)
+        ends.append(pos)
+    return b"".join(out), ends
+
+
+def split_records(text):
+    """Reference splitter for the tests: per-record (start, seq, plus, qual) offsets."""
+    lines, starts, p = [], [], 0
+    while p < len(text):
+        e = text.index(b"\n", p)
+        starts.append(p)
+        lines.append((p, e))
+        p = e + 1
+    recs = []
+    for i in range(0, len(lines) - 3, 4):
+        recs.append((lines[i][0], lines[i + 1][0], lines[i + 2][0], lines[i + 3][0]))
+    return recs
