@@ -187,6 +187,37 @@ const char *hpgq_version(void) { return "hpgq 0.1 (gfx950)"; }
 
 const char *hpgq_kernel_name(const hpgq_ctx_t *ctx) { return ctx ? ctx->kname : ""; }
 
+int hpgq_host_alloc(void **ptr, size_t bytes) {
+  if (!ptr) return HPGQ_E_INVALID;
+  *ptr = nullptr;
+  if (hipHostMalloc(ptr, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) return HPGQ_E_NOMEM;
+  return HPGQ_OK;
+}
+
+void hpgq_host_free(void *ptr) {
+  if (ptr) (void)hipHostFree(ptr);
+}
+
+int hpgq_device_alloc(int device, void **ptr, size_t bytes) {
+  if (!ptr) return HPGQ_E_INVALID;
+  *ptr = nullptr;
+  HPGQ_HIP_TRY(hipSetDevice(device));
+  if (hipMalloc(ptr, bytes ? bytes : 1) != hipSuccess) return HPGQ_E_NOMEM;
+  return HPGQ_OK;
+}
+
+void hpgq_device_free(void *ptr) {
+  if (ptr) (void)hipFree(ptr);
+}
+
+int hpgq_copy_to_host(hpgq_ctx_t *c, void *dst, const void *src_dev, size_t bytes) {
+  if (!c || (!dst && bytes) || (!src_dev && bytes)) return HPGQ_E_INVALID;
+  if (!bytes) return HPGQ_OK;
+  HPGQ_HIP_TRY(hipSetDevice(c->device));
+  HPGQ_HIP_TRY(hipMemcpyAsync(dst, src_dev, bytes, hipMemcpyDeviceToHost, c->stream));
+  return HPGQ_OK;
+}
+
 int hpgq_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;

@@ -1,0 +1,71 @@
+/*
+ * hpgq_cli.h — the C host side of hpg-fastq on libhpgq (stats | filter | edit).
+ *
+ * Mirrors the reference's command line (src/hpg-fastq.c; options
+ * src/stats_options.c:260-300, src/filter_options.c:235-258,
+ * src/edit_options.c:267-290), its producer -> worker -> consumer pipeline
+ * (src/stats_fastq.c:174-250, src/filter_fastq.c:106-174,
+ * src/edit_fastq.c:113-206) and its outputs (passed.fq / failed.fq,
+ * edit.fq, <in>.summary.txt + data files, src/stats_report.c), with the
+ * worker's bioinfo-libs calls replaced by the libhpgq C-ABI (include/hpgq.h)
+ * and the reader's parsing moved onto the GPU (hpgq_parse_*).
+ */
+#ifndef HPGQ_CLI_H
+#define HPGQ_CLI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "hpgq.h"
+
+enum { CMD_STATS = 0, CMD_FILTER = 1, CMD_EDIT = 2 };
+
+typedef struct {
+  int command;
+  const char *command_name;
+  const char *exec_name;
+  char *in_filename;
+  char *out_dirname;
+  int num_threads;          /* reader threads */
+  int batch_size;           /* accepted for compatibility; chunks are sized in bytes */
+  char *quality_encoding_name;
+  int quality_encoding_value;
+  int kmers_on;
+  /* filter / trim options, NO_VALUE (-1) when unset (src/stats_options.c:18-40) */
+  char *read_length_range, *read_quality_range, *left_quality_range, *right_quality_range;
+  int min_read_length, max_read_length, min_read_quality, max_read_quality;
+  int left_length, min_left_quality, max_left_quality;
+  int right_length, min_right_quality, max_right_quality;
+  int max_N, max_out_of_quality;
+  int filter_on;
+  /* MI355X build options */
+  int device;
+  int lmax;                 /* per-position arrays (longest read kept) */
+  int chunk_mb;             /* FASTQ text per parse unit */
+  int print_params;         /* print hpgq_params_t and exit (no device) */
+  char *counters_out;       /* raw u64 counter dump (tests) */
+  int quiet;
+} cli_options_t;
+
+/* parse + validate (exits with the reference's messages on errors) */
+cli_options_t *cli_parse(int command, const char *exec_name, int argc, char **argv);
+void cli_display(const cli_options_t *o);
+void cli_free(cli_options_t *o);
+/* NO_VALUE -> MIN/MAX defaults and the libhpgq params (src/filter_fastq.c:195-206) */
+void cli_params(const cli_options_t *o, hpgq_params_t *p);
+void cli_print_params(const hpgq_params_t *p);
+/* src/commons_fastq.c:31-103 */
+int cli_parse_range(int *min, int *max, const char *range, const char *msg);
+
+/* pipeline: returns 0 or a negative HPGQ_E* code */
+typedef struct {
+  uint64_t num_reads, num_passed, num_failed, num_edited;
+  double seconds, fastq_bytes;
+} cli_result_t;
+
+int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, cli_result_t *res);
+
+/* src/stats_report.c: summary + data files */
+int cli_report(const cli_options_t *o, const hpgq_params_t *p, const uint64_t *counters);
+
+#endif

@@ -1,0 +1,143 @@
+/*
+ * hpgq_report.c — stats report files, after src/stats_report.c.
+ *
+ * <in>.summary.txt (report_summary :60-153), <in>.length.histogram.data
+ * (:159-180), <in>.read.quality.histogram.data (:363-390),
+ * <in>.GC.histogram.data (:215-232), <in>.GC.per.nt.data (:268-285),
+ * <in>.quality.per.nt.data (final form, quirk Q6: :306-322),
+ * <in>.nucleotides.data (:336-352).  Values come from the dense device
+ * counters: per-position maps are read by position, not by
+ * khash bucket (quirk Q3); the mean quality is the exact fixed-point mean
+ * (quirk Q2).  The gnuplot images are not produced (gnuplot is absent).
+ */
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "hpgq_cli.h"
+
+#define NORM_Q(q, phred) ((int)round((q) - (phred)))   /* _normalize_quality, :26 */
+
+static FILE *open_out(const cli_options_t *o, const char *base, const char *suffix) {
+  char path[4096];
+  snprintf(path, sizeof(path), "%s/%s.%s", o->out_dirname, base, suffix);
+  return fopen(path, "w");
+}
+
+int cli_report(const cli_options_t *o, const hpgq_params_t *p, const uint64_t *c) {
+  const int lmax = p->lmax, phred = p->phred;
+  const char *slash = strrchr(o->in_filename, '/');
+  const char *base = slash ? slash + 1 : o->in_filename;
+  hpgq_summary_t s;
+  if (hpgq_counters_summary(c, lmax, &s)) return -1;
+  const uint64_t *hl = c + hpgq_off_hist_len(lmax), *hq = c + hpgq_off_hist_meanq(lmax);
+  const uint64_t *hg = c + hpgq_off_hist_gc(lmax), *pq = c + hpgq_off_pos_qsum(lmax);
+  const uint64_t *pA = c + hpgq_off_pos_base(lmax, 0), *pC = c + hpgq_off_pos_base(lmax, 1);
+  const uint64_t *pG = c + hpgq_off_pos_base(lmax, 2), *pT = c + hpgq_off_pos_base(lmax, 3);
+  const uint64_t *pN = c + hpgq_off_pos_base(lmax, 4);
+  const int maxlen = s.num_reads ? s.max_length : 0;
+  /* count per position = reads longer than it */
+  uint64_t *cnt = calloc((size_t)lmax + 1, sizeof(uint64_t));
+  for (int j = lmax - 1; j >= 0; --j) cnt[j] = cnt[j + 1] + hl[j + 1];
+
+  FILE *f = open_out(o, base, "summary.txt");
+  if (!f) { free(cnt); return -1; }
+  const uint64_t nt = s.num_A + s.num_C + s.num_G + s.num_T + s.num_N;
+  fprintf(f, "-----------------------------------\n");
+  fprintf(f, "      FastQ quality report\n");
+  fprintf(f, "-----------------------------------\n");
+  fprintf(f, "FastQ filename: %s\n\n", base);
+  if (p->filter_on) {
+    fprintf(f, "Filter options:\n");
+    if (o->read_length_range) fprintf(f, "\tRead length range   : %s\n", o->read_length_range);
+    if (o->read_quality_range) fprintf(f, "\tRead quality range  : %s\n", o->read_quality_range);
+    if (p->left_length != HPGQ_MIN_VALUE && o->left_quality_range) {
+      fprintf(f, "\tLeft length         : %i nucleotides\n", p->left_length);
+      fprintf(f, "\tLeft quality range  : %s\n", o->left_quality_range);
+    }
+    if (p->right_length != HPGQ_MIN_VALUE && o->right_quality_range) {
+      fprintf(f, "\tRight length        : %i nucleotides\n", p->right_length);
+      fprintf(f, "\tRight quality range : %s\n", o->right_quality_range);
+    }
+    if (p->max_N != HPGQ_MAX_VALUE) fprintf(f, "\tMax. number of Ns   : %i\n", p->max_N);
+    if (p->max_out_of_quality != HPGQ_MAX_VALUE && o->read_quality_range)
+      fprintf(f, "\tMax. out of quality : %i nucletotides\n", p->max_out_of_quality);
+    fprintf(f, "\n");
+    const uint64_t tot = s.num_passed + s.num_failed;
+    fprintf(f, "Number of reads in file  : %lu\n", (unsigned long)tot);
+    fprintf(f, "Number of processed reads: %lu (%0.2f %%)\n", (unsigned long)s.num_reads,
+            tot ? 100.0f * s.num_reads / tot : 0.0f);
+  } else {
+    fprintf(f, "Filter         : Disabled\n");
+    fprintf(f, "Number of reads: %lu\n", (unsigned long)s.num_reads);
+  }
+  fprintf(f, "\n");
+  fprintf(f, "Read length (min., mean, max.): (%i, %0.2f, %i)\n", s.num_reads ? s.min_length : 0,
+          s.num_reads ? 1.0f * s.acc_length / s.num_reads : 0.0f, maxlen);
+  fprintf(f, "\n");
+  int qual = NORM_Q(s.mean_quality_raw, phred);
+  fprintf(f, "Mean quality = %i [%c]\n", qual, qual + phred);
+  fprintf(f, "\n");
+  fprintf(f, "Nucleotide content (A, C, G, T, N)\n");
+  fprintf(f, "\tA: %0.2f %%\n", nt ? 100.0f * s.num_A / nt : 0.0f);
+  fprintf(f, "\tT: %0.2f %%\n", nt ? 100.0f * s.num_T / nt : 0.0f);
+  fprintf(f, "\tG: %0.2f %%\n", nt ? 100.0f * s.num_G / nt : 0.0f);
+  fprintf(f, "\tC: %0.2f %%\n", nt ? 100.0f * s.num_C / nt : 0.0f);
+  fprintf(f, "\tN: %0.2f %%\n", nt ? 100.0f * s.num_N / nt : 0.0f);
+  fprintf(f, "GC content\n");
+  fprintf(f, "\tCG: %0.2f %%\n", nt ? 100.0f * (s.num_G + s.num_C) / nt : 0.0f);
+  fprintf(f, "\n");
+  fprintf(f, "Mean quality per nucleotide position\n");
+  for (int k = 0; k < maxlen; k++) {
+    qual = cnt[k] ? NORM_Q(1.0 * pq[k] / cnt[k], phred) : 0;
+    fprintf(f, "\tpos. %i: %i [%c]\t", k + 1, qual, qual + phred);
+    if ((k + 1) % 5 == 0) fprintf(f, "\n");
+  }
+  fprintf(f, "\n");
+  fclose(f);
+
+  if ((f = open_out(o, base, "length.histogram.data"))) {
+    for (int i = 1; i <= maxlen; i++) fprintf(f, "%i\t%lu\n", i, (unsigned long)hl[i]);
+    fclose(f);
+  }
+  if ((f = open_out(o, base, "read.quality.histogram.data"))) {
+    int lo = -1, hi = -1;
+    for (int i = 0; i < HPGQ_MEANQ_BINS; i++)
+      if (hq[i]) {
+        if (lo < 0) lo = i;
+        hi = i;
+      }
+    for (int i = lo; lo >= 0 && i <= hi; i++) fprintf(f, "%i\t%lu\n", i - phred, (unsigned long)hq[i]);
+    fclose(f);
+  }
+  if ((f = open_out(o, base, "GC.histogram.data"))) {
+    for (int i = 1; i < 100; i++)
+      if (hg[i]) fprintf(f, "%i\t%lu\n", i, (unsigned long)hg[i]);
+    fclose(f);
+  }
+  if ((f = open_out(o, base, "GC.per.nt.data"))) {
+    for (int k = 0; k < maxlen; k++) {
+      const uint64_t t = pA[k] + pC[k] + pG[k] + pT[k] + pN[k];
+      const float v = t ? 100.0f * (pG[k] + pC[k]) / t : 0.0f;
+      if (v > 1.0f) fprintf(f, "%i\t%0.2f\n", k + 1, v);
+    }
+    fclose(f);
+  }
+  if ((f = open_out(o, base, "quality.per.nt.data"))) {
+    for (int k = 0; k < maxlen; k++)
+      fprintf(f, "%i\t%i\n", k, cnt[k] ? NORM_Q(1.0 * pq[k] / cnt[k], phred) : 0);
+    fclose(f);
+  }
+  if ((f = open_out(o, base, "nucleotides.data"))) {
+    for (int k = 0; k < maxlen; k++) {
+      const uint64_t t = pA[k] + pC[k] + pG[k] + pT[k] + pN[k];
+      const float d = t ? 100.0f / t : 0.0f;
+      fprintf(f, "%i\t%0.2f\t%0.2f\t%0.2f\t%0.2f\t%0.2f\n", k + 1, d * pA[k], d * pT[k], d * pG[k],
+              d * pC[k], d * pN[k]);
+    }
+    fclose(f);
+  }
+  free(cnt);
+  return 0;
+}

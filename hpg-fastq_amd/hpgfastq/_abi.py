@@ -128,6 +128,11 @@ _SIGS = [
     ("hpgq_strerror", C.c_char_p, [C.c_int]),
     ("hpgq_version", C.c_char_p, []),
     ("hpgq_kernel_name", C.c_char_p, [C.c_void_p]),
+    ("hpgq_host_alloc", C.c_int, [C.POINTER(C.c_void_p), C.c_size_t]),
+    ("hpgq_host_free", None, [C.c_void_p]),
+    ("hpgq_device_alloc", C.c_int, [C.c_int, C.POINTER(C.c_void_p), C.c_size_t]),
+    ("hpgq_device_free", None, [C.c_void_p]),
+    ("hpgq_copy_to_host", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t]),
 ]
 
 

@@ -343,6 +343,15 @@ const char *hpgq_version(void);
 /* the engine kernel instance a ctx runs (for profiles / bench reports) */
 const char *hpgq_kernel_name(const hpgq_ctx_t *ctx);
 
+/* memory helpers for HIP-free hosts (the C CLI): page-locked host buffers
+ * (fast, asynchronous H2D), device buffers, and a device -> host copy queued
+ * on a ctx stream (complete after hpgq_sync) */
+int  hpgq_host_alloc(void **ptr, size_t bytes);
+void hpgq_host_free(void *ptr);
+int  hpgq_device_alloc(int device, void **ptr, size_t bytes);
+void hpgq_device_free(void *ptr);
+int  hpgq_copy_to_host(hpgq_ctx_t *ctx, void *dst, const void *src_dev, size_t bytes);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,102 @@
+"""The C host CLI end to end on the GPU: FASTQ file -> hpg-fastq stats |
+filter | edit -> counters / output files, against the oracle on the same
+reads.  Small --chunk-mb forces records to be carried across parse units."""
+import os
+
+import numpy as np
+import pytest
+
+import hpgfastq as H
+import oracle_lib as O
+from cli_lib import run_cli
+from fastq_io import to_fastq
+
+pytestmark = pytest.mark.gpu
+
+
+def _records(reads, crlf=False):
+    nl = b"\r\n" if crlf else b"\n"
+    out = []
+    for i in range(reads.n):
+        s, q = reads.read(i)
+        h = f"r{i} extra:{i % 7}".encode()
+        out.append((b"@" + h + nl, s, b"+" + nl, q, nl))
+    return out
+
+
+def _write(tmp_path, reads, crlf=False, name="in.fq"):
+    text, _ = to_fastq(reads, crlf=crlf)
+    path = tmp_path / name
+    path.write_bytes(text)
+    return str(path)
+
+
+@pytest.mark.parametrize("chunk_mb", [1, 256])
+def test_cli_stats_matches_oracle(tmp_path, chunk_mb):
+    reads = O.synth(20000, seed=21, L=150)
+    fq = _write(tmp_path, reads)
+    out = tmp_path / "out"
+    out.mkdir()
+    ctr = tmp_path / "ctr.bin"
+    run_cli(["stats", "-f", fq, "-o", out, "--read-quality-range", "20,", "--read-length-range",
+             "50,", "--lmax", 150, "--chunk-mb", chunk_mb, "--counters-out", ctr, "--quiet"])
+    got = np.fromfile(ctr, np.uint64)
+    p = H.stats_params(lmax=150, read_quality_range="20,", read_length_range="50,")
+    _, _, want = O.run(p, reads)
+    np.testing.assert_array_equal(got, want)
+    summ = (out / "in.fq.summary.txt").read_text()
+    assert f"Number of processed reads: {int(want[H.S_NUM_PASSED])}" in summ
+    for f in ("length.histogram.data", "read.quality.histogram.data", "GC.histogram.data",
+              "GC.per.nt.data", "quality.per.nt.data", "nucleotides.data"):
+        assert (out / f"in.fq.{f}").exists(), f
+
+
+@pytest.mark.parametrize("crlf", [False, True])
+def test_cli_filter_outputs(tmp_path, crlf):
+    reads = O.synth(15000, seed=22, L=150)
+    fq = _write(tmp_path, reads, crlf=crlf)
+    run_cli(["filter", "-f", fq, "-o", tmp_path, "--read-quality-range", "20,",
+             "--read-length-range", "50,", "--max-N", "1", "--chunk-mb", 1, "--quiet"])
+    p = H.filter_params(lmax=1024, read_quality_range="20,", read_length_range="50,", max_N=1)
+    mask, _, _ = O.run(p, reads)
+    recs = [h + sq + nl + plus + q + nl for (h, sq, plus, q, nl) in _records(reads, crlf)]
+    passed = b"".join(r for r, m in zip(recs, mask) if m)
+    failed = b"".join(r for r, m in zip(recs, mask) if not m)
+    assert (tmp_path / "passed.fq").read_bytes() == passed
+    assert (tmp_path / "failed.fq").read_bytes() == failed
+
+
+def test_cli_edit_outputs(tmp_path):
+    reads = O.synth(12000, seed=24, L=150)
+    fq = _write(tmp_path, reads)
+    run_cli(["edit", "-f", fq, "-o", tmp_path, "--left-length", 10, "--left-quality-range", "20,",
+             "--right-length", 30, "--right-quality-range", "20,", "--read-length-range", "60,",
+             "--chunk-mb", 1, "--quiet"])
+    p = H.edit_params(lmax=1024, left_length=10, left_quality_range="20,", right_length=30,
+                      right_quality_range="20,", read_length_range="60,")
+    mask, trim, _ = O.run(p, reads)
+    ok, bad = [], []
+    for (h, s, plus, q, nl), m, t in zip(_records(reads), mask, trim):
+        ts, te = int(t) & 0xFFFF, int(t) >> 16
+        rec = h + s[ts:len(s) - te] + b"\n" + plus + q[ts:len(q) - te] + b"\n"
+        (ok if m else bad).append(rec)
+    assert (tmp_path / "edit.fq").read_bytes() == b"".join(ok)
+    assert (tmp_path / "failed.fq").read_bytes() == b"".join(bad)
+
+
+def test_cli_kat_stats(tmp_path):
+    import json
+    from fastq_io import check_partial
+    gold = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    kat = json.load(open(os.path.join(gold, "kat_expected.json")))
+    ctr = tmp_path / "ctr.bin"
+    run_cli(["stats", "-f", os.path.join(gold, kat["reads"]), "-o", tmp_path, "--lmax", kat["lmax"],
+             "--counters-out", ctr, "--quiet"])
+    check_partial(np.fromfile(ctr, np.uint64), kat["stats"], kat["lmax"], H.layout(kat["lmax"]))
+
+
+def test_cli_read_too_long(tmp_path):
+    reads = O.synth(100, seed=3, L=150)
+    fq = _write(tmp_path, reads)
+    r = run_cli(["stats", "-f", fq, "-o", tmp_path, "--lmax", 100, "--quiet"], check=False)
+    assert r.returncode != 0 and "longer than lmax" in r.stderr
