@@ -127,13 +127,19 @@ static const void *kernel_for(int nm, int nch, bool gen, bool tri, char *name, s
   if (tri) {
     const char *w = std::getenv("HPGQ_TRI_WAVES");      // occupancy experiment knob
     const char *u = std::getenv("HPGQ_TRI_UNALIGNED");  // load-scheme experiment knob
-    int mw = w ? std::atoi(w) : 5;
+    int mw = w ? std::atoi(w) : (nm == 2 ? 4 : 5);   // spill-free occupancy per variant
     mw = mw <= 4 ? 4 : (mw == 5 ? 5 : 6);
     const bool un = u && std::atoi(u) != 0;
-    std::snprintf(name, cap, "hpgq::engine_tri_kernel<%d, %s>", mw, un ? "true" : "false");
-    if (mw <= 4) return un ? (const void *)hpgq::engine_tri_kernel<4, true> : (const void *)hpgq::engine_tri_kernel<4, false>;
-    if (mw == 5) return un ? (const void *)hpgq::engine_tri_kernel<5, true> : (const void *)hpgq::engine_tri_kernel<5, false>;
-    return un ? (const void *)hpgq::engine_tri_kernel<6, true> : (const void *)hpgq::engine_tri_kernel<6, false>;
+    if (nm == 2) {   // paired-end: aligned loads only
+      std::snprintf(name, cap, "hpgq::engine_tri_kernel<%d, false, 2>", mw);
+      if (mw <= 4) return (const void *)hpgq::engine_tri_kernel<4, false, 2>;
+      if (mw == 5) return (const void *)hpgq::engine_tri_kernel<5, false, 2>;
+      return (const void *)hpgq::engine_tri_kernel<6, false, 2>;
+    }
+    std::snprintf(name, cap, "hpgq::engine_tri_kernel<%d, %s, 1>", mw, un ? "true" : "false");
+    if (mw <= 4) return un ? (const void *)hpgq::engine_tri_kernel<4, true, 1> : (const void *)hpgq::engine_tri_kernel<4, false, 1>;
+    if (mw == 5) return un ? (const void *)hpgq::engine_tri_kernel<5, true, 1> : (const void *)hpgq::engine_tri_kernel<5, false, 1>;
+    return un ? (const void *)hpgq::engine_tri_kernel<6, true, 1> : (const void *)hpgq::engine_tri_kernel<6, false, 1>;
   }
   std::snprintf(name, cap, "hpgq::engine_kernel<%d, %d, %s>", nm, nch == 1 ? 1 : (nch == 2 ? 2 : 5),
                 gen ? "true" : "false");
@@ -253,7 +259,7 @@ int hpgq_open(hpgq_ctx_t **out, int device, const hpgq_params_t *p) {
   c->gen = needs_generic(engine_flags(*p));
   {
     const char *force = std::getenv("HPGQ_KERNEL");   // "single" forces the one-read kernel
-    c->tri = c->nm == 1 && !c->gen && p->lmax <= hpgq::kTriPos &&
+    c->tri = !c->gen && p->lmax <= hpgq::kTriPos &&
              !(force && std::strcmp(force, "single") == 0);
   }
   {
@@ -261,9 +267,11 @@ int hpgq_open(hpgq_ctx_t **out, int device, const hpgq_params_t *p) {
     const size_t hist_words = ((size_t)c->nm * hlen + 1) & ~(size_t)1;
     c->lds_bytes = ((size_t)c->nm * 6 * p->lmax + hist_words) * 4 +
                    (size_t)c->nm * HPGQ_NUM_SCALARS * 8 + sizeof(hpgq::ColdParams);
-    // the three-read kernel also keeps per-wave read tables (2 x 1 KB + 256 B)
-    const size_t tri_lds = ((size_t)6 * p->lmax + hist_words) * 4 + HPGQ_NUM_SCALARS * 8 + 16 +
-                           (size_t)hpgq::kWaves * (2 * 256 + 64) * 4;
+    // the three-read kernel: per mate [6][lmax] + hist + scalars, and per wave
+    // and mate two read tables (2 x 1 KB) + segment ends (256 B)
+    const size_t mate_words = (size_t)6 * p->lmax + (((size_t)hlen + 1) & ~(size_t)1) + 2 * HPGQ_NUM_SCALARS;
+    const size_t tri_lds = (size_t)c->nm * mate_words * 4 + 16 +
+                           (size_t)hpgq::kWaves * c->nm * (2 * 256 + 64) * 4;
     if (tri_lds > c->lds_bytes) c->lds_bytes = tri_lds;
   }
   HPGQ_HIP_TRY(hipSetDevice(device));

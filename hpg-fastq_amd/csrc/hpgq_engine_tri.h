@@ -117,6 +117,9 @@ struct TriAcc {
   }
   // bytes -> LDS (pos_acc [6][lmax]: qsum, A, C, G, T, N/other); nibbles empty
   __device__ __forceinline__ void flush(uint32_t *pos_acc, int lmax, int p0) {
+    // rare (every <= 255 triples): keep its 40 LDS addresses out of the hot
+    // loop's registers (hipcc would hoist them as loop invariants and spill)
+    asm volatile("" : "+v"(p0), "+s"(lmax), "+s"(pos_acc));
 #pragma unroll
     for (int w = 0; w < 2; ++w) {
       const uint32_t qv[4] = {q02[w] & 0xFFFFu, q13[w] & 0xFFFFu, q02[w] >> 16, q13[w] >> 16};
@@ -148,6 +151,7 @@ __device__ __forceinline__ uint32_t tri_codes(uint32_t s, uint32_t m, uint32_t &
 // and one "other" count per position (sign: +1 add, -1 subtract)
 __device__ __forceinline__ uint32_t tri_fix(uint32_t s, uint32_t m, uint32_t codes, uint32_t *other,
                                             int lmax, int pos0, uint32_t sign) {
+  asm volatile("" : "+v"(pos0), "+s"(lmax), "+s"(other));   // rare path: no hoisted addresses
   const uint32_t ex = __builtin_amdgcn_perm(kX7Hi, kX7Lo, codes);
   const uint32_t ff = nonzero_bytes((s ^ ex) & m);
   if (ff) {
@@ -166,9 +170,18 @@ using AddTag = TriTag<false>;
 using SubTag = TriTag<true>;
 
 // MINW: minimum waves per SIMD the register allocation must allow (occupancy)
+template <int M>
+struct MateTag {
+  static constexpr int value = M;
+};
+
 // UNAL: unaligned 8-byte loads at the read's byte offset; else dword-aligned
-// loads realigned with DPP wave_shl:1 + v_alignbyte
-template <int MINW, bool UNAL>
+// loads realigned with DPP wave_shl:1 + v_alignbyte.
+// NM = 2: paired-end.  A block is 54 pairs; the wave runs mate 1's triples,
+// then mate 2's, each mate with its own accumulators / LDS partials / counter
+// set; the epilogue takes the pair decision (both mates pass) and subtracts
+// failed pairs from both sets.
+template <int MINW, bool UNAL, int NM>
 __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x;
@@ -185,79 +198,100 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
   // raw-sum bounds: pass iff min_len <= n <= max_len and lo_r*n <= S <= hi_r*n
   const int lo_r = A.min_q + A.phred, hi_r = A.max_q + A.phred;
 
-  // LDS: pos_acc [6][lmax] u32 | hist [hlen] u32 | sc [8] u64 | per-wave tables
+  // LDS per mate: pos_acc [6][lmax] u32 | hist [hlen] u32 | sc [8] u64, then
+  // per wave: per mate two read tables [64] x 16 B (seq offset, qual offset,
+  // length | alignments, -) alternating between blocks, and segment ends [64]
   // (pos_acc row 5 holds "other" counts until the epilogue turns it into N)
-  uint32_t *pos_acc = reinterpret_cast<uint32_t *>(lds);
-  uint32_t *other = pos_acc + 5 * lmax;
-  uint32_t *hist = pos_acc + 6 * lmax;
   const int hist_words = (hlen + 1) & ~1;
-  unsigned long long *sc = reinterpret_cast<unsigned long long *>(hist + hist_words);
-  // per wave: two read tables [64] x 16 B (seq offset, qual offset, length, -)
-  // alternating between consecutive blocks, and the segment ends [64] u32
-  const int tab_words = (6 * lmax + hist_words + 2 * HPGQ_NUM_SCALARS + 3) & ~3;   // 16 B aligned
-  uint32_t *wtab = pos_acc + tab_words + wave * (2 * 256 + 64);
-  uint32_t *wends = wtab + 2 * 256;
-  for (int i = tid; i < 6 * lmax + hist_words; i += kWG) pos_acc[i] = 0;
-  for (int i = tid; i < HPGQ_NUM_SCALARS; i += kWG) sc[i] = 0;
+  const int mate_words = 6 * lmax + hist_words + 2 * HPGQ_NUM_SCALARS;   // even: sc 8-B aligned
+  uint32_t *base = reinterpret_cast<uint32_t *>(lds);
+  auto pos_acc = [&](int m) { return base + m * mate_words; };
+  auto other = [&](int m) { return base + m * mate_words + 5 * lmax; };
+  auto hist = [&](int m) { return base + m * mate_words + 6 * lmax; };
+  auto sc = [&](int m) {
+    return reinterpret_cast<unsigned long long *>(base + m * mate_words + 6 * lmax + hist_words);
+  };
+  constexpr int kWaveWords = NM * (2 * 256 + 64);
+  const int tab_words = (NM * mate_words + 3) & ~3;   // 16 B aligned (host: + 16 B)
+  uint32_t *wtab = base + tab_words + wave * kWaveWords;
+  auto tab = [&](int m, int tb) { return wtab + m * (2 * 256 + 64) + tb * 256; };
+  auto wends = [&](int m) { return wtab + m * (2 * 256 + 64) + 2 * 256; };
+  for (int i = tid; i < NM * mate_words; i += kWG) base[i] = 0;
   __syncthreads();
 
-  // SRDs: the read bytes plus the load slack (unaligned 8-byte windows)
-  const int data_end = uni(A.idx[0][A.num_reads]);
-  const uintptr_t ps = reinterpret_cast<uintptr_t>(A.seq[0]), pq = reinterpret_cast<uintptr_t>(A.qual[0]);
-  const int bs = UNAL ? 0 : (int)(ps & 3), bq = UNAL ? 0 : (int)(pq & 3);   // base misalignment
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-      (void *)(ps - bs), (short)0, bs + data_end + kTriSlack, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(
-      (void *)(pq - bq), (short)0, bq + data_end + kTriSlack, 0x00020000);
-  TriAcc acc;
-  acc.zero();
-  int since_flush = 0;   // triples added since the last LDS flush (a byte grows <= 1 per triple)
-  uint64_t fx16 = 0;
-  uint32_t cnt[7] = {0, 0, 0, 0, 0, 0, 0};   // input, passed, failed, edited, stats, long, any-long
+  // SRDs: the read bytes plus the load slack
+  __amdgpu_buffer_rsrc_t rs[NM], rq[NM];
+  int bs[NM], bq[NM];
+#pragma unroll
+  for (int m = 0; m < NM; ++m) {
+    const int data_end = uni(A.idx[m][A.num_reads]);
+    const uintptr_t ps = reinterpret_cast<uintptr_t>(A.seq[m]), pq = reinterpret_cast<uintptr_t>(A.qual[m]);
+    bs[m] = UNAL ? 0 : (int)(ps & 3);
+    bq[m] = UNAL ? 0 : (int)(pq & 3);
+    rs[m] = __builtin_amdgcn_make_buffer_rsrc((void *)(ps - bs[m]), (short)0,
+                                              bs[m] + data_end + kTriSlack, 0x00020000);
+    rq[m] = __builtin_amdgcn_make_buffer_rsrc((void *)(pq - bq[m]), (short)0,
+                                              bq[m] + data_end + kTriSlack, 0x00020000);
+  }
+  TriAcc acc[NM];
+#pragma unroll
+  for (int m = 0; m < NM; ++m) acc[m].zero();
+  int since_flush = 0;   // triples per mate added since the last LDS flush (a byte grows <= 1 per triple)
+  uint64_t fx16[NM];
+  uint32_t cnt[NM][7];   // input, passed, failed, edited, stats, long, any-long
+#pragma unroll
+  for (int m = 0; m < NM; ++m) {
+    fx16[m] = 0;
+    for (int k = 0; k < 7; ++k) cnt[m][k] = 0;
+  }
 
   const int64_t nblocks = (A.num_reads + kTriBlock - 1) / kTriBlock;
   const int64_t gw = (int64_t)blockIdx.x * kWaves + wave;
   const int64_t nw = (int64_t)gridDim.x * kWaves;
 
-  // block prologue: lane j describes read r0 + j in read table `tb`; lanes >=
-  // nr get length 0, so whatever gathers them contributes nothing.  Returns
-  // this lane's length (the epilogue needs it).
-  auto load_block = [&](int64_t blk, int tb) -> uint32_t {
+  // block prologue: lane j describes read (pair) r0 + j in read table `tb`;
+  // lanes >= nr get length 0, so whatever gathers them contributes nothing.
+  // Returns this lane's lengths (the epilogue needs them).
+  auto load_block = [&](int64_t blk, int tb, uint32_t (&len)[NM]) {
     const int64_t r0 = blk * kTriBlock;
     const int nr = (int)min((int64_t)kTriBlock, A.num_reads - r0);
     const int l = min(lane, nr - 1);
-    const int a = A.idx[0][r0 + l], e = A.idx[0][r0 + l + 1];
-    const uint32_t n = lane < nr ? (uint32_t)(e - a) : 0u;
-    const uint32_t xs = (uint32_t)(bs + a), xq = (uint32_t)(bq + a);
-    v4u rec;
-    if (UNAL) rec = v4u{xs, xq, n, 0u};
-    else rec = v4u{xs & ~3u, xq & ~3u, n | ((xs & 3u) << 16) | ((xq & 3u) << 20), 0u};
-    *reinterpret_cast<v4u *>(wtab + tb * 256 + 4 * lane) = rec;
-    __builtin_amdgcn_wave_barrier();   // other lanes read it (LDS is in order per wave)
-    return n;
+#pragma unroll
+    for (int m = 0; m < NM; ++m) {
+      const int a = A.idx[m][r0 + l], e = A.idx[m][r0 + l + 1];
+      const uint32_t n = lane < nr ? (uint32_t)(e - a) : 0u;
+      const uint32_t xs = (uint32_t)(bs[m] + a), xq = (uint32_t)(bq[m] + a);
+      v4u rec;
+      if (UNAL) rec = v4u{xs, xq, n, 0u};
+      else rec = v4u{xs & ~3u, xq & ~3u, n | ((xs & 3u) << 16) | ((xq & 3u) << 20), 0u};
+      *reinterpret_cast<v4u *>(tab(m, tb) + 4 * lane) = rec;
+      len[m] = n;
+    }
+    __builtin_amdgcn_wave_barrier();   // other lanes read them (LDS is in order per wave)
   };
-  // lane -> its segment's read (entry `src` of read table tb)
-  auto gather = [&](int tb, int src, TriPending &pd) {
-    const v4u rec = *reinterpret_cast<const v4u *>(wtab + tb * 256 + 4 * src);
+  // lane -> its segment's read (entry `src` of mate m's read table tb)
+  auto gather = [&](int m, int tb, int src, TriPending &pd) {
+    const v4u rec = *reinterpret_cast<const v4u *>(tab(m, tb) + 4 * src);
     pd.n = rec.z;
-    pd.s = __builtin_amdgcn_raw_buffer_load_b64(rs, rec.x + lane8, 0, 0);
-    pd.q = __builtin_amdgcn_raw_buffer_load_b64(rq, rec.y + lane8, 0, 0);
+    pd.s = __builtin_amdgcn_raw_buffer_load_b64(rs[m], rec.x + lane8, 0, 0);
+    pd.q = __builtin_amdgcn_raw_buffer_load_b64(rq[m], rec.y + lane8, 0, 0);
   };
 
   TriPending grp[2][kTriU];
-  // issue group g (kTriU triples); triples past the block end gather lane 63
-  // (length 0), so they add nothing
-  auto load_group = [&](int tb, int nt, int g, int slot) {
+  // issue group g (kTriU triples) of mate m; triples past the block end
+  // gather lane 63 (length 0), so they add nothing
+  auto load_group = [&](int m, int tb, int nt, int g, int slot) {
 #pragma unroll
     for (int u = 0; u < kTriU; ++u) {
       const int t = g * kTriU + u;
-      gather(tb, t < nt ? min(3 * t + seg, 63) : 63, grp[slot][u]);
+      gather(m, tb, t < nt ? min(3 * t + seg, 63) : 63, grp[slot][u]);
     }
   };
 
   // one triple: per-lane partial (raw quality | G+C << 18); adds (SUB = false)
-  // or removes (SUB = true) the lane's positions from the counters
-  auto account = [&](const TriPending &pd, bool count, auto sub_tag) -> uint32_t {
+  // or removes (SUB = true) the lane's positions from mate m's counters
+  auto account = [&](auto mtag, const TriPending &pd, bool count, auto sub_tag) -> uint32_t {
+    constexpr int m = decltype(mtag)::value;
     constexpr bool SUB = decltype(sub_tag)::value;
     uint32_t s0 = pd.s.x, s1 = pd.s.y, q0 = pd.q.x, q1 = pd.q.y;
     if (!UNAL) {
@@ -275,38 +309,39 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
     uint32_t c1 = tri_codes(s1, m1, bad);
     if (__builtin_expect(bad != 0, 0)) {
       const uint32_t sign = SUB ? 0xFFFFFFFFu : 1u;
-      c0 = tri_fix(s0, m0, c0, other, count ? lmax : 0, p0, sign);
-      c1 = tri_fix(s1, m1, c1, other, count ? lmax : 0, p0 + 4, sign);
+      c0 = tri_fix(s0, m0, c0, other(m), count ? lmax : 0, p0, sign);
+      c1 = tri_fix(s1, m1, c1, other(m), count ? lmax : 0, p0 + 4, sign);
     }
     const uint32_t cg0 = __builtin_amdgcn_perm(kCGHi, kCGLo, c0);
     const uint32_t cg1 = __builtin_amdgcn_perm(kCGHi, kCGLo, c1);
     if (count) {
+      TriAcc &ac = acc[m];
       const uint32_t at0 = __builtin_amdgcn_perm(kATHi, kATLo, c0);
       const uint32_t at1 = __builtin_amdgcn_perm(kATHi, kATLo, c1);
       const uint32_t h0 = __builtin_amdgcn_perm(0u, qm0, 0x0C030C01u);   // bytes 1, 3
       const uint32_t h1 = __builtin_amdgcn_perm(0u, qm1, 0x0C030C01u);
       if (SUB) {
-        acc.c8[0][1] -= cg0 & 0x0F0F0F0Fu;
-        acc.c8[0][2] -= (cg0 >> 4) & 0x0F0F0F0Fu;
-        acc.c8[0][0] -= at0 & 0x0F0F0F0Fu;
-        acc.c8[0][3] -= (at0 >> 4) & 0x0F0F0F0Fu;
-        acc.c8[1][1] -= cg1 & 0x0F0F0F0Fu;
-        acc.c8[1][2] -= (cg1 >> 4) & 0x0F0F0F0Fu;
-        acc.c8[1][0] -= at1 & 0x0F0F0F0Fu;
-        acc.c8[1][3] -= (at1 >> 4) & 0x0F0F0F0Fu;
-        acc.q02[0] -= qm0 & 0x00FF00FFu;
-        acc.q13[0] -= h0;
-        acc.q02[1] -= qm1 & 0x00FF00FFu;
-        acc.q13[1] -= h1;
+        ac.c8[0][1] -= cg0 & 0x0F0F0F0Fu;
+        ac.c8[0][2] -= (cg0 >> 4) & 0x0F0F0F0Fu;
+        ac.c8[0][0] -= at0 & 0x0F0F0F0Fu;
+        ac.c8[0][3] -= (at0 >> 4) & 0x0F0F0F0Fu;
+        ac.c8[1][1] -= cg1 & 0x0F0F0F0Fu;
+        ac.c8[1][2] -= (cg1 >> 4) & 0x0F0F0F0Fu;
+        ac.c8[1][0] -= at1 & 0x0F0F0F0Fu;
+        ac.c8[1][3] -= (at1 >> 4) & 0x0F0F0F0Fu;
+        ac.q02[0] -= qm0 & 0x00FF00FFu;
+        ac.q13[0] -= h0;
+        ac.q02[1] -= qm1 & 0x00FF00FFu;
+        ac.q13[1] -= h1;
       } else {
-        acc.n4[0][0] += cg0;
-        acc.n4[0][1] += at0;
-        acc.n4[1][0] += cg1;
-        acc.n4[1][1] += at1;
-        acc.q02[0] += qm0 & 0x00FF00FFu;
-        acc.q13[0] += h0;
-        acc.q02[1] += qm1 & 0x00FF00FFu;
-        acc.q13[1] += h1;
+        ac.n4[0][0] += cg0;
+        ac.n4[0][1] += at0;
+        ac.n4[1][0] += cg1;
+        ac.n4[1][1] += at1;
+        ac.q02[0] += qm0 & 0x00FF00FFu;
+        ac.q13[0] += h0;
+        ac.q02[1] += qm1 & 0x00FF00FFu;
+        ac.q13[1] += h1;
       }
     }
     const uint32_t gc = (uint32_t)__builtin_popcount(cg1) + (uint32_t)__builtin_popcount(cg0);
@@ -314,13 +349,13 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
     return qs + (gc << 18);
   };
 
-  uint32_t len = 0, lenn = 0;
+  uint32_t len[NM], lenn[NM];
   int tb = 0;   // read table of the current block
   int64_t blk = gw;
   if (blk < nblocks) {
-    len = load_block(blk, tb);
+    load_block(blk, tb, len);
     const int nr0 = (int)min((int64_t)kTriBlock, A.num_reads - blk * kTriBlock);
-    load_group(tb, (nr0 + 2) / 3, 0, 0);
+    load_group(0, tb, (nr0 + 2) / 3, 0, 0);
   }
   const uint64_t not_seg_first = 0x6DB6DB6DB6DB6DB6ull;   // lanes j with j % 3 != 0
   for (; blk < nblocks; blk += nw) {
@@ -329,121 +364,160 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
     const int nt = (nr + 2) / 3;
     const int64_t nblk = blk + nw < nblocks ? blk + nw : blk;   // next block (or self)
     const int nnt = ((int)min((int64_t)kTriBlock, A.num_reads - nblk * kTriBlock) + 2) / 3;
-    lenn = load_block(nblk, tb ^ 1);
+    load_block(nblk, tb ^ 1, lenn);
     if (stats && since_flush > kByteEvery - kTriBlock / 3) {   // keep every byte <= 255
-      acc.flush(pos_acc, lmax, p0);
+#pragma unroll
+      for (int m = 0; m < NM; ++m) acc[m].flush(pos_acc(m), lmax, p0);
       since_flush = 0;
     }
+    // an even number of groups per mate, so every mate (and block) starts in
+    // slot 0 (the padding group gathers length-0 reads)
+    const int ngroups = ((nt + kTriU - 1) / kTriU + 1) & ~1;
 
-    auto process_group = [&](int g, int slot) {
+    auto run_mate = [&](auto mtag) {
+      constexpr int m = decltype(mtag)::value;
+      auto process_group = [&](int g, int slot) {
 #pragma unroll
-      for (int u = 0; u < kTriU; ++u) {
-        const int t = g * kTriU + u;
-        // every read is added; failed ones are taken out in the block epilogue
-        const uint32_t x = account(grp[slot][u], stats, AddTag{});
-        const uint32_t P = wave_scan(x);
-        // segment ends (lanes 20, 41, 62) -> wends[3t + seg], no wait needed
-        if (ls == 20 && seg < 3 && t < nt) wends[3 * t + seg] = P;
-      }
-    };
-
-    const int ngroups = (nt + kTriU - 1) / kTriU;
-    for (int g = 0; g < ngroups; g += 2) {
-      if (g + 1 < ngroups) load_group(tb, nt, g + 1, 1);
-      else load_group(tb ^ 1, nnt, 0, 1);
-      process_group(g, 0);
-      if (g + 1 < ngroups) {
-        if (g + 2 < ngroups) load_group(tb, nt, g + 2, 0);
-        else load_group(tb ^ 1, nnt, 0, 0);
+        for (int u = 0; u < kTriU; ++u) {
+          const int t = g * kTriU + u;
+          // every read is added; failed ones are taken out in the block epilogue
+          const uint32_t x = account(MateTag<m>{}, grp[slot][u], stats, AddTag{});
+          const uint32_t P = wave_scan(x);
+          // segment ends (lanes 20, 41, 62) -> wends[3t + seg], no wait needed
+          if (ls == 20 && seg < 3 && t < nt) wends(m)[3 * t + seg] = P;
+        }
+      };
+      // after this mate's last group: the next mate's first group, or the next block's
+      auto load_next_unit = [&](int slot) {
+        if (m + 1 < NM) load_group(m + 1 < NM ? m + 1 : 0, tb, nt, 0, slot);
+        else load_group(0, tb ^ 1, nnt, 0, slot);
+      };
+      for (int g = 0; g < ngroups; g += 2) {
+        load_group(m, tb, nt, g + 1, 1);
+        process_group(g, 0);
+        if (g + 2 < ngroups) load_group(m, tb, nt, g + 2, 0);
+        else load_next_unit(0);
         process_group(g + 1, 1);
+        // nibbles hold at most 15 triples: widen after groups 0-3 and at the end
+        static_assert(4 * kTriU <= kNibbleEvery && kTriBlock / 3 - 4 * kTriU <= kNibbleEvery, "");
+        if (stats && g == 2) acc[m].widen();
       }
-      // nibbles hold at most 15 triples: widen after groups 0-3 and at block end
-      static_assert(4 * kTriU <= kNibbleEvery && kTriBlock / 3 - 4 * kTriU <= kNibbleEvery, "");
-      if (stats && g == 2) acc.widen();
-    }
-    if (stats) acc.widen();
+      if (stats) acc[m].widen();
+    };
+    run_mate(MateTag<0>{});
+    if (NM == 2) run_mate(MateTag<NM - 1>{});
     since_flush += nt;
 
-    // ---- block epilogue (lane j = read r0 + j) ----------------------------
+    // ---- block epilogue (lane j = read / pair r0 + j) --------------------
     const bool valid = lane < nr;
-    const int n = (int)len;
-    // per-read sums: difference of consecutive segment ends within a triple
-    // (wends[3t + k] = inclusive wave prefix at the end of segment k)
     __builtin_amdgcn_wave_barrier();
-    const uint32_t ends = lane < nr ? wends[lane] : 0u;
-    const uint32_t prev = __builtin_amdgcn_mov_dpp(ends, 0x138, 0xF, 0xF, true);   // lane j-1
-    const uint32_t r1 = ends - (((not_seg_first >> lane) & 1u) ? prev : 0u);
-    const int sraw = (int)(r1 & 0x3FFFFu);
+    uint32_t r1[NM];
     bool pass = valid;
-    if (filter)
-      pass = pass && n >= A.min_len && n <= A.max_len && lo_r * n <= sraw && sraw <= hi_r * n;
-    const bool lg = valid && n > lmax;
+#pragma unroll
+    for (int m = 0; m < NM; ++m) {
+      // per-read sums: difference of consecutive segment ends within a triple
+      // (wends[3t + k] = inclusive wave prefix at the end of segment k)
+      const uint32_t ends = valid ? wends(m)[lane] : 0u;
+      const uint32_t prev = __builtin_amdgcn_mov_dpp(ends, 0x138, 0xF, 0xF, true);   // lane j-1
+      r1[m] = ends - (((not_seg_first >> lane) & 1u) ? prev : 0u);
+      const int n = (int)len[m];
+      const int sraw = (int)(r1[m] & 0x3FFFFu);
+      if (filter)
+        pass = pass && n >= A.min_len && n <= A.max_len && lo_r * n <= sraw && sraw <= hi_r * n;
+    }
     if (valid && A.mask) A.mask[r0 + lane] = (uint8_t)pass;
     const uint64_t failed = __ballot(valid && !pass);
-    cnt[0] += (uint32_t)nr;
-    cnt[1] += (uint32_t)__builtin_popcountll(__ballot(pass));
-    cnt[2] += (uint32_t)__builtin_popcountll(failed);
-    cnt[6] += (uint32_t)__builtin_popcountll(__ballot(lg));
-    if (stats) {
-      cnt[4] += (uint32_t)__builtin_popcountll(__ballot(pass));
-      cnt[5] += (uint32_t)__builtin_popcountll(__ballot(pass && lg));
-      if (pass && !lg) {
-        const uint32_t gc = r1 >> 18, wn = (uint32_t)n, s = (uint32_t)sraw;
-        atomicAdd(&hist[wn], 1u);
-        if (wn > 0) {
-          atomicAdd(&hist[lmax + 1 + (2 * s + wn) / (2 * wn)], 1u);
-          atomicAdd(&hist[lmax + 1 + HPGQ_MEANQ_BINS + (100 * gc) / wn], 1u);
-          const uint32_t q = s / wn, rem = s - q * wn;
-          fx16 += ((uint64_t)q << 16) + (((uint32_t)rem << 16) / wn);
+    const uint32_t npass = (uint32_t)__builtin_popcountll(__ballot(pass));
+#pragma unroll
+    for (int m = 0; m < NM; ++m) {
+      const int n = (int)len[m];
+      const bool lg = valid && n > lmax;
+      cnt[m][0] += (uint32_t)nr;
+      cnt[m][1] += npass;
+      cnt[m][2] += (uint32_t)__builtin_popcountll(failed);
+      cnt[m][6] += (uint32_t)__builtin_popcountll(__ballot(lg));
+      if (stats) {
+        cnt[m][4] += npass;
+        cnt[m][5] += (uint32_t)__builtin_popcountll(__ballot(pass && lg));
+        if (pass && !lg) {
+          const uint32_t gc = r1[m] >> 18, wn = (uint32_t)n, s = r1[m] & 0x3FFFFu;
+          uint32_t *h = hist(m);
+          atomicAdd(&h[wn], 1u);
+          if (wn > 0) {
+            atomicAdd(&h[lmax + 1 + (2 * s + wn) / (2 * wn)], 1u);
+            atomicAdd(&h[lmax + 1 + HPGQ_MEANQ_BINS + (100 * gc) / wn], 1u);
+            const uint32_t q = s / wn, rem = s - q * wn;
+            fx16[m] += ((uint64_t)q << 16) + (((uint32_t)rem << 16) / wn);
+          }
         }
       }
-      // take the failed reads back out, a triple at a time (same lanes as the add)
-      uint64_t fl = failed;
-      while (fl) {
-        const int j = (int)__builtin_ctzll(fl);
-        const int t = j / 3;
-        const uint32_t fbits = (uint32_t)(fl >> (3 * t)) & 7u;
-        fl &= ~(7ull << (3 * t));
-        TriPending pd;
-        gather(tb, ((fbits >> (seg & 3)) & 1u) ? min(3 * t + seg, 63) : 63, pd);
-        (void)account(pd, true, SubTag{});
-      }
     }
-    len = lenn;
+    if (stats) {
+      // take the failed reads (pairs: both mates) back out, a triple at a time
+      auto sub_mate = [&](auto mtag) {
+        constexpr int m = decltype(mtag)::value;
+        uint64_t fl = failed;
+        while (fl) {
+          const int j = (int)__builtin_ctzll(fl);
+          const int t = j / 3;
+          const uint32_t fbits = (uint32_t)(fl >> (3 * t)) & 7u;
+          fl &= ~(7ull << (3 * t));
+          TriPending pd;
+          gather(m, tb, ((fbits >> (seg & 3)) & 1u) ? min(3 * t + seg, 63) : 63, pd);
+          (void)account(MateTag<m>{}, pd, true, SubTag{});
+        }
+      };
+      sub_mate(MateTag<0>{});
+      if (NM == 2) sub_mate(MateTag<NM - 1>{});
+    }
+#pragma unroll
+    for (int m = 0; m < NM; ++m) len[m] = lenn[m];
     tb ^= 1;
   }
 
   // ---- workgroup epilogue ---------------------------------------------------
-  acc.widen();
-  acc.flush(pos_acc, lmax, p0);
-  {
-    const uint32_t lo = (uint32_t)fx16, hi = (uint32_t)(fx16 >> 32);
+#pragma unroll
+  for (int m = 0; m < NM; ++m) {
+    acc[m].widen();
+    acc[m].flush(pos_acc(m), lmax, p0);
+    const uint32_t lo = (uint32_t)fx16[m], hi = (uint32_t)(fx16[m] >> 32);
     const uint64_t tot = (uint64_t)wave_sum(lo & 0xFFFFu) + ((uint64_t)wave_sum(lo >> 16) << 16) +
                          ((uint64_t)wave_sum(hi) << 32);
     if (lane == 0) {
-      if (cnt[0]) atomicAdd(&sc[HPGQ_S_NUM_INPUT], (unsigned long long)cnt[0]);
-      if (cnt[1]) atomicAdd(&sc[HPGQ_S_NUM_PASSED], (unsigned long long)cnt[1]);
-      if (cnt[2]) atomicAdd(&sc[HPGQ_S_NUM_FAILED], (unsigned long long)cnt[2]);
-      if (cnt[4]) atomicAdd(&sc[HPGQ_S_NUM_STATS], (unsigned long long)cnt[4]);
-      if (cnt[5]) atomicAdd(&sc[HPGQ_S_LONG_READS], (unsigned long long)cnt[5]);
-      if (tot) atomicAdd(&sc[HPGQ_S_ACC_MEANQ_FX16], (unsigned long long)tot);
-      if (cnt[6] && A.err) atomicOr(A.err, 1);
+      unsigned long long *s = sc(m);
+      if (cnt[m][0]) atomicAdd(&s[HPGQ_S_NUM_INPUT], (unsigned long long)cnt[m][0]);
+      if (cnt[m][1]) atomicAdd(&s[HPGQ_S_NUM_PASSED], (unsigned long long)cnt[m][1]);
+      if (cnt[m][2]) atomicAdd(&s[HPGQ_S_NUM_FAILED], (unsigned long long)cnt[m][2]);
+      if (cnt[m][4]) atomicAdd(&s[HPGQ_S_NUM_STATS], (unsigned long long)cnt[m][4]);
+      if (cnt[m][5]) atomicAdd(&s[HPGQ_S_LONG_READS], (unsigned long long)cnt[m][5]);
+      if (tot) atomicAdd(&s[HPGQ_S_ACC_MEANQ_FX16], (unsigned long long)tot);
+      if (cnt[m][6] && A.err) atomicOr(A.err, 1);
     }
   }
   __syncthreads();
-  // N at position p = (stats reads longer than p) - A - C - G - T - other
-  for (int p = tid; p < lmax; p += kWG) {
-    uint32_t c = 0;
-    for (int L = p + 1; L <= lmax; ++L) c += hist[L];
-    other[p] = c - pos_acc[lmax + p] - pos_acc[2 * lmax + p] - pos_acc[3 * lmax + p] -
-               pos_acc[4 * lmax + p] - other[p];
+  const int off_pos = HPGQ_NUM_SCALARS + hlen;
+#pragma unroll
+  for (int m = 0; m < NM; ++m) {
+    // N at position p = (stats reads longer than p) - A - C - G - T - other
+    uint32_t *pa = pos_acc(m), *h = hist(m);
+    for (int p = tid; p < lmax; p += kWG) {
+      uint32_t c = 0;
+      for (int L = p + 1; L <= lmax; ++L) c += h[L];
+      pa[5 * lmax + p] = c - pa[lmax + p] - pa[2 * lmax + p] - pa[3 * lmax + p] -
+                         pa[4 * lmax + p] - pa[5 * lmax + p];
+    }
   }
   __syncthreads();
-  uint64_t *row = A.slab + (size_t)blockIdx.x * A.clen;
-  const int off_pos = HPGQ_NUM_SCALARS + hlen;
-  for (int i = tid; i < HPGQ_NUM_SCALARS; i += kWG) row[i] += sc[i];
-  for (int i = tid; i < hlen; i += kWG) row[HPGQ_NUM_SCALARS + i] += hist[i];
-  for (int i = tid; i < 6 * lmax; i += kWG) row[off_pos + i] += pos_acc[i];
+  uint64_t *row = A.slab + (size_t)blockIdx.x * NM * A.clen;
+#pragma unroll
+  for (int m = 0; m < NM; ++m) {
+    uint64_t *rm = row + (size_t)m * A.clen;
+    const unsigned long long *s = sc(m);
+    const uint32_t *h = hist(m), *pa = pos_acc(m);
+    for (int i = tid; i < HPGQ_NUM_SCALARS; i += kWG) rm[i] += s[i];
+    for (int i = tid; i < hlen; i += kWG) rm[HPGQ_NUM_SCALARS + i] += h[i];
+    for (int i = tid; i < 6 * lmax; i += kWG) rm[off_pos + i] += pa[i];
+  }
 }
 
 }  // namespace hpgq
