@@ -26,7 +26,10 @@ struct hpgq_ctx {
   const void *kfn = nullptr;
   int nch = 1;
   bool gen = false;               // generic (edit / N / OOR / left-right) kernel variant
-  bool tri = false;               // three-reads-per-wave FAST kernel (SE, lmax <= 160)
+  bool tri = false;               // three-reads-per-wave FAST kernel (lmax <= 160)
+  bool tri_edit = false;          // ... with the trim pre-pass (single-end edit)
+  uint32_t *d_trim_tmp = nullptr; // trims when the caller wants none back
+  size_t trim_tmp_cap = 0;
   int grid = 0;
   uint64_t *d_slab = nullptr;     // [grid][nm * clen] per-workgroup partials
   hpgq::ColdParams *d_cold = nullptr;
@@ -123,7 +126,14 @@ static const void *kernel_nch(int nch) {
   }
 }
 
-static const void *kernel_for(int nm, int nch, bool gen, bool tri, char *name, size_t cap) {
+static const void *kernel_for(int nm, int nch, bool gen, bool tri, bool edit, char *name, size_t cap) {
+  if (tri && edit) {   // single-end edit: trim pre-pass + windows
+    const char *w = std::getenv("HPGQ_TRI_WAVES");
+    const int mw = w && std::atoi(w) == 4 ? 4 : 5;
+    std::snprintf(name, cap, "hpgq::engine_tri_kernel<%d, false, 1, true>", mw);
+    return mw == 4 ? (const void *)hpgq::engine_tri_kernel<4, false, 1, true>
+                   : (const void *)hpgq::engine_tri_kernel<5, false, 1, true>;
+  }
   if (tri) {
     const char *w = std::getenv("HPGQ_TRI_WAVES");      // occupancy experiment knob
     const char *u = std::getenv("HPGQ_TRI_UNALIGNED");  // load-scheme experiment knob
@@ -131,15 +141,15 @@ static const void *kernel_for(int nm, int nch, bool gen, bool tri, char *name, s
     mw = mw <= 4 ? 4 : (mw == 5 ? 5 : 6);
     const bool un = u && std::atoi(u) != 0;
     if (nm == 2) {   // paired-end: aligned loads only
-      std::snprintf(name, cap, "hpgq::engine_tri_kernel<%d, false, 2>", mw);
-      if (mw <= 4) return (const void *)hpgq::engine_tri_kernel<4, false, 2>;
-      if (mw == 5) return (const void *)hpgq::engine_tri_kernel<5, false, 2>;
-      return (const void *)hpgq::engine_tri_kernel<6, false, 2>;
+      std::snprintf(name, cap, "hpgq::engine_tri_kernel<%d, false, 2, false>", mw);
+      if (mw <= 4) return (const void *)hpgq::engine_tri_kernel<4, false, 2, false>;
+      if (mw == 5) return (const void *)hpgq::engine_tri_kernel<5, false, 2, false>;
+      return (const void *)hpgq::engine_tri_kernel<6, false, 2, false>;
     }
-    std::snprintf(name, cap, "hpgq::engine_tri_kernel<%d, %s, 1>", mw, un ? "true" : "false");
-    if (mw <= 4) return un ? (const void *)hpgq::engine_tri_kernel<4, true, 1> : (const void *)hpgq::engine_tri_kernel<4, false, 1>;
-    if (mw == 5) return un ? (const void *)hpgq::engine_tri_kernel<5, true, 1> : (const void *)hpgq::engine_tri_kernel<5, false, 1>;
-    return un ? (const void *)hpgq::engine_tri_kernel<6, true, 1> : (const void *)hpgq::engine_tri_kernel<6, false, 1>;
+    std::snprintf(name, cap, "hpgq::engine_tri_kernel<%d, %s, 1, false>", mw, un ? "true" : "false");
+    if (mw <= 4) return un ? (const void *)hpgq::engine_tri_kernel<4, true, 1, false> : (const void *)hpgq::engine_tri_kernel<4, false, 1, false>;
+    if (mw == 5) return un ? (const void *)hpgq::engine_tri_kernel<5, true, 1, false> : (const void *)hpgq::engine_tri_kernel<5, false, 1, false>;
+    return un ? (const void *)hpgq::engine_tri_kernel<6, true, 1, false> : (const void *)hpgq::engine_tri_kernel<6, false, 1, false>;
   }
   std::snprintf(name, cap, "hpgq::engine_kernel<%d, %d, %s>", nm, nch == 1 ? 1 : (nch == 2 ? 2 : 5),
                 gen ? "true" : "false");
@@ -259,8 +269,12 @@ int hpgq_open(hpgq_ctx_t **out, int device, const hpgq_params_t *p) {
   c->gen = needs_generic(engine_flags(*p));
   {
     const char *force = std::getenv("HPGQ_KERNEL");   // "single" forces the one-read kernel
-    c->tri = !c->gen && p->lmax <= hpgq::kTriPos &&
+    const int fl = engine_flags(*p);
+    const bool filter_extras = fl & (hpgq::F_NEED_N | hpgq::F_NEED_OOR | hpgq::F_NEED_LR);
+    const bool edit = fl & hpgq::F_EDIT;
+    c->tri = !filter_extras && (!edit || c->nm == 1) && p->lmax <= hpgq::kTriPos &&
              !(force && std::strcmp(force, "single") == 0);
+    c->tri_edit = c->tri && edit;
   }
   {
     const int hlen = p->lmax + 1 + HPGQ_MEANQ_BINS + HPGQ_GC_BINS;
@@ -282,7 +296,7 @@ int hpgq_open(hpgq_ctx_t **out, int device, const hpgq_params_t *p) {
   HPGQ_HIP_TRY(hipMemsetAsync(c->d_err, 0, sizeof(int32_t), c->stream));
   int cus = 0;
   HPGQ_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-  const void *kfn = kernel_for(c->nm, c->nch, c->gen, c->tri, c->kname, sizeof(c->kname));
+  const void *kfn = kernel_for(c->nm, c->nch, c->gen, c->tri, c->tri_edit, c->kname, sizeof(c->kname));
   c->kfn = kfn;
   if (c->lds_bytes > 64 * 1024)
     HPGQ_HIP_TRY(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -314,6 +328,7 @@ void hpgq_close(hpgq_ctx_t *c) {
   (void)hipFree(c->d_err);
   (void)hipFree(c->d_slab);
   (void)hipFree(c->d_cold);
+  (void)hipFree(c->d_trim_tmp);
   (void)hipFree(c->d_buf);
   (void)hipFree(c->d_mask);
   (void)hipFree(c->d_trim);
@@ -325,6 +340,21 @@ static int launch(hpgq_ctx *c, hpgq::EngineArgs &A) {
   if (A.num_reads <= 0) return HPGQ_OK;
   A.slab = c->d_slab;
   A.err = c->d_err;
+  if (c->tri_edit) {   // trims first (into the caller's trim buffer, else a scratch one)
+    if (!A.trim) {
+      if ((size_t)A.num_reads > c->trim_tmp_cap) {
+        (void)hipFree(c->d_trim_tmp);
+        c->d_trim_tmp = nullptr;
+        c->trim_tmp_cap = 0;
+        const size_t cap = (size_t)A.num_reads + (size_t)A.num_reads / 4 + 1024;
+        if (hipMalloc(&c->d_trim_tmp, cap * 4) != hipSuccess) return HPGQ_E_NOMEM;
+        c->trim_tmp_cap = cap;
+      }
+      A.trim = c->d_trim_tmp;
+    }
+    hpgq::trim_kernel<<<(unsigned)((A.num_reads + 255) / 256), 256, 0, c->stream>>>(A, A.trim);
+    HPGQ_HIP_TRY(hipGetLastError());
+  }
   const int64_t per_block = c->tri ? hpgq::kTriBlock : 64;
   const int64_t nblocks = (A.num_reads + per_block - 1) / per_block;
   const int64_t need = (nblocks + hpgq::kWaves - 1) / hpgq::kWaves;

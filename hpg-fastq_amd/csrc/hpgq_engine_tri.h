@@ -170,6 +170,61 @@ using AddTag = TriTag<false>;
 using SubTag = TriTag<true>;
 
 // MINW: minimum waves per SIMD the register allocation must allow (occupancy)
+// ---- edit (A6) pre-pass for the three-read kernel ---------------------------
+// One thread per read: the leading run of out-of-range qualities within the
+// first min(edit_left_length, n) bases and the trailing run within the last
+// min(edit_right_length, n - ts), 8 bytes at a time with the
+// SWAR in_range test.  Writes trim[r] = ts | te << 16 — the edit output — and
+// the three-read kernel then reads each window [ts, n - te) directly.
+__global__ void __launch_bounds__(256) trim_kernel(EngineArgs A, uint32_t *trim) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r >= A.num_reads) return;
+  const ColdParams &C = *A.cold;
+  const int data_end = uni(A.idx[0][A.num_reads]);
+  const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)A.qual[0], (short)0, data_end + kTriSlack, 0x00020000);
+  const int a = A.idx[0][r], n = A.idx[0][r + 1] - a;
+  auto ok8 = [&](int pos, int lo_none_sel) -> uint64_t {   // 0x80 per in-range byte of [pos, pos+8)
+    const v2u w = __builtin_amdgcn_raw_buffer_load_b64(rq, (uint32_t)(a + pos), 0, 0);
+    uint32_t lo, hi;
+    if (lo_none_sel == 0) {
+      lo = in_range(w.x, C.el_lo4, C.el_hi4, C.el_lo_none, C.el_hi_none, C.el_none_in);
+      hi = in_range(w.y, C.el_lo4, C.el_hi4, C.el_lo_none, C.el_hi_none, C.el_none_in);
+    } else {
+      lo = in_range(w.x, C.er_lo4, C.er_hi4, C.er_lo_none, C.er_hi_none, C.er_none_in);
+      hi = in_range(w.y, C.er_lo4, C.er_hi4, C.er_lo_none, C.er_hi_none, C.er_none_in);
+    }
+    return (uint64_t)lo | ((uint64_t)hi << 32);
+  };
+  auto low_bytes = [](int k) -> uint64_t { return k >= 8 ? ~0ull : ((1ull << (8 * max(k, 0))) - 1); };
+  int ts = 0, te = 0;
+  if (C.e_left_len > 0) {
+    const int lim = min(C.e_left_len, n);
+    ts = lim;
+    for (int c = 0; c < lim; c += 8) {
+      const uint64_t ok = ok8(c, 0) & low_bytes(lim - c);
+      if (ok) {
+        ts = c + (__builtin_ctzll(ok) >> 3);
+        break;
+      }
+    }
+  }
+  if (C.e_right_len > 0) {
+    const int lim = min(C.e_right_len, n - ts);
+    const int lo = n - lim;
+    te = lim;
+    for (int e = n; e > lo; e -= 8) {
+      const int st = max(e - 8, lo);
+      const uint64_t ok = ok8(st, 1) & low_bytes(e - st);
+      if (ok) {
+        te = n - 1 - (st + ((63 - __builtin_clzll(ok)) >> 3));
+        break;
+      }
+    }
+  }
+  trim[r] = (uint32_t)ts | ((uint32_t)te << 16);
+}
+
 template <int M>
 struct MateTag {
   static constexpr int value = M;
@@ -181,8 +236,11 @@ struct MateTag {
 // then mate 2's, each mate with its own accumulators / LDS partials / counter
 // set; the epilogue takes the pair decision (both mates pass) and subtracts
 // failed pairs from both sets.
-template <int MINW, bool UNAL, int NM>
+// EDIT (NM = 1): trim_kernel ran first; each read is its window [ts, n - te)
+// (offset + ts, length n - ts - te): stats and filter see the trimmed read.
+template <int MINW, bool UNAL, int NM, bool EDIT>
 __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
+  static_assert(!EDIT || NM == 1, "edit on the three-read kernel is single-end");
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -252,13 +310,20 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
   // block prologue: lane j describes read (pair) r0 + j in read table `tb`;
   // lanes >= nr get length 0, so whatever gathers them contributes nothing.
   // Returns this lane's lengths (the epilogue needs them).
-  auto load_block = [&](int64_t blk, int tb, uint32_t (&len)[NM]) {
+  auto load_block = [&](int64_t blk, int tb, uint32_t (&len)[NM], uint32_t &tw, uint32_t &nraw) {
     const int64_t r0 = blk * kTriBlock;
     const int nr = (int)min((int64_t)kTriBlock, A.num_reads - r0);
     const int l = min(lane, nr - 1);
 #pragma unroll
     for (int m = 0; m < NM; ++m) {
-      const int a = A.idx[m][r0 + l], e = A.idx[m][r0 + l + 1];
+      int a = A.idx[m][r0 + l], e = A.idx[m][r0 + l + 1];
+      nraw = lane < nr ? (uint32_t)(e - a) : 0u;
+      if (EDIT) {   // the trimmed window
+        tw = lane < nr ? A.trim[r0 + l] : 0u;
+        a += (int)(tw & 0xFFFFu);
+        e -= (int)(tw >> 16);
+        if (e < a) e = a;
+      }
       const uint32_t n = lane < nr ? (uint32_t)(e - a) : 0u;
       const uint32_t xs = (uint32_t)(bs[m] + a), xq = (uint32_t)(bq[m] + a);
       v4u rec;
@@ -350,10 +415,11 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
   };
 
   uint32_t len[NM], lenn[NM];
+  uint32_t tw = 0, twn = 0, nraw = 0, nrawn = 0;   // EDIT: trim word, untrimmed length
   int tb = 0;   // read table of the current block
   int64_t blk = gw;
   if (blk < nblocks) {
-    load_block(blk, tb, len);
+    load_block(blk, tb, len, tw, nraw);
     const int nr0 = (int)min((int64_t)kTriBlock, A.num_reads - blk * kTriBlock);
     load_group(0, tb, (nr0 + 2) / 3, 0, 0);
   }
@@ -364,7 +430,7 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
     const int nt = (nr + 2) / 3;
     const int64_t nblk = blk + nw < nblocks ? blk + nw : blk;   // next block (or self)
     const int nnt = ((int)min((int64_t)kTriBlock, A.num_reads - nblk * kTriBlock) + 2) / 3;
-    load_block(nblk, tb ^ 1, lenn);
+    load_block(nblk, tb ^ 1, lenn, twn, nrawn);
     if (stats && since_flush > kByteEvery - kTriBlock / 3) {   // keep every byte <= 255
 #pragma unroll
       for (int m = 0; m < NM; ++m) acc[m].flush(pos_acc(m), lmax, p0);
@@ -428,10 +494,12 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
     if (valid && A.mask) A.mask[r0 + lane] = (uint8_t)pass;
     const uint64_t failed = __ballot(valid && !pass);
     const uint32_t npass = (uint32_t)__builtin_popcountll(__ballot(pass));
+    if (EDIT) cnt[0][3] += (uint32_t)__builtin_popcountll(__ballot(valid && tw != 0u));
 #pragma unroll
     for (int m = 0; m < NM; ++m) {
       const int n = (int)len[m];
-      const bool lg = valid && n > lmax;
+      // too long for the counters: the untrimmed length decides (as engine_kernel)
+      const bool lg = valid && (EDIT ? (int)nraw : n) > lmax;
       cnt[m][0] += (uint32_t)nr;
       cnt[m][1] += npass;
       cnt[m][2] += (uint32_t)__builtin_popcountll(failed);
@@ -472,6 +540,8 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
     }
 #pragma unroll
     for (int m = 0; m < NM; ++m) len[m] = lenn[m];
+    tw = twn;
+    nraw = nrawn;
     tb ^= 1;
   }
 
@@ -488,6 +558,7 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
       if (cnt[m][0]) atomicAdd(&s[HPGQ_S_NUM_INPUT], (unsigned long long)cnt[m][0]);
       if (cnt[m][1]) atomicAdd(&s[HPGQ_S_NUM_PASSED], (unsigned long long)cnt[m][1]);
       if (cnt[m][2]) atomicAdd(&s[HPGQ_S_NUM_FAILED], (unsigned long long)cnt[m][2]);
+      if (cnt[m][3]) atomicAdd(&s[HPGQ_S_NUM_EDITED], (unsigned long long)cnt[m][3]);
       if (cnt[m][4]) atomicAdd(&s[HPGQ_S_NUM_STATS], (unsigned long long)cnt[m][4]);
       if (cnt[m][5]) atomicAdd(&s[HPGQ_S_LONG_READS], (unsigned long long)cnt[m][5]);
       if (tot) atomicAdd(&s[HPGQ_S_ACC_MEANQ_FX16], (unsigned long long)tot);

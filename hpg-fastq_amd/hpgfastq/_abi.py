@@ -4,7 +4,8 @@ import os
 import sys
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "libhpgq.so")
+# HPGQ_LIB_PATH: load another build of the same C-ABI (A/B timing of kernel variants)
+LIB_PATH = os.environ.get("HPGQ_LIB_PATH") or os.path.join(os.path.dirname(_HERE), "libhpgq.so")
 
 NO_VALUE, MIN_VALUE, MAX_VALUE = -1, 0, 100000
 LMAX_LIMIT = 1024
