@@ -270,3 +270,19 @@ def test_committed_vectors_gpu(name, kernel_choice):
     np.testing.assert_array_equal(ctr, z["counters"])
     if p.edit_on:
         np.testing.assert_array_equal(trim, z["trim"])
+
+
+def test_rccl_allreduce_single_rank():
+    """hpgq_comm_init + hpgq_allreduce on a one-rank communicator: the RCCL
+    path bench.py takes at N > 1 (fold, in-place u64 sum) leaves the counters
+    equal to the oracle's."""
+    reads = O.synth(30000, seed=31, L=150)
+    p = H.stats_params(lmax=150, read_quality_range="20,", read_length_range="50,")
+    with H.Engine(p) as e:
+        e.comm_init(1, 0, H.engine.comm_unique_id())
+        e.process(reads.seq, reads.qual, reads.idx)
+        e.allreduce()
+        e.sync()
+        got = e.counters()
+    _, _, want = O.run(p, reads)
+    np.testing.assert_array_equal(got, want)
