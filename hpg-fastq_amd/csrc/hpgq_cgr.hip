@@ -125,25 +125,38 @@ __device__ __forceinline__ void fill_classes(uint8_t *cls, int tid, int nthreads
 // One base of chaos_game_fill_tables (:197-260), branch-free.  FULL adds the
 // word to the tables (sign = 1 adds, 0xFFFFFFFF takes it back out); !FULL only
 // advances f, the word counter and the boundary clamp (context replay).
-// UNCOND: the tables have a spare row + cell, so the add is issued for every
-// base (adding 0 when no word completes) instead of under a divergent branch.
+//
+// f moves as the reference's
+//     A/T (axis bit 1): f = f + (dim - f) * 0.5       C/G (bit 0): f = f * 0.5
+// computed as  D = fma(f, S, C);  f = fma(D, 0.5, f)  with S = -1 (moving
+// base) / 0, C = dim (bit 1) / 0: D = round(dim - f) exactly as the
+// subtraction, and D * 0.5 is exact, so fma(D, 0.5, f) rounds f + (dim - f) *
+// 0.5 once as the reference does; bit 0 gives fma(-f, 0.5, f) = f / 2 exactly
+// (= f * 0.5); a non-moving byte gives fma(0, 0.5, f) = f.  Two FP64 ops per
+// axis and no selects.
+//
+// UNCOND (LDS tables, sign = 1): one 64-bit LDS add per word into an
+// interleaved table — count in the low half (<= 2^32 words per workgroup
+// launch, so it never carries), quality sum in the high half (wraps mod 2^32
+// like the reference's unsigned int) — issued for every base (adding 0 when no
+// word completes; the spare row + cell take the out-of-range index).
 template <int K, bool FULL, bool UNCOND>
 __device__ __forceinline__ void step(uint32_t fl, uint32_t qb, uint32_t qold, State &st, int &cnt,
                                      uint32_t &acc, uint32_t *ts, uint32_t *tq, uint32_t sign,
                                      uint32_t sub, uint32_t &words) {
   constexpr int dim = 1 << K;
-  const bool mv = fl & F_MV, bx = fl & F_BX, by = fl & F_BY, isN = fl & F_N;
-  const double hx = st.fx * 0.5, hy = st.fy * 0.5;
-  // f + (dim - f) * 0.5 with the product exact: one fma rounds identically
-  const double gx = __builtin_fma((double)dim - st.fx, 0.5, st.fx);
-  const double gy = __builtin_fma((double)dim - st.fy, 0.5, st.fy);
-  // keep both candidates computed unconditionally (else hipcc sinks them under
-  // an exec-mask branch per base, which costs more than the arithmetic)
-  asm volatile("" ::"v"(hx), "v"(gx), "v"(hy), "v"(gy));
-  st.fx = mv ? (bx ? gx : hx) : st.fx;
-  st.fy = mv ? (by ? gy : hy) : st.fy;
-  cnt = isN ? 0 : cnt + (mv ? 1 : 0);
-  if (FULL) acc = isN ? 0u : acc + (mv ? qb : 0u);
+  constexpr uint32_t kDimHi = (uint32_t)(1023 + K) << 20;   // high word of (double)dim
+  const uint32_t mvm = (uint32_t)((int32_t)(fl << 31) >> 31);   // all ones when moving
+  const uint32_t bxm = (uint32_t)((int32_t)(fl << 30) >> 31);
+  const uint32_t bym = (uint32_t)((int32_t)(fl << 29) >> 31);
+  const uint32_t nm = (uint32_t)((int32_t)(fl << 28) >> 31);    // 'N'
+  const double S = __hiloint2double((int)(mvm & 0xBFF00000u), 0);
+  const double Cx = __hiloint2double((int)(bxm & kDimHi), 0);
+  const double Cy = __hiloint2double((int)(bym & kDimHi), 0);
+  st.fx = __builtin_fma(__builtin_fma(st.fx, S, Cx), 0.5, st.fx);
+  st.fy = __builtin_fma(__builtin_fma(st.fy, S, Cy), 0.5, st.fy);
+  cnt = (int)(((uint32_t)cnt + (fl & F_MV)) & ~nm);
+  if (FULL) acc = (acc + (qb & mvm)) & ~nm;
   const bool word = cnt == K;
   int cx = (int)st.fx, cy = (int)st.fy;
   // boundary clamp (:241-251): f == dim only after ~50 A/T (x) or G/T (y) in a row
@@ -161,8 +174,8 @@ __device__ __forceinline__ void step(uint32_t fl, uint32_t qb, uint32_t qold, St
   if (FULL) {
     const int cell = cx * dim + cy;   // <= dim*dim + dim only when !word (spare cells)
     if (UNCOND) {
-      atomicAdd(&ts[cell], word ? sign : 0u);
-      atomicAdd(&tq[cell], word ? sign * (acc - sub) : 0u);
+      const uint64_t inc = ((uint64_t)(word ? acc - sub : 0u) << 32) | (word ? 1u : 0u);
+      atomicAdd(reinterpret_cast<unsigned long long *>(ts) + cell, (unsigned long long)inc);
     } else if (word) {
       atomicAdd(&ts[cell], sign);
       atomicAdd(&tq[cell], sign * (acc - sub));
@@ -311,8 +324,9 @@ __global__ void __launch_bounds__(kWG) cgr_fill_kernel(Args A) {
   constexpr int cells = dim * dim + dim + 1;   // + the spare row/cell of the unconditional adds
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   __shared__ uint8_t cls[256];
+  // LDS: one u64 per cell, count | quality sum << 32 (see step)
   uint32_t *ts = kLds ? lds : A.ts;
-  uint32_t *tq = kLds ? lds + cells : A.tq;
+  uint32_t *tq = kLds ? nullptr : A.tq;
   if (kLds)
     for (int i = threadIdx.x; i < 2 * cells; i += kWG) lds[i] = 0;
   fill_classes(cls, threadIdx.x, kWG);
@@ -336,8 +350,8 @@ __global__ void __launch_bounds__(kWG) cgr_fill_kernel(Args A) {
   if (kLds) {
     __syncthreads();
     for (int i = threadIdx.x; i < dim * dim; i += kWG) {
-      if (lds[i]) atomicAdd(&A.ts[i], lds[i]);
-      if (lds[cells + i]) atomicAdd(&A.tq[i], lds[cells + i]);
+      if (lds[2 * i]) atomicAdd(&A.ts[i], lds[2 * i]);
+      if (lds[2 * i + 1]) atomicAdd(&A.tq[i], lds[2 * i + 1]);
     }
   }
 }
@@ -365,47 +379,56 @@ __global__ void __launch_bounds__(64) cgr_fix_kernel(Args A) {
   __shared__ uint8_t cls[256];
   fill_classes(cls, threadIdx.x, 64);
   __syncthreads();
-  if (threadIdx.x != 0) return;
+  const int lane = threadIdx.x;
   const Src S = make_src(A);
   const int64_t nw = (A.num_reads + 63) >> 6;
   const int64_t ns = (nw + 63) >> 6;
-  int64_t last = 0;   // reads <= last are final
+  int64_t last = 0;   // reads <= last are final (lane 0)
   unsigned long long replays = 0;
   uint32_t dummy = 0;
-  for (int64_t si = 0; si < ns; ++si) {
-    unsigned long long sw = A.sum[si];
-    while (sw) {
-      const int64_t wi = si * 64 + __builtin_ctzll(sw);
-      sw &= sw - 1;
-      unsigned long long fw = A.flags[wi];
-      while (fw) {
-        int64_t r = wi * 64 + __builtin_ctzll(fw);
-        fw &= fw - 1;
-        if (r <= last) continue;
-        double2 entry = A.e[r - 1];
-        for (;;) {
-          if (valid_read(A, r)) {
-            const double2 g = A.g[r];
-            State s1 = {g.x, g.y};
-            run_read<K, true, false>(A, S, A.idx[r], A.idx[r + 1] - A.idx[r], 0, 0, s1,
-                                     A.ts, A.tq, 0xFFFFFFFFu, dummy);   // undo
+  // the wave scans 64 summary words at a time; lane 0 replays in read order
+  for (int64_t sb = 0; sb < ns; sb += 64) {
+    const unsigned long long v = sb + lane < ns ? A.sum[sb + lane] : 0ull;
+    unsigned long long nz = __ballot(v != 0ull);
+    while (nz) {
+      const int l = __builtin_ctzll(nz);
+      nz &= nz - 1;
+      unsigned long long sw = __shfl(v, l);
+      if (lane != 0) continue;
+      const int64_t si = sb + l;
+      while (sw) {
+        const int64_t wi = si * 64 + __builtin_ctzll(sw);
+        sw &= sw - 1;
+        unsigned long long fw = A.flags[wi];
+        while (fw) {
+          int64_t r = wi * 64 + __builtin_ctzll(fw);
+          fw &= fw - 1;
+          if (r <= last) continue;
+          double2 entry = A.e[r - 1];
+          for (;;) {
+            if (valid_read(A, r)) {
+              const double2 g = A.g[r];
+              State s1 = {g.x, g.y};
+              run_read<K, true, false>(A, S, A.idx[r], A.idx[r + 1] - A.idx[r], 0, 0, s1, A.ts,
+                                       A.tq, 0xFFFFFFFFu, dummy);   // undo
+            }
+            State s2 = {entry.x, entry.y};
+            if (valid_read(A, r))
+              run_read<K, true, false>(A, S, A.idx[r], A.idx[r + 1] - A.idx[r], 0, 0, s2, A.ts,
+                                       A.tq, 1u, dummy);
+            const double2 ex = make_double2(s2.fx, s2.fy);
+            A.e[r] = ex;
+            ++replays;
+            last = r;
+            if (r + 1 >= A.num_reads || same(ex, A.g[r + 1])) break;
+            entry = ex;
+            ++r;
           }
-          State s2 = {entry.x, entry.y};
-          if (valid_read(A, r))
-            run_read<K, true, false>(A, S, A.idx[r], A.idx[r + 1] - A.idx[r], 0, 0, s2,
-                                     A.ts, A.tq, 1u, dummy);
-          const double2 ex = make_double2(s2.fx, s2.fy);
-          A.e[r] = ex;
-          ++replays;
-          last = r;
-          if (r + 1 >= A.num_reads || same(ex, A.g[r + 1])) break;
-          entry = ex;
-          ++r;
         }
       }
     }
   }
-  *A.replays = replays;
+  if (lane == 0) *A.replays = replays;
 }
 
 template <int K>
