@@ -135,12 +135,17 @@ __device__ __forceinline__ void fill_classes(uint8_t *cls, int tid, int nthreads
 // (= f * 0.5); a non-moving byte gives fma(0, 0.5, f) = f.  Two FP64 ops per
 // axis and no selects.
 //
-// UNCOND (LDS tables, sign = 1): one 64-bit LDS add per word into an
+// UNCOND (LDS tables, sign = 1): one 64-bit LDS add per base into an
 // interleaved table — count in the low half (<= 2^32 words per workgroup
-// launch, so it never carries), quality sum in the high half (wraps mod 2^32
-// like the reference's unsigned int) — issued for every base (adding 0 when no
-// word completes; the spare row + cell take the out-of-range index).
-template <int K, bool FULL, bool UNCOND>
+// launch, so it never carries), the raw quality accumulator in the high half
+// (mod 2^32; the flush takes count * sub back out, so the table holds
+// sum(acc - sub) as the reference's unsigned int does) — a base that
+// completes no word adds to the spare cell dim*dim instead.
+//
+// CLAMP: the boundary clamp (:241-251) can fire in this step.  f reaches dim
+// only after ~50 A/T (x) or G/T (y) in a row; run_chunk proves per 8 bases
+// that it cannot (see kHot) and runs the clamp-free steps.
+template <int K, bool FULL, bool UNCOND, bool CLAMP>
 __device__ __forceinline__ void step(uint32_t fl, uint32_t qb, uint32_t qold, State &st, int &cnt,
                                      uint32_t &acc, uint32_t *ts, uint32_t *tq, uint32_t sign,
                                      uint32_t sub, uint32_t &words) {
@@ -159,8 +164,7 @@ __device__ __forceinline__ void step(uint32_t fl, uint32_t qb, uint32_t qold, St
   if (FULL) acc = (acc + (qb & mvm)) & ~nm;
   const bool word = cnt == K;
   int cx = (int)st.fx, cy = (int)st.fy;
-  // boundary clamp (:241-251): f == dim only after ~50 A/T (x) or G/T (y) in a row
-  if (__builtin_expect(__ballot(word && (cx == dim || cy == dim)) != 0, 0)) {
+  if (CLAMP) {
     if (word && cx == dim) {
       cx = dim - 1;
       st.fx = st.fx - kEps;
@@ -170,17 +174,18 @@ __device__ __forceinline__ void step(uint32_t fl, uint32_t qb, uint32_t qold, St
       st.fy = st.fy - kEps;
     }
   }
-  cnt -= word ? 1 : 0;
+  cnt = word ? K - 1 : cnt;
   if (FULL) {
-    const int cell = cx * dim + cy;   // <= dim*dim + dim only when !word (spare cells)
     if (UNCOND) {
-      const uint64_t inc = ((uint64_t)(word ? acc - sub : 0u) << 32) | (word ? 1u : 0u);
+      const uint32_t cell = word ? (uint32_t)(cx * dim + cy) : (uint32_t)(dim * dim);
+      const uint64_t inc = ((uint64_t)acc << 32) | 1u;
       atomicAdd(reinterpret_cast<unsigned long long *>(ts) + cell, (unsigned long long)inc);
     } else if (word) {
+      const int cell = cx * dim + cy;
       atomicAdd(&ts[cell], sign);
       atomicAdd(&tq[cell], sign * (acc - sub));
     }
-    words += word ? 1u : 0u;
+    if (!UNCOND) words += word ? 1u : 0u;   // LDS tables: the flush sums the counts
     acc -= word ? qold : 0u;   // quality[quality_position - word_size] (:259), raw position
   }
 }
@@ -215,8 +220,34 @@ __device__ int count_before(const Args &A, const Src &S, const uint8_t *cls, int
   return m;
 }
 
+// A step moves f at most halfway towards dim (d' >= d/2 - ulp/2 for d = dim
+// - f, ulp = dim * 2^-53; 'C'/'G' and the kEps nudge leave d >= 1e-5), so
+// from d >= dim * 2^-30 at a chunk start f stays below dim for 8 steps and
+// the clamp cannot fire: kHot is the wave-uniform test for the CLAMP steps.
+template <int K>
+__device__ __forceinline__ bool hot(const State &st) {
+  constexpr double kHot = (double)(1 << K) * (1.0 - 0x1p-30);
+  return __ballot(st.fx > kHot || st.fy > kHot) != 0ull;
+}
+
 // One 8-byte chunk of a read at byte c (< n).  h1/h2: the two previous
 // quality chunks (for quality[qpos - K]), rotated here.
+template <int K, bool FULL, bool UNCOND, bool CLAMP>
+__device__ __forceinline__ void run_chunk_steps(v2u cl, v2u qv, v2u h1, v2u h2, State &st, int &cnt,
+                                                uint32_t &acc, uint32_t *ts, uint32_t *tq,
+                                                uint32_t sign, uint32_t sub, uint32_t &words) {
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    uint32_t qold = 0;
+    if (FULL) {
+      const int o = u + 1 - K;   // raw byte j+1-K relative to this chunk
+      qold = o >= 0 ? sbyte_of(qv, o) : (o >= -8 ? sbyte_of(h1, o + 8) : sbyte_of(h2, o + 16));
+    }
+    step<K, FULL, UNCOND, CLAMP>(byte_of(cl, u), FULL ? sbyte_of(qv, u) : 0u, qold, st, cnt, acc,
+                                 ts, tq, sign, sub, words);
+  }
+}
+
 template <int K, bool FULL, bool UNCOND>
 __device__ __forceinline__ void run_chunk(v2u sv, v2u qv, v2u &h1, v2u &h2, int left, State &st,
                                           int &cnt, uint32_t &acc, uint32_t *ts, uint32_t *tq,
@@ -226,16 +257,10 @@ __device__ __forceinline__ void run_chunk(v2u sv, v2u qv, v2u &h1, v2u &h2, int 
   sv.x &= (uint32_t)m;
   sv.y &= (uint32_t)(m >> 32);
   const v2u cl = {classes4(sv.x), classes4(sv.y)};
-#pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    uint32_t qold = 0;
-    if (FULL) {
-      const int o = u + 1 - K;   // raw byte j+1-K relative to this chunk
-      qold = o >= 0 ? sbyte_of(qv, o) : (o >= -8 ? sbyte_of(h1, o + 8) : sbyte_of(h2, o + 16));
-    }
-    step<K, FULL, UNCOND>(byte_of(cl, u), FULL ? sbyte_of(qv, u) : 0u, qold, st, cnt, acc, ts, tq,
-                          sign, sub, words);
-  }
+  if (__builtin_expect(hot<K>(st), 0))
+    run_chunk_steps<K, FULL, UNCOND, true>(cl, qv, h1, h2, st, cnt, acc, ts, tq, sign, sub, words);
+  else
+    run_chunk_steps<K, FULL, UNCOND, false>(cl, qv, h1, h2, st, cnt, acc, ts, tq, sign, sub, words);
   if (FULL) {
     h2 = h1;
     h1 = qv;
@@ -321,7 +346,7 @@ template <int K>
 __global__ void __launch_bounds__(kWG) cgr_fill_kernel(Args A) {
   constexpr int dim = 1 << K;
   constexpr bool kLds = K <= kLdsMaxK;
-  constexpr int cells = dim * dim + dim + 1;   // + the spare row/cell of the unconditional adds
+  constexpr int cells = dim * dim + 1;   // + the spare cell of the unconditional adds
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   __shared__ uint8_t cls[256];
   // LDS: one u64 per cell, count | quality sum << 32 (see step)
@@ -343,17 +368,21 @@ __global__ void __launch_bounds__(kWG) cgr_fill_kernel(Args A) {
     }
     A.e[r] = make_double2(st.fx, st.fy);
   }
+  if (kLds) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < dim * dim; i += kWG) {
+      const uint32_t c = lds[2 * i];
+      if (c) {
+        atomicAdd(&A.ts[i], c);
+        atomicAdd(&A.tq[i], lds[2 * i + 1] - c * A.base_quality * (uint32_t)K);
+      }
+      words += c;   // every completed word added 1 to one real cell
+    }
+  }
   // fq_word_count: wave sum, one atomic per wave
   uint64_t w = words;
   for (int o = 32; o > 0; o >>= 1) w += __shfl_xor(w, o);
   if ((threadIdx.x & 63) == 0 && w) atomicAdd(A.words, (unsigned long long)w);
-  if (kLds) {
-    __syncthreads();
-    for (int i = threadIdx.x; i < dim * dim; i += kWG) {
-      if (lds[2 * i]) atomicAdd(&A.ts[i], lds[2 * i]);
-      if (lds[2 * i + 1]) atomicAdd(&A.tq[i], lds[2 * i + 1]);
-    }
-  }
 }
 
 __device__ __forceinline__ bool same(double2 a, double2 b) {
@@ -534,7 +563,7 @@ int hpgq_cgr_open(hpgq_cgr_t **cg, int device, int k, int base_quality) {
   HPGQ_HIP_TRY(hipMemsetAsync(c->d_tq, 0, cells * 4, c->stream));
   HPGQ_HIP_TRY(hipMemsetAsync(c->d_words, 0, 8, c->stream));
   HPGQ_HIP_TRY(hipMemsetAsync(c->d_replays, 0, 8, c->stream));
-  c->lds = k <= hpgq::cgr::kLdsMaxK ? 2 * (cells + c->dim + 1) * 4 : 0;
+  c->lds = k <= hpgq::cgr::kLdsMaxK ? 2 * (cells + 1) * 4 : 0;   // u64 per cell + spare
   const void *kfn = hpgq::cgr::fill_for(k);
   if (c->lds > 64 * 1024)
     HPGQ_HIP_TRY(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->lds));

@@ -122,6 +122,23 @@ def test_cgr_homopolymers_replay_exactly():
     assert rep >= 0
 
 
+@pytest.mark.parametrize("k", [2, 7, 9])
+def test_cgr_boundary_clamp_runs(k):
+    """Runs long enough for f to reach dim (the clamp at old/chaos_game.c:241-251)
+    on x (A), y (G) and both (T), at ragged lengths so the clamp lands at every
+    offset of the 8-base chunks the kernel proves clamp-free."""
+    rng = np.random.default_rng(11 + k)
+    pairs = []
+    for i in range(600):
+        L = int(rng.integers(1, 260))
+        run = bytes([b"AGT"[i % 3]]) * int(rng.integers(40, 200))
+        mix = np.array(rng.choice(list(b"ACGTN"), L), np.uint8).tobytes()
+        s = (mix[: L // 3] + run + mix[L // 3:])[:L] if i % 4 else run[:L]
+        q = rng.integers(33, 75, len(s)).astype(np.uint8).tobytes()
+        pairs.append((s, q))
+    assert_cgr(k, [O.Reads.from_pairs(pairs)])
+
+
 def test_cgr_edge_bytes_and_lengths():
     pairs = [(b"", b""), (b"A", b"I"), (b"acgtACGTnNxX", b"IIII5555++++"),
              (b"ACGT" * 30, bytes([200] * 60 + [40] * 60)), (b"NNNNACGTACGTN", b"#" * 13),
