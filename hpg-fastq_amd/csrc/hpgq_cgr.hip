@@ -145,21 +145,28 @@ __device__ __forceinline__ void fill_classes(uint8_t *cls, int tid, int nthreads
 // CLAMP: the boundary clamp (:241-251) can fire in this step.  f reaches dim
 // only after ~50 A/T (x) or G/T (y) in a row; run_chunk proves per 8 bases
 // that it cannot (see kHot) and runs the clamp-free steps.
-template <int K, bool FULL, bool UNCOND, bool CLAMP>
-__device__ __forceinline__ void step(uint32_t fl, uint32_t qb, uint32_t qold, State &st, int &cnt,
-                                     uint32_t &acc, uint32_t *ts, uint32_t *tq, uint32_t sign,
-                                     uint32_t sub, uint32_t &words) {
-  constexpr int dim = 1 << K;
+// f's move for byte class fl (see above)
+template <int K>
+__device__ __forceinline__ void move(uint32_t fl, State &st) {
   constexpr uint32_t kDimHi = (uint32_t)(1023 + K) << 20;   // high word of (double)dim
-  const uint32_t mvm = (uint32_t)((int32_t)(fl << 31) >> 31);   // all ones when moving
+  const uint32_t mvm = (uint32_t)((int32_t)(fl << 31) >> 31);
   const uint32_t bxm = (uint32_t)((int32_t)(fl << 30) >> 31);
   const uint32_t bym = (uint32_t)((int32_t)(fl << 29) >> 31);
-  const uint32_t nm = (uint32_t)((int32_t)(fl << 28) >> 31);    // 'N'
   const double S = __hiloint2double((int)(mvm & 0xBFF00000u), 0);
   const double Cx = __hiloint2double((int)(bxm & kDimHi), 0);
   const double Cy = __hiloint2double((int)(bym & kDimHi), 0);
   st.fx = __builtin_fma(__builtin_fma(st.fx, S, Cx), 0.5, st.fx);
   st.fy = __builtin_fma(__builtin_fma(st.fy, S, Cy), 0.5, st.fy);
+}
+
+template <int K, bool FULL, bool UNCOND, bool CLAMP>
+__device__ __forceinline__ void step(uint32_t fl, uint32_t qb, uint32_t qold, State &st, int &cnt,
+                                     uint32_t &acc, uint32_t *ts, uint32_t *tq, uint32_t sign,
+                                     uint32_t sub, uint32_t &words) {
+  constexpr int dim = 1 << K;
+  const uint32_t mvm = (uint32_t)((int32_t)(fl << 31) >> 31);   // all ones when moving
+  const uint32_t nm = (uint32_t)((int32_t)(fl << 28) >> 31);    // 'N'
+  move<K>(fl, st);
   cnt = (int)(((uint32_t)cnt + (fl & F_MV)) & ~nm);
   if (FULL) acc = (acc + (qb & mvm)) & ~nm;
   const bool word = cnt == K;
@@ -230,41 +237,59 @@ __device__ __forceinline__ bool hot(const State &st) {
   return __ballot(st.fx > kHot || st.fy > kHot) != 0ull;
 }
 
-// One 8-byte chunk of a read at byte c (< n).  h1/h2: the two previous
-// quality chunks (for quality[qpos - K]), rotated here.
+__device__ __forceinline__ int opaque(int x) {
+  asm volatile("" : "+v"(x));
+  return x;
+}
+
+// Quality bytes around an 8-byte chunk at c: m = [c-8, c+8) and, for K > 9
+// (quality[qpos - K] up to 11 bytes back), lo = [c-16, c-8).  Loaded fresh
+// for every chunk rather than rotated through registers: a loop-carried copy
+// of the newest load makes the loop head wait for it (vmcnt(0)).  Offsets
+// before the buffer read 0 (raw buffer range check); bytes before the read are
+// never used (a word holds K bases of the read).
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+struct QWin {
+  v4u m;
+  v2u lo;
+};
+
+template <int K>
+__device__ __forceinline__ uint32_t qbyte(const QWin &q, int o) {   // o in [-16, 8)
+  if (o >= -8) {
+    const int i = o + 8;
+    return (uint32_t)(int32_t)(int8_t)((q.m[i >> 2] >> (8 * (i & 3))) & 0xFFu);
+  }
+  return sbyte_of(q.lo, o + 16);
+}
+
+// One 8-byte chunk of a read (classes cl, qualities q).
 template <int K, bool FULL, bool UNCOND, bool CLAMP>
-__device__ __forceinline__ void run_chunk_steps(v2u cl, v2u qv, v2u h1, v2u h2, State &st, int &cnt,
+__device__ __forceinline__ void run_chunk_steps(v2u cl, const QWin &q, State &st, int &cnt,
                                                 uint32_t &acc, uint32_t *ts, uint32_t *tq,
                                                 uint32_t sign, uint32_t sub, uint32_t &words) {
 #pragma unroll
   for (int u = 0; u < 8; ++u) {
-    uint32_t qold = 0;
-    if (FULL) {
-      const int o = u + 1 - K;   // raw byte j+1-K relative to this chunk
-      qold = o >= 0 ? sbyte_of(qv, o) : (o >= -8 ? sbyte_of(h1, o + 8) : sbyte_of(h2, o + 16));
-    }
-    step<K, FULL, UNCOND, CLAMP>(byte_of(cl, u), FULL ? sbyte_of(qv, u) : 0u, qold, st, cnt, acc,
+    // quality[j + 1 - K], raw position (the reference's quality_position - word_size)
+    const uint32_t qold = FULL ? qbyte<K>(q, u + 1 - K) : 0u;
+    step<K, FULL, UNCOND, CLAMP>(byte_of(cl, u), FULL ? qbyte<K>(q, u) : 0u, qold, st, cnt, acc,
                                  ts, tq, sign, sub, words);
   }
 }
 
 template <int K, bool FULL, bool UNCOND>
-__device__ __forceinline__ void run_chunk(v2u sv, v2u qv, v2u &h1, v2u &h2, int left, State &st,
-                                          int &cnt, uint32_t &acc, uint32_t *ts, uint32_t *tq,
-                                          uint32_t sign, uint32_t sub, uint32_t &words) {
+__device__ __forceinline__ void run_chunk(v2u sv, const QWin &q, int left, State &st, int &cnt,
+                                          uint32_t &acc, uint32_t *ts, uint32_t *tq, uint32_t sign,
+                                          uint32_t sub, uint32_t &words) {
   // bytes past the read end -> 0 (class 0: no-op); left <= 0 masks all
   const uint64_t m = left >= 8 ? ~0ull : ((1ull << (8 * max(left, 0))) - 1);
   sv.x &= (uint32_t)m;
   sv.y &= (uint32_t)(m >> 32);
   const v2u cl = {classes4(sv.x), classes4(sv.y)};
   if (__builtin_expect(hot<K>(st), 0))
-    run_chunk_steps<K, FULL, UNCOND, true>(cl, qv, h1, h2, st, cnt, acc, ts, tq, sign, sub, words);
+    run_chunk_steps<K, FULL, UNCOND, true>(cl, q, st, cnt, acc, ts, tq, sign, sub, words);
   else
-    run_chunk_steps<K, FULL, UNCOND, false>(cl, qv, h1, h2, st, cnt, acc, ts, tq, sign, sub, words);
-  if (FULL) {
-    h2 = h1;
-    h1 = qv;
-  }
+    run_chunk_steps<K, FULL, UNCOND, false>(cl, q, st, cnt, acc, ts, tq, sign, sub, words);
 }
 
 // Run read [a, a+n) from byte p0 (word counter cnt0) with state st.  The
@@ -276,22 +301,99 @@ __device__ void run_read(const Args &A, const Src &S, int a, int n, int p0, int 
   const uint32_t sub = A.base_quality * (uint32_t)K;
   int cnt = cnt0;
   uint32_t acc = 0;
-  const v2u z = {0u, 0u};
-  v2u h1 = z, h2 = z;
   auto ld_s = [&](int c) { return __builtin_amdgcn_raw_buffer_load_b64(S.rs, (uint32_t)(a + c), 0, 0); };
   auto ld_q = [&](int c) {
-    return FULL ? __builtin_amdgcn_raw_buffer_load_b64(S.rq, (uint32_t)(a + c), 0, 0) : z;
+    QWin q;
+    q.m = v4u{0u, 0u, 0u, 0u};
+    q.lo = v2u{0u, 0u};
+    if (FULL) q.m = __builtin_amdgcn_raw_buffer_load_b128(S.rq, (uint32_t)(a + c - 8), 0, 0);
+    if (FULL && K > 9) q.lo = __builtin_amdgcn_raw_buffer_load_b64(S.rq, (uint32_t)(a + c - 16), 0, 0);
+    return q;
   };
-  v2u sA = ld_s(p0), qA = ld_q(p0), sB = ld_s(p0 + 8), qB = ld_q(p0 + 8);
+  // the second pair's offset is laundered: merged with the first into wider
+  // loads, it would leave the loop head waiting on the newest loads
+  v2u sA = ld_s(p0);
+  QWin qA = ld_q(p0);
+  // a read starting in the buffer's first 8 bytes: its first window would
+  // start before offset 0, and the range check zeroes the whole load — take
+  // [0, 16) and shift it into place (the bytes before 0 are never used)
+  if (FULL && a + p0 < 8) {
+    const v4u t = __builtin_amdgcn_raw_buffer_load_b128(S.rq, 0u, 0, 0);
+    const int sh = 8 * (8 - (a + p0));   // 8..64 bits
+    const uint64_t lo = ((uint64_t)t[1] << 32) | t[0], hi = ((uint64_t)t[3] << 32) | t[2];
+    const uint64_t nlo = sh == 64 ? 0ull : lo << sh;
+    const uint64_t nhi = sh == 64 ? lo : (hi << sh) | (lo >> (64 - sh));
+    qA.m = v4u{(uint32_t)nlo, (uint32_t)(nlo >> 32), (uint32_t)nhi, (uint32_t)(nhi >> 32)};
+  }
+  const int p8 = opaque(p0 + 8);
+  v2u sB = ld_s(p8);
+  QWin qB = ld_q(p8);
   // one exit (a second chunk past the end is all class 0)
   for (int c = p0; c < n; c += 16) {
-    run_chunk<K, FULL, UNCOND>(sA, qA, h1, h2, n - c, st, cnt, acc, ts, tq, sign, sub, words);
+    run_chunk<K, FULL, UNCOND>(sA, qA, n - c, st, cnt, acc, ts, tq, sign, sub, words);
     sA = ld_s(c + 16);
     qA = ld_q(c + 16);
-    run_chunk<K, FULL, UNCOND>(sB, qB, h1, h2, n - c - 8, st, cnt, acc, ts, tq, sign, sub, words);
+    run_chunk<K, FULL, UNCOND>(sB, qB, n - c - 8, st, cnt, acc, ts, tq, sign, sub, words);
     sB = ld_s(c + 24);
     qB = ld_q(c + 24);
   }
+}
+
+// Context replay, all reads valid: the context of read r is the kWarm bytes
+// [c, ar) before it in seq (reads are contiguous), so every lane runs the same
+// kWarm / 16 iterations.  Away from the clamp, f does not depend on the word
+// counter, so a chunk only moves f (4 FP64 ops per base); a chunk kHot flags
+// replays byte by byte with the counter rebuilt at its first byte and reset
+// at every read start (warm_exact).
+template <int K>
+__device__ __noinline__ State warm_exact(const Args &A, const Src &S, const uint8_t *cls,
+                                         int64_t r, int c, int end, State st) {
+  int64_t t = r - 1;
+  while (A.idx[t] > c) --t;   // the read holding byte c
+  int cnt = count_before<K>(A, S, cls, A.idx[t], c - A.idx[t]);
+  int nxt = A.idx[t + 1];
+  uint32_t acc = 0, words = 0;
+  for (int j = c; j < end; ++j) {
+    while (j == nxt) {   // read start: the counter resets (empty reads included)
+      cnt = 0;
+      ++t;
+      nxt = A.idx[t + 1];
+    }
+    step<K, false, false, true>(cls[(uint8_t)A.seq[j]], 0u, 0u, st, cnt, acc, nullptr, nullptr, 0u,
+                                0u, words);
+  }
+  return st;   // by value: a State behind a reference to a call would live in scratch
+}
+
+template <int K>
+__device__ __forceinline__ void warm_chunk(const Args &A, const Src &S, const uint8_t *cls,
+                                           int64_t r, v2u sv, int c, int end, State &st) {
+  const int left = end - c;
+  const uint64_t m = left >= 8 ? ~0ull : ((1ull << (8 * max(left, 0))) - 1);
+  if (__builtin_expect(hot<K>(st), 0)) {
+    if (left > 0) st = warm_exact<K>(A, S, cls, r, c, min(c + 8, end), st);
+    return;
+  }
+  const v2u cl = {classes4(sv.x & (uint32_t)m), classes4(sv.y & (uint32_t)(m >> 32))};
+#pragma unroll
+  for (int u = 0; u < 8; ++u) move<K>(byte_of(cl, u), st);
+}
+
+template <int K>
+__device__ State warm_contiguous(const Args &A, const Src &S, const uint8_t *cls, int64_t r) {
+  constexpr double half = (double)(1 << K) * 0.5;   // :107-108
+  State st = {half, half};
+  const int ar = A.idx[r];
+  const int c0 = max(A.idx[0], ar - kWarm);   // at the batch start: exact
+  auto ld = [&](int c) { return __builtin_amdgcn_raw_buffer_load_b64(S.rs, (uint32_t)c, 0, 0); };
+  v2u sA = ld(c0), sB = ld(opaque(c0 + 8));   // two loads, see run_read
+  for (int c = c0; c < ar; c += 16) {
+    warm_chunk<K>(A, S, cls, r, sA, c, ar, st);
+    sA = ld(c + 16);
+    warm_chunk<K>(A, S, cls, r, sB, c + 8, ar, st);
+    sB = ld(c + 24);
+  }
+  return st;
 }
 
 // the entry state guess for read r: replay the kWarm bytes of (valid) context
@@ -302,6 +404,7 @@ __device__ State guess_entry(const Args &A, const Src &S, const uint8_t *cls, in
   constexpr double half = (double)(1 << K) * 0.5;   // :107-108
   State st = {half, half};
   if (r == 0) return st;
+  if (A.mode != HPGQ_CGR_ONLY_VALID_READS) return warm_contiguous<K>(A, S, cls, r);
   // common case: the previous read alone holds kWarm bytes
   const int ap = A.idx[r - 1], ar = A.idx[r];
   int64_t t;

@@ -20,6 +20,7 @@ ap.add_argument("--reads", type=int, default=10_000_000)
 ap.add_argument("--iters", type=int, default=5)
 ap.add_argument("--mode", default="c2")
 ap.add_argument("--L", type=int, default=150)
+ap.add_argument("--k", type=int, default=7)
 args = ap.parse_args()
 
 dev = torch.device("cuda", 0)
@@ -36,7 +37,7 @@ if args.mode == "cgr":
     H.check(H.lib.hpgq_synth_device(C.byref(s), 0, n, sq.data_ptr(), ql.data_ptr(),
                                     ix.data_ptr(), None), "synth")
     torch.cuda.synchronize()
-    cg = H.ChaosGame(7)
+    cg = H.ChaosGame(args.k)
     b = H.engine.device_batch(n, sq.data_ptr(), ql.data_ptr(), ix.data_ptr())
     for _ in range(args.iters):
         cg.fill_device(b)
