@@ -42,6 +42,10 @@ namespace cgr {
 constexpr double kEps = 0.00001;   // old/chaos_game.h:41
 constexpr int kWG = 1024;       // 16 waves share one set of LDS tables (128 KB at k = 7)
 constexpr int kWarm = 128;         // bytes of context replayed to guess a read's entry state
+#ifndef HPGQ_CGR_RING
+#define HPGQ_CGR_RING 4
+#endif
+constexpr int kRing = HPGQ_CGR_RING;   // 8-byte chunks in flight per lane (run_read, warm)
 constexpr int kLdsMaxK = 7;        // 2 x 4^7 x 4 B = 128 KB of LDS tables
 
 typedef unsigned v2u __attribute__((ext_vector_type(2)));
@@ -186,6 +190,9 @@ __device__ __forceinline__ void step(uint32_t fl, uint32_t qb, uint32_t qold, St
     if (UNCOND) {
       const uint32_t cell = word ? (uint32_t)(cx * dim + cy) : (uint32_t)(dim * dim);
       const uint64_t inc = ((uint64_t)acc << 32) | 1u;
+#if HPGQ_CGR_ABL == 1   // timing probe only: the table add skipped
+      if (__builtin_expect(sub == 0xDEADBEEFu, 0))
+#endif
       atomicAdd(reinterpret_cast<unsigned long long *>(ts) + cell, (unsigned long long)inc);
     } else if (word) {
       const int cell = cx * dim + cy;
@@ -293,8 +300,8 @@ __device__ __forceinline__ void run_chunk(v2u sv, const QWin &q, int left, State
 }
 
 // Run read [a, a+n) from byte p0 (word counter cnt0) with state st.  The
-// next two chunks' loads are issued before a chunk is processed; each buffer
-// register is reloaded right after its chunk is consumed.
+// next kRing chunks' loads are in flight while a chunk is processed; each
+// buffer register is reloaded right after its chunk is consumed.
 template <int K, bool FULL, bool UNCOND>
 __device__ void run_read(const Args &A, const Src &S, int a, int n, int p0, int cnt0, State &st,
                          uint32_t *ts, uint32_t *tq, uint32_t sign, uint32_t &words) {
@@ -310,10 +317,18 @@ __device__ void run_read(const Args &A, const Src &S, int a, int n, int p0, int 
     if (FULL && K > 9) q.lo = __builtin_amdgcn_raw_buffer_load_b64(S.rq, (uint32_t)(a + c - 16), 0, 0);
     return q;
   };
-  // the second pair's offset is laundered: merged with the first into wider
-  // loads, it would leave the loop head waiting on the newest loads
-  v2u sA = ld_s(p0);
-  QWin qA = ld_q(p0);
+  // kRing chunks in flight per lane: a lane enters a new 128-byte line every
+  // 16 chunks and the wave waits for its slowest lane, so some lane takes an
+  // HBM miss in most chunks.  Offsets after the first are laundered: merged
+  // into wider loads, the loop head would wait on the newest loads.
+  v2u sv[kRing];
+  QWin qv[kRing];
+#pragma unroll
+  for (int i = 0; i < kRing; ++i) {
+    const int o = i ? opaque(p0 + 8 * i) : p0;
+    sv[i] = ld_s(o);
+    qv[i] = ld_q(o);
+  }
   // a read starting in the buffer's first 8 bytes: its first window would
   // start before offset 0, and the range check zeroes the whole load — take
   // [0, 16) and shift it into place (the bytes before 0 are never used)
@@ -323,19 +338,16 @@ __device__ void run_read(const Args &A, const Src &S, int a, int n, int p0, int 
     const uint64_t lo = ((uint64_t)t[1] << 32) | t[0], hi = ((uint64_t)t[3] << 32) | t[2];
     const uint64_t nlo = sh == 64 ? 0ull : lo << sh;
     const uint64_t nhi = sh == 64 ? lo : (hi << sh) | (lo >> (64 - sh));
-    qA.m = v4u{(uint32_t)nlo, (uint32_t)(nlo >> 32), (uint32_t)nhi, (uint32_t)(nhi >> 32)};
+    qv[0].m = v4u{(uint32_t)nlo, (uint32_t)(nlo >> 32), (uint32_t)nhi, (uint32_t)(nhi >> 32)};
   }
-  const int p8 = opaque(p0 + 8);
-  v2u sB = ld_s(p8);
-  QWin qB = ld_q(p8);
-  // one exit (a second chunk past the end is all class 0)
-  for (int c = p0; c < n; c += 16) {
-    run_chunk<K, FULL, UNCOND>(sA, qA, n - c, st, cnt, acc, ts, tq, sign, sub, words);
-    sA = ld_s(c + 16);
-    qA = ld_q(c + 16);
-    run_chunk<K, FULL, UNCOND>(sB, qB, n - c - 8, st, cnt, acc, ts, tq, sign, sub, words);
-    sB = ld_s(c + 24);
-    qB = ld_q(c + 24);
+  // one exit (chunks past the end are all class 0)
+  for (int c = p0; c < n; c += 8 * kRing) {
+#pragma unroll
+    for (int i = 0; i < kRing; ++i) {
+      run_chunk<K, FULL, UNCOND>(sv[i], qv[i], n - c - 8 * i, st, cnt, acc, ts, tq, sign, sub, words);
+      sv[i] = ld_s(c + 8 * (i + kRing));
+      qv[i] = ld_q(c + 8 * (i + kRing));
+    }
   }
 }
 
@@ -386,12 +398,15 @@ __device__ State warm_contiguous(const Args &A, const Src &S, const uint8_t *cls
   const int ar = A.idx[r];
   const int c0 = max(A.idx[0], ar - kWarm);   // at the batch start: exact
   auto ld = [&](int c) { return __builtin_amdgcn_raw_buffer_load_b64(S.rs, (uint32_t)c, 0, 0); };
-  v2u sA = ld(c0), sB = ld(opaque(c0 + 8));   // two loads, see run_read
-  for (int c = c0; c < ar; c += 16) {
-    warm_chunk<K>(A, S, cls, r, sA, c, ar, st);
-    sA = ld(c + 16);
-    warm_chunk<K>(A, S, cls, r, sB, c + 8, ar, st);
-    sB = ld(c + 24);
+  v2u sv[kRing];   // see run_read
+#pragma unroll
+  for (int i = 0; i < kRing; ++i) sv[i] = ld(i ? opaque(c0 + 8 * i) : c0);
+  for (int c = c0; c < ar; c += 8 * kRing) {
+#pragma unroll
+    for (int i = 0; i < kRing; ++i) {
+      warm_chunk<K>(A, S, cls, r, sv[i], c + 8 * i, ar, st);
+      sv[i] = ld(c + 8 * (i + kRing));
+    }
   }
   return st;
 }
@@ -404,6 +419,9 @@ __device__ State guess_entry(const Args &A, const Src &S, const uint8_t *cls, in
   constexpr double half = (double)(1 << K) * 0.5;   // :107-108
   State st = {half, half};
   if (r == 0) return st;
+#if HPGQ_CGR_ABL == 2   // timing probe only: no context replay
+  if (A.num_reads > 0) return st;
+#endif
   if (A.mode != HPGQ_CGR_ONLY_VALID_READS) return warm_contiguous<K>(A, S, cls, r);
   // common case: the previous read alone holds kWarm bytes
   const int ap = A.idx[r - 1], ar = A.idx[r];
