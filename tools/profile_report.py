@@ -24,21 +24,55 @@ PROF = os.path.join(ROOT, "gpurun_out", "prof")
 OUT = os.path.join(ROOT, "profiles")
 
 
-def counters(sub, kern):
+KERNELS = {"c2": ("engine_tri_kernel", "engine_kernel", "trim_kernel"),
+           "c3": ("engine_tri_kernel", "engine_kernel", "trim_kernel"),
+           "c4": ("engine_tri_kernel", "engine_kernel", "trim_kernel"),
+           "c5": ("cgr_fill_kernel", "cgr_check_kernel", "cgr_fix_kernel")}
+
+
+def counters(sub, kerns):
+    """Per-launch sums: the last dispatch of every kernel the library call runs."""
+    if isinstance(kerns, str):
+        kerns = (kerns,)
     f = glob.glob(os.path.join(PROF, sub, "**", "run_counter_collection.csv"), recursive=True)
     if not f:
         return {}, None
-    rows = [r for r in csv.DictReader(open(f[0])) if kern in r["Kernel_Name"]]
+    rows = [r for r in csv.DictReader(open(f[0])) if any(k in r["Kernel_Name"] for k in kerns)]
     if not rows:
         return {}, None
-    last = max(int(r["Dispatch_Id"]) for r in rows)
-    agg = collections.defaultdict(float)
-    name = None
+    last = {}
     for r in rows:
-        if int(r["Dispatch_Id"]) == last:
+        last[r["Kernel_Name"]] = max(last.get(r["Kernel_Name"], -1), int(r["Dispatch_Id"]))
+    agg = collections.defaultdict(float)
+    for r in rows:
+        if int(r["Dispatch_Id"]) == last[r["Kernel_Name"]]:
             agg[r["Counter_Name"]] += float(r["Counter_Value"])
-            name = r["Kernel_Name"]
-    return dict(agg), name
+    return dict(agg), " + ".join(sorted(last))
+
+
+def bench_line(path):
+    if not os.path.exists(path):
+        return None
+    lines = open(path).read().strip().splitlines()
+    return json.loads(lines[-1]) if lines else None
+
+
+def config_record(rnd, cfg):
+    b = bench_line(os.path.join(PROF, f"bench_{cfg}.json"))
+    fetch, kname = counters(f"fetch_{cfg}", KERNELS[cfg])
+    write, _ = counters(f"write_{cfg}", KERNELS[cfg])
+    if not (b and fetch and write):
+        return None
+    rec = {"round": rnd, "config": cfg, "kernel_symbols": kname,
+           "batch_reads": b["config"]["batch_reads"], "kernel": b["roofline"]["kernel"],
+           "alg_bytes_per_launch": b["roofline"]["alg_bytes_per_launch"],
+           "source": "tools/gpu_profile.sh; rocprofv3 --kernel-trace --pmc, one counter per pass, "
+                     "last dispatch of each kernel of one library call (tools/prof_engine.py)",
+           "FETCH_SIZE_kB": fetch.get("FETCH_SIZE"), "fetch_bytes_x2": int(fetch["FETCH_SIZE"] * 1024 * 2),
+           "WRITE_SIZE_kB": write.get("WRITE_SIZE"), "write_bytes": int(write["WRITE_SIZE"] * 1024)}
+    rec["hbm_bytes_per_launch"] = rec["fetch_bytes_x2"] + rec["write_bytes"]
+    rec["traffic_over_alg"] = round(rec["hbm_bytes_per_launch"] / rec["alg_bytes_per_launch"], 4)
+    return rec
 
 
 def main():
@@ -53,38 +87,24 @@ def main():
         for r in csv.DictReader(open(stats[0])):
             if a.kernel in r["Name"]:
                 print("kernel-trace avg ns:", r["AverageNs"], "calls", r["Calls"])
-    bench = os.path.join(PROF, "bench.json")
-    if os.path.exists(bench):
-        line = open(bench).read().strip().splitlines()[-1]
-        b = json.loads(line)
+    b = bench_line(os.path.join(PROF, "bench.json"))
+    if b:
         json.dump(b, open(os.path.join(OUT, f"{a.round}_bench.json"), "w"), indent=1)
         print("bench value", b["value"], "avg_launch_us", b["roofline"]["avg_launch_us"])
-    else:
-        b = None
-    fetch, kname = counters("fetch", a.kernel)
-    write, _ = counters("write", a.kernel)
-    sq1, _ = counters("sq1", a.kernel)
-    sq2, _ = counters("sq2", a.kernel)
-    rec = {"round": a.round, "kernel_symbol": kname, "batch_reads": 10_000_000,
-           "source": "tools/gpu_profile.sh; rocprofv3 --kernel-trace --pmc, one counter group "
-                     "per pass, last dispatch of tools/prof_engine.py --mode c2"}
-    if b:
-        rec["kernel"] = b["roofline"]["kernel"]
-        rec["alg_bytes_per_launch"] = b["roofline"]["alg_bytes_per_launch"]
-    if fetch:
-        rec["FETCH_SIZE_kB"] = fetch.get("FETCH_SIZE")
-        rec["fetch_bytes_x2"] = int(fetch["FETCH_SIZE"] * 1024 * 2)
-    if write:
-        rec["WRITE_SIZE_kB"] = write.get("WRITE_SIZE")
-        rec["write_bytes"] = int(write["WRITE_SIZE"] * 1024)
-    if fetch and write:
-        rec["hbm_bytes_per_launch"] = rec["fetch_bytes_x2"] + rec["write_bytes"]
-        if b:
-            rec["traffic_over_alg"] = round(rec["hbm_bytes_per_launch"] / rec["alg_bytes_per_launch"], 4)
-    rec["sq"] = {**sq1, **sq2}
-    for name in (f"{a.round}_pmc_engine_c2.json", "pmc_engine_c2.json"):
-        json.dump(rec, open(os.path.join(OUT, name), "w"), indent=1)
-    print(json.dumps({k: v for k, v in rec.items() if k != "sq"}, indent=1))
+    for cfg in KERNELS:
+        rec = config_record(a.round, cfg)
+        if rec is None:
+            continue
+        if cfg == "c2":
+            sq1, _ = counters("sq1", a.kernel)
+            sq2, _ = counters("sq2", a.kernel)
+            rec["sq"] = {**sq1, **sq2}
+        cb = bench_line(os.path.join(PROF, f"bench_{cfg}.json"))
+        if cb:
+            json.dump(cb, open(os.path.join(OUT, f"{a.round}_bench_{cfg}.json"), "w"), indent=1)
+        for name in (f"{a.round}_pmc_engine_{cfg}.json", f"pmc_engine_{cfg}.json"):
+            json.dump(rec, open(os.path.join(OUT, name), "w"), indent=1)
+        print(cfg, json.dumps({k: v for k, v in rec.items() if k != "sq"}))
 
 
 if __name__ == "__main__":
