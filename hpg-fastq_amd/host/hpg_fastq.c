@@ -58,7 +58,13 @@ int main(int argc, char **argv) {
     if (!f || fwrite(counters, sizeof(uint64_t), clen, f) != clen) rc = 1;
     if (f) fclose(f);
   }
-  if (cmd == CMD_STATS && cli_report(o, &p, counters)) rc = 1;
+  if (o->kmers_out && r.kmers) {
+    const size_t kn = (size_t)HPGQ_NUM_KMERS * (size_t)r.kmers_npos;
+    FILE *f = fopen(o->kmers_out, "wb");
+    if (!f || fwrite(r.kmers, sizeof(uint64_t), kn, f) != kn) rc = 1;
+    if (f) fclose(f);
+  }
+  if (cmd == CMD_STATS && cli_report(o, &p, counters, &r)) rc = 1;
 
   if (!o->quiet) {
     printf("\n\nRESULTS\n");
@@ -91,6 +97,7 @@ int main(int argc, char **argv) {
     printf("=================================================\n");
   }
   free(counters);
+  free(r.kmers);
   cli_free(o);
   return rc;
 }

@@ -44,6 +44,7 @@ typedef struct {
   int chunk_mb;             /* FASTQ text per parse unit */
   int print_params;         /* print hpgq_params_t and exit (no device) */
   char *counters_out;       /* raw u64 counter dump (tests) */
+  char *kmers_out;          /* raw u64 k-mer table dump (tests) */
   int quiet;
 } cli_options_t;
 
@@ -61,11 +62,14 @@ int cli_parse_range(int *min, int *max, const char *range, const char *msg);
 typedef struct {
   uint64_t num_reads, num_passed, num_failed, num_edited;
   double seconds, fastq_bytes;
+  uint64_t *kmers;          /* --kmers: by_pos [HPGQ_NUM_KMERS][kmers_npos] (malloc'd) */
+  int kmers_npos;
 } cli_result_t;
 
 int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, cli_result_t *res);
 
-/* src/stats_report.c: summary + data files */
-int cli_report(const cli_options_t *o, const hpgq_params_t *p, const uint64_t *counters);
+/* src/stats_report.c: summary + data files (+ k-mer files when res->kmers) */
+int cli_report(const cli_options_t *o, const hpgq_params_t *p, const uint64_t *counters,
+               const cli_result_t *res);
 
 #endif

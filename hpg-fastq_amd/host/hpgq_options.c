@@ -5,7 +5,7 @@
  * src/stats_options.c:15-300, src/filter_options.c:15-258,
  * src/edit_options.c:15-290; parse_range src/commons_fastq.c:31-103.
  * Build-specific additions: --gpu, --lmax, --chunk-mb, --print-params,
- * --counters-out, --quiet.  --quality-encoding is accepted by every command
+ * --counters-out, --kmers-out, --quiet.  --quality-encoding is accepted by every command
  * (quirk Q11).
  */
 #define _GNU_SOURCE
@@ -90,6 +90,8 @@ static void usage(const cli_options_t *o) {
   printf("  --chunk-mb=<int>                FastQ text per GPU parse unit (default 256)\n");
   printf("  --print-params                  Print the engine parameters and exit\n");
   printf("  --counters-out=<file>           Write the raw u64 counter set\n");
+  if (o->command == CMD_STATS)
+    printf("  --kmers-out=<file>              Write the raw u64 k-mer table [1024][lmax-4]\n");
   printf("  --quiet                         No parameter / result display\n");
   exit(-1);
 }
@@ -101,7 +103,8 @@ static int exists(const char *path) {
 
 enum {
   O_THREADS = 1000, O_BATCH, O_QENC, O_KMERS, O_LRANGE, O_QRANGE, O_LLEN, O_LQRANGE, O_RLEN,
-  O_RQRANGE, O_MAXN, O_MAXOOQ, O_GPU, O_LMAX, O_CHUNK, O_PRINT, O_COUNTERS, O_QUIET
+  O_RQRANGE, O_MAXN, O_MAXOOQ, O_GPU, O_LMAX, O_CHUNK, O_PRINT, O_COUNTERS, O_QUIET,
+  O_KMERSOUT
 };
 
 cli_options_t *cli_parse(int command, const char *exec_name, int argc, char **argv) {
@@ -140,6 +143,7 @@ cli_options_t *cli_parse(int command, const char *exec_name, int argc, char **ar
       {"chunk-mb", required_argument, 0, O_CHUNK},
       {"print-params", no_argument, 0, O_PRINT},
       {"counters-out", required_argument, 0, O_COUNTERS},
+      {"kmers-out", required_argument, 0, O_KMERSOUT},
       {"quiet", no_argument, 0, O_QUIET},
       {0, 0, 0, 0}};
   if (argc < 2) usage(o);
@@ -170,13 +174,10 @@ cli_options_t *cli_parse(int command, const char *exec_name, int argc, char **ar
       case O_CHUNK: o->chunk_mb = atoi(optarg); break;
       case O_PRINT: o->print_params = 1; break;
       case O_COUNTERS: o->counters_out = strdup(optarg); break;
+      case O_KMERSOUT: o->kmers_out = strdup(optarg); break;
       case O_QUIET: o->quiet = 1; break;
       default: usage(o);
     }
-  }
-  if (o->kmers_on) {
-    printf("\nError: --kmers is not available in this build (DESIGN.md §7)\n");
-    exit(-1);
   }
   /* validation, src/stats_options.c:108-160 */
   if (!o->print_params && !exists(o->in_filename)) {
@@ -339,5 +340,6 @@ void cli_free(cli_options_t *o) {
   free(o->left_quality_range);
   free(o->right_quality_range);
   free(o->counters_out);
+  free(o->kmers_out);
   free(o);
 }

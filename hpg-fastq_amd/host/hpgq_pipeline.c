@@ -280,8 +280,12 @@ int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, 
 
   hpgq_ctx_t *ctx = NULL;
   hpgq_parser_t *ps = NULL;
+  hpgq_kmers_t *km = NULL;
   int rc = hpgq_open(&ctx, o->device, p);
   if (rc == 0) rc = hpgq_parser_open(&ps, o->device, hpgq_stream(ctx));
+  /* --kmers counts the reads the stats merge (passed ones when filtering,
+   * src/stats_fastq.c:268-272,384-410) on the engine's stream, after it */
+  if (rc == 0 && o->kmers_on) rc = hpgq_kmers_open(&km, o->device, p->lmax, hpgq_stream(ctx));
   const size_t chunk = (size_t)o->chunk_mb << 20;
   for (int i = 0; i < NSLOTS && rc == 0; ++i) {
     P.slot[i].cap = chunk + MAX_CARRY;
@@ -293,6 +297,7 @@ int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, 
   size_t dcap = 0;
   const int writes = o->command != CMD_STATS;
   const int edit = o->command == CMD_EDIT;
+  const int need_mask = writes || (km && o->filter_on);
   if (rc == 0 && writes) {
     char path[4096];
     snprintf(path, sizeof(path), "%s/%s.fq", o->out_dirname, edit ? "edit" : "passed");
@@ -322,14 +327,15 @@ int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, 
     hpgq_batch_t b;
     rc = hpgq_parse_host(ps, s->buf, (int64_t)s->use, &b);
     if (rc == 0 && b.num_reads > 0) {
-      if (writes && (size_t)b.num_reads > dcap) {
+      if (need_mask && (size_t)b.num_reads > dcap) {
         hpgq_device_free(d_mask);
         hpgq_device_free(d_trim);
         dcap = (size_t)b.num_reads + (size_t)b.num_reads / 4 + 1024;
         rc = hpgq_device_alloc(o->device, (void **)&d_mask, dcap);
         if (rc == 0) rc = hpgq_device_alloc(o->device, (void **)&d_trim, dcap * 4);
       }
-      if (rc == 0) rc = hpgq_run_device(ctx, &b, NULL, writes ? d_mask : NULL, edit ? d_trim : NULL);
+      if (rc == 0) rc = hpgq_run_device(ctx, &b, NULL, need_mask ? d_mask : NULL, edit ? d_trim : NULL);
+      if (rc == 0 && km) rc = hpgq_kmers_count_device(km, &b, o->filter_on ? d_mask : NULL);
       if (rc == 0 && writes) {
         s->nreads = b.num_reads;
         if (ensure_results(s, b.num_reads)) rc = HPGQ_E_NOMEM;
@@ -358,6 +364,11 @@ int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, 
   if (rc == 0 && P.error) rc = P.error < 0 && P.error != HPGQ_E_FORMAT ? HPGQ_E_INVALID : P.error;
   if (rc == 0) rc = hpgq_sync(ctx);   /* surfaces HPGQ_E_READ_TOO_LONG */
   if (rc == 0) rc = hpgq_read_counters(ctx, counters, hpgq_counters_size(ctx));
+  if (rc == 0 && km) {
+    res->kmers_npos = p->lmax > HPGQ_KMER_K - 1 ? p->lmax - (HPGQ_KMER_K - 1) : 0;
+    res->kmers = calloc(hpgq_kmers_size(km) + 1, sizeof(uint64_t));
+    rc = res->kmers ? hpgq_kmers_read(km, res->kmers, hpgq_kmers_size(km)) : HPGQ_E_NOMEM;
+  }
   res->seconds = now_s() - t0;
   if (rc == 0) {
     res->num_passed = counters[HPGQ_S_NUM_PASSED];
@@ -382,6 +393,7 @@ done:
   }
   free(P.carry);
   hpgq_parser_close(ps);
+  hpgq_kmers_close(km);
   hpgq_close(ctx);
   close(P.fd);
   return rc;

@@ -5,7 +5,8 @@
  * (:159-180), <in>.read.quality.histogram.data (:363-390),
  * <in>.GC.histogram.data (:215-232), <in>.GC.per.nt.data (:268-285),
  * <in>.quality.per.nt.data (final form, quirk Q6: :306-322),
- * <in>.nucleotides.data (:336-352).  Values come from the dense device
+ * <in>.nucleotides.data (:336-352), and with --kmers <in>.kmers.txt and
+ * <in>.kmers.per.nt.data (:492-530) plus the summary's k-mer list (:144-150).  Values come from the dense device
  * counters: per-position maps are read by position, not by
  * khash bucket (quirk Q3); the mean quality is the exact fixed-point mean
  * (quirk Q2).  The gnuplot images are not produced (gnuplot is absent).
@@ -25,7 +26,72 @@ static FILE *open_out(const cli_options_t *o, const char *base, const char *suff
   return fopen(path, "w");
 }
 
-int cli_report(const cli_options_t *o, const hpgq_params_t *p, const uint64_t *c) {
+/* --kmers: k-mers ordered by count, descending; ties by id (kmers_sort in the
+ * absent bioinfo-libs, src/stats_fastq.c:481 -> build-defined) */
+typedef struct {
+  uint64_t count;
+  int id;
+  int size;   /* 1 + last start position with a nonzero count (counter_by_pos_size) */
+} kmer_row_t;
+
+static int kmer_cmp(const void *a, const void *b) {
+  const kmer_row_t *x = a, *y = b;
+  if (x->count != y->count) return x->count > y->count ? -1 : 1;
+  return x->id - y->id;
+}
+
+static void kmer_string(int id, char out[HPGQ_KMER_K + 1]) {   /* kmers_string, :479 */
+  for (int i = 0; i < HPGQ_KMER_K; ++i) out[i] = "ACGT"[(id >> (2 * (HPGQ_KMER_K - 1 - i))) & 3];
+  out[HPGQ_KMER_K] = 0;
+}
+
+static kmer_row_t *kmer_rows(const cli_result_t *res) {
+  kmer_row_t *rows = calloc(HPGQ_NUM_KMERS, sizeof(kmer_row_t));
+  if (!rows) return NULL;
+  for (int id = 0; id < HPGQ_NUM_KMERS; ++id) {
+    const uint64_t *bp = res->kmers + (size_t)id * res->kmers_npos;
+    rows[id].id = id;
+    for (int j = 0; j < res->kmers_npos; ++j) {
+      rows[id].count += bp[j];
+      if (bp[j]) rows[id].size = j + 1;
+    }
+  }
+  qsort(rows, HPGQ_NUM_KMERS, sizeof(kmer_row_t), kmer_cmp);
+  return rows;
+}
+
+/* report_kmers, src/stats_report.c:492-530: <in>.kmers.txt (all 1024 by
+ * count) and <in>.kmers.per.nt.data (the top 5 per start position; rows past a
+ * k-mer's size read 0 instead of the reference's index-`size` read, quirk Q10) */
+static int report_kmers(const cli_options_t *o, const char *base, const cli_result_t *res,
+                        const kmer_row_t *rows) {
+  char ks[HPGQ_KMER_K + 1];
+  FILE *f = open_out(o, base, "kmers.txt");
+  if (!f) return -1;
+  fprintf(f, "# Sequence\tCount\n");
+  for (int i = 0; i < HPGQ_NUM_KMERS; i++) {
+    kmer_string(rows[i].id, ks);
+    fprintf(f, "%s\t%lu\n", ks, (unsigned long)rows[i].count);
+  }
+  fclose(f);
+  if (!(f = open_out(o, base, "kmers.per.nt.data"))) return -1;
+  int num_cols = 0;
+  for (int i = 0; i < 5; i++)
+    if (num_cols < rows[i].size) num_cols = rows[i].size;
+  for (int i = 0; i < num_cols; i++) {
+    fprintf(f, "%i", i + 1);
+    for (int t = 0; t < 5; t++) {
+      const uint64_t v = i < rows[t].size ? res->kmers[(size_t)rows[t].id * res->kmers_npos + i] : 0;
+      fprintf(f, "\t%lu", (unsigned long)v);
+    }
+    fprintf(f, "\n");
+  }
+  fclose(f);
+  return 0;
+}
+
+int cli_report(const cli_options_t *o, const hpgq_params_t *p, const uint64_t *c,
+               const cli_result_t *res) {
   const int lmax = p->lmax, phred = p->phred;
   const char *slash = strrchr(o->in_filename, '/');
   const char *base = slash ? slash + 1 : o->in_filename;
@@ -95,7 +161,23 @@ int cli_report(const cli_options_t *o, const hpgq_params_t *p, const uint64_t *c
     if ((k + 1) % 5 == 0) fprintf(f, "\n");
   }
   fprintf(f, "\n");
+  kmer_row_t *krows = res && res->kmers ? kmer_rows(res) : NULL;
+  if (krows) {   /* :144-150 (21 rows there; the header's 20 here, quirk Q10) */
+    char ks[HPGQ_KMER_K + 1];
+    fprintf(f, "K-mers (top 20)\n");
+    fprintf(f, "\tSequence\tCount\n");
+    for (int i = 0; i < 20; i++) {
+      kmer_string(krows[i].id, ks);
+      fprintf(f, "\t%s\t\t%lu\n", ks, (unsigned long)krows[i].count);
+    }
+  }
   fclose(f);
+  if (krows && report_kmers(o, base, res, krows)) {
+    free(krows);
+    free(cnt);
+    return -1;
+  }
+  free(krows);
 
   if ((f = open_out(o, base, "length.histogram.data"))) {
     for (int i = 1; i <= maxlen; i++) fprintf(f, "%i\t%lu\n", i, (unsigned long)hl[i]);

@@ -12,5 +12,5 @@ from ._abi import (  # noqa: F401
     NO_VALUE, MIN_VALUE, MAX_VALUE, LMAX_LIMIT, DEVICE_SLACK, CGR_ALL_READS, CGR_ONLY_VALID_READS,
     counters_len, layout, check, params_default, exported_symbols,
 )
-from .engine import Engine, ChaosGame, Parser, summary, complete_prefix  # noqa: F401
+from .engine import Engine, ChaosGame, Kmers, Parser, summary, complete_prefix  # noqa: F401
 from .options import parse_range, filter_params, edit_params, stats_params  # noqa: F401

@@ -114,6 +114,14 @@ _SIGS = [
     ("hpgq_cgr_read", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     ("hpgq_cgr_stream", C.c_void_p, [C.c_void_p]),
     ("hpgq_cgr_last_replays", C.c_int64, [C.c_void_p]),
+    ("hpgq_kmers_open", C.c_int, [C.POINTER(C.c_void_p), C.c_int, C.c_int, C.c_void_p]),
+    ("hpgq_kmers_close", None, [C.c_void_p]),
+    ("hpgq_kmers_count_device", C.c_int, [C.c_void_p, C.POINTER(Batch), C.c_void_p]),
+    ("hpgq_kmers_sync", C.c_int, [C.c_void_p]),
+    ("hpgq_kmers_reset", C.c_int, [C.c_void_p]),
+    ("hpgq_kmers_size", C.c_size_t, [C.c_void_p]),
+    ("hpgq_kmers_read", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
+    ("hpgq_kmers_device", C.c_void_p, [C.c_void_p]),
     ("hpgq_synth_length", C.c_int32, [C.POINTER(Synth), C.c_int64]),
     ("hpgq_synth_indices_host", C.c_int, [C.POINTER(Synth), C.c_int64, C.c_int64, C.c_void_p]),
     ("hpgq_synth_device", C.c_int, [C.POINTER(Synth), C.c_int64, C.c_int64, C.c_void_p,

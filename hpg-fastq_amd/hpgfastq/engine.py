@@ -168,6 +168,44 @@ class ChaosGame:
         return ts.reshape(self.dim, self.dim), tq.reshape(self.dim, self.dim), int(wc[0])
 
 
+class Kmers:
+    """hpgq_kmers: `stats --kmers` 5-mer counts per start position
+    (merge src/stats_fastq.c:384-410; build-defined per-read rule)."""
+
+    def __init__(self, lmax, device=0, stream=None):
+        self.lmax = lmax
+        self.npos = max(lmax - 4, 0)
+        h = C.c_void_p()
+        check(lib.hpgq_kmers_open(C.byref(h), device, lmax, stream), "hpgq_kmers_open")
+        self._h = h
+
+    def close(self):
+        if self._h:
+            lib.hpgq_kmers_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def count_device(self, batch, mask_ptr=None):
+        check(lib.hpgq_kmers_count_device(self._h, C.byref(batch), mask_ptr),
+              "hpgq_kmers_count_device")
+
+    def sync(self):
+        check(lib.hpgq_kmers_sync(self._h), "hpgq_kmers_sync")
+
+    def reset(self):
+        check(lib.hpgq_kmers_reset(self._h), "hpgq_kmers_reset")
+
+    def by_pos(self):
+        out = np.zeros((1024, self.npos), dtype=np.uint64)
+        check(lib.hpgq_kmers_read(self._h, _ptr(out), out.size), "hpgq_kmers_read")
+        return out
+
+
 def complete_prefix(buf, at_eof=False):
     """hpgq_fastq_complete_prefix: bytes of `buf` holding whole FASTQ records."""
     return int(lib.hpgq_fastq_complete_prefix(buf, len(buf), 1 if at_eof else 0))

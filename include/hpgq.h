@@ -281,6 +281,40 @@ void *hpgq_cgr_stream(hpgq_cgr_t *cg);
 int64_t hpgq_cgr_last_replays(hpgq_cgr_t *cg);
 
 /* ---------------------------------------------------------------------- */
+/* stats --kmers: 5-mer counts (src/stats_options.c:274, merge              */
+/* src/stats_fastq.c:384-410, report src/stats_report.c:492-563)            */
+/* ---------------------------------------------------------------------- */
+
+#define HPGQ_KMER_K    5
+#define HPGQ_NUM_KMERS 1024   /* NUM_KMERS, src/stats_fastq.h:58 */
+
+/*
+ * Build-defined (the per-read k-mer code is in the absent bioinfo-libs;
+ * DESIGN.md §2.6): 5-mers of exact uppercase A/C/G/T, id = sum code_i *
+ * 4^(4-i) with A=0 C=1 G=2 T=3, counted at every start position
+ * p <= len-5 (p < lmax-4) of every counted read.  by_pos is
+ * [HPGQ_NUM_KMERS][lmax-4] u64 (counter_by_pos); a k-mer's counter is its row
+ * sum.
+ */
+typedef struct hpgq_kmers hpgq_kmers_t;
+
+/* stream: run on this HIP stream (e.g. hpgq_stream(ctx), so counting sees the
+ * engine's mask of the same batch), or NULL for an own stream */
+int  hpgq_kmers_open(hpgq_kmers_t **km, int device, int lmax, void *stream);
+void hpgq_kmers_close(hpgq_kmers_t *km);
+/* Count a DEVICE batch, async; mask (device, may be NULL): only reads with
+ * mask[i] == 1 (the engine's mask_out: passed) are counted. */
+int  hpgq_kmers_count_device(hpgq_kmers_t *km, const hpgq_batch_t *b, const uint8_t *mask);
+int  hpgq_kmers_sync(hpgq_kmers_t *km);
+int  hpgq_kmers_reset(hpgq_kmers_t *km);
+/* HPGQ_NUM_KMERS * (lmax-4) (0 when lmax < 5) */
+size_t hpgq_kmers_size(const hpgq_kmers_t *km);
+/* copy by_pos to host (synchronises); n >= hpgq_kmers_size() */
+int  hpgq_kmers_read(hpgq_kmers_t *km, uint64_t *by_pos, size_t n);
+/* device pointer of by_pos (for an external all-reduce) */
+uint64_t *hpgq_kmers_device(hpgq_kmers_t *km);
+
+/* ---------------------------------------------------------------------- */
 /* FASTQ text -> device batch (the parsing half of the producer's          */
 /* fastq_fread_se, src/stats_fastq.c:183, moved onto the GPU)              */
 /* ---------------------------------------------------------------------- */

@@ -16,6 +16,8 @@
  *     derived from the call sites and help texts cited inline.
  *     -> "parity unpinned": the reference holds no tests, fixtures or golden
  *        vectors for this path, and its CPU path cannot be built here.
+ *   - --kmers (§8f rank 2): build-defined 5-mer counts;
+ *     the per-read k-mer code is in the same absent bioinfo-libs -> unpinned.
  *   - CGR (A7): line-by-line restatement of chaos_game_fill_tables,
  *     old/chaos_game.c:165-267.  The reference file needs an absent header
  *     (qc_batch.h) so it is not built here -> also "parity unpinned".
@@ -379,6 +381,44 @@ int oracle_cgr_fill_batches(int k, int base_quality, const hpgq_batch_t *bs, int
   free(ts);
   free(wc);
   return err;
+}
+
+/* ------------------------------------------------------------------ */
+/* stats --kmers: build-defined 5-mer counts (the      */
+/* per-read kmers of fastq_reads_stats are in the absent bioinfo-libs, */
+/* merged at src/stats_fastq.c:384-410) -> parity unpinned             */
+/* ------------------------------------------------------------------ */
+
+static inline int o_kcode(unsigned char c) {
+  switch (c) {   /* exact uppercase only, like the per-position counts (:360-372) */
+    case 'A': return 0;
+    case 'C': return 1;
+    case 'G': return 2;
+    case 'T': return 3;
+    default: return -1;
+  }
+}
+
+/* by_pos[HPGQ_NUM_KMERS][lmax-4] += counts of b's reads with mask[i] == 1
+ * (all reads when mask is NULL) */
+int oracle_kmers(const hpgq_batch_t *b, const uint8_t *mask, int lmax, uint64_t *by_pos) {
+  const int npos = lmax > HPGQ_KMER_K - 1 ? lmax - (HPGQ_KMER_K - 1) : 0;
+  if (!b || b->num_reads < 0 || lmax < 1) return HPGQ_E_INVALID;
+  for (int64_t r = 0; r < b->num_reads; ++r) {
+    if (mask && mask[r] != 1) continue;
+    const int32_t a = b->data_indices[r], n = b->data_indices[r + 1] - a;
+    const unsigned char *s = (const unsigned char *)b->seq + a;
+    for (int p = 0; p + HPGQ_KMER_K <= n && p < npos; ++p) {
+      int id = 0, ok = 1;
+      for (int i = 0; i < HPGQ_KMER_K; ++i) {
+        const int c = o_kcode(s[p + i]);
+        if (c < 0) ok = 0;
+        id = id * 4 + (c < 0 ? 0 : c);
+      }
+      if (ok) by_pos[(size_t)id * npos + p]++;
+    }
+  }
+  return HPGQ_OK;
 }
 
 int oracle_max_threads(void) { return omp_get_max_threads(); }

@@ -11,6 +11,7 @@ Reference lines followed:
   filter options      src/filter_fastq.c:140-145, src/stats_options.c:275-282
   edit options        src/edit_fastq.c:148-151, src/edit_options.c:280-283
   chaos game          old/chaos_game.c:165-267
+  --kmers merge       src/stats_fastq.c:384-410 (per-read k-mers: build-defined)
 """
 
 NUM_SCALARS = 8
@@ -197,3 +198,28 @@ def cgr_fill(k, base_quality, reads, status=None, only_valid=False,
         cnt = 0
         acc = 0
     return table_seq, table_q, word_count
+
+
+def kmers(reads, lmax, mask=None):
+    """stats --kmers, build-defined: {(kmer id, start pos): count}."""
+    code = {"A": 0, "C": 1, "G": 2, "T": 3}
+    out = {}
+    for r, (s, _q) in enumerate(reads):
+        if mask is not None and mask[r] != 1:
+            continue
+        s = s.decode("latin-1") if isinstance(s, bytes) else s
+        for p in range(len(s) - 4):
+            if p >= lmax - 4:
+                break
+            word = s[p:p + 5]
+            if all(ch in code for ch in word):
+                kid = 0
+                for ch in word:
+                    kid = kid * 4 + code[ch]
+                out[(kid, p)] = out.get((kid, p), 0) + 1
+    return out
+
+
+def kmer_string(kid):
+    """id -> 5 letters, first base most significant (kmers_string, src/stats_fastq.c:479)."""
+    return "".join("ACGT"[(kid >> (2 * (4 - i))) & 3] for i in range(5))

@@ -97,3 +97,19 @@ def cgr(k, reads, base_quality=33, status=None, mode=0, tables=None):
                               _p(wc))
     assert rc == 0, rc
     return ts, tq, wc
+
+
+_lib.oracle_kmers.argtypes = [C.POINTER(H.Batch), C.c_void_p, C.c_int, C.c_void_p]
+_lib.oracle_kmers.restype = C.c_int
+
+
+def kmers(reads, lmax, mask=None, by_pos=None):
+    """oracle --kmers counts: [1024, lmax-4] uint64 (added into by_pos if given)."""
+    npos = max(lmax - 4, 0)
+    if by_pos is None:
+        by_pos = np.zeros((1024, npos), dtype=np.uint64)
+    b = reads.batch()
+    m = None if mask is None else np.ascontiguousarray(mask, dtype=np.uint8)
+    rc = _lib.oracle_kmers(C.byref(b), _p(m), lmax, _p(by_pos))
+    assert rc == 0, rc
+    return by_pos

@@ -44,7 +44,7 @@ def test_cli_params_match_python_options(cmd, flags, py):
     ["stats", "--print-params", "--quality-encoding", "solexa"],
     ["filter", "--print-params"],                       # nothing to filter
     ["edit", "--print-params", "--max-N", "2"],          # nothing to edit
-    ["stats", "--print-params", "--kmers"],              # not in this build
+    ["filter", "--print-params", "--kmers", "--max-N", "1"],   # --kmers is a stats flag
     ["stats", "-f", "/nonexistent.fq"],
     ["bogus"],
 ])

@@ -100,3 +100,39 @@ def test_cli_read_too_long(tmp_path):
     fq = _write(tmp_path, reads)
     r = run_cli(["stats", "-f", fq, "-o", tmp_path, "--lmax", 100, "--quiet"], check=False)
     assert r.returncode != 0 and "longer than lmax" in r.stderr
+
+
+@pytest.mark.parametrize("filt", [False, True])
+def test_cli_stats_kmers(tmp_path, filt):
+    """stats --kmers: the raw table equals the oracle's over the merged reads (the
+    passed ones when filtering), and kmers.txt / kmers.per.nt.data follow it."""
+    rng = np.random.default_rng(31)
+    reads = O.synth(15000, seed=31, L=150)
+    fq = _write(tmp_path, reads)
+    out = tmp_path / "out"
+    out.mkdir()
+    kb = tmp_path / "k.bin"
+    flags = ["--read-quality-range", "20,", "--read-length-range", "50,"] if filt else []
+    run_cli(["stats", "-f", fq, "-o", out, "--kmers", "--kmers-out", kb, "--lmax", 150,
+             "--chunk-mb", 1, "--quiet"] + flags)
+    got = np.fromfile(kb, np.uint64).reshape(1024, 146)
+    mask = None
+    if filt:
+        p = H.stats_params(lmax=150, read_quality_range="20,", read_length_range="50,")
+        mask, _, _ = O.run(p, reads)
+    want = O.kmers(reads, 150, None if mask is None else np.asarray(mask, np.uint8))
+    np.testing.assert_array_equal(got, want)
+    tot = want.sum(axis=1)
+    order = sorted(range(1024), key=lambda i: (-int(tot[i]), i))
+    names = ["".join("ACGT"[(i >> (2 * (4 - j))) & 3] for j in range(5)) for i in range(1024)]
+    lines = (out / "in.fq.kmers.txt").read_text().splitlines()
+    assert lines[0] == "# Sequence\tCount"
+    assert lines[1:] == [f"{names[i]}\t{int(tot[i])}" for i in order]
+    rows = (out / "in.fq.kmers.per.nt.data").read_text().splitlines()
+    top = order[:5]
+    size = max(int(np.nonzero(want[i])[0].max()) + 1 for i in top)
+    assert len(rows) == size
+    assert rows[0] == "1\t" + "\t".join(str(int(want[i, 0])) for i in top)
+    summ = (out / "in.fq.summary.txt").read_text()
+    assert "K-mers (top 20)" in summ and f"\t{names[order[0]]}\t\t{int(tot[order[0]])}" in summ
+    del rng

@@ -1,0 +1,75 @@
+"""--kmers parity: hpgq_kmers_* (gfx950) vs the oracle's 5-mer counts, bit for
+bit (build-defined semantics, DESIGN.md §2.6 -> parity unpinned)."""
+import numpy as np
+import pytest
+
+import hpgfastq as H
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev(reads, mask=None, offset=0):
+    import torch
+    dev = torch.device("cuda", 0)
+    pad = np.zeros(H.DEVICE_SLACK, np.uint8)
+    lead = np.full(offset, ord("A"), np.uint8)
+    t = dict(seq=torch.from_numpy(np.concatenate([lead, reads.seq, pad])).to(dev),
+             qual=torch.from_numpy(np.concatenate([lead, reads.qual, pad])).to(dev),
+             idx=torch.from_numpy((reads.idx + offset).astype(np.int32)).to(dev))
+    if mask is not None:
+        t["mask"] = torch.from_numpy(mask).to(dev)
+    torch.cuda.synchronize()
+    return t
+
+
+def gpu_kmers(lmax, batches, masks=None, offset=0):
+    km = H.Kmers(lmax)
+    keep = []
+    for i, reads in enumerate(batches):
+        m = masks[i] if masks is not None else None
+        t = _dev(reads, m, offset)
+        keep.append(t)
+        b = H.engine.device_batch(reads.n, t["seq"].data_ptr(), t["qual"].data_ptr(),
+                                  t["idx"].data_ptr())
+        km.count_device(b, t["mask"].data_ptr() if m is not None else None)
+    km.sync()
+    out = km.by_pos()
+    km.close()
+    return out
+
+
+def _random_reads(rng, n, lo, hi, alphabet=b"ACGTACGTACGTNacgtRY"):
+    pairs = []
+    for _ in range(n):
+        L = int(rng.integers(lo, hi))
+        s = np.array(rng.choice(list(alphabet), L), np.uint8).tobytes()
+        pairs.append((s, b"I" * L))
+    return O.Reads.from_pairs(pairs)
+
+
+@pytest.mark.parametrize("lmax", [5, 6, 20, 150, 256])
+def test_kmers_edge_lengths(lmax):
+    rng = np.random.default_rng(lmax)
+    reads = _random_reads(rng, 3000, 0, lmax + 40)   # includes reads longer than lmax
+    np.testing.assert_array_equal(gpu_kmers(lmax, [reads]), O.kmers(reads, lmax))
+
+
+def test_kmers_mask_multi_batch_and_offsets():
+    rng = np.random.default_rng(3)
+    batches = [_random_reads(rng, 2000, 0, 160) for _ in range(3)]
+    masks = [(rng.random(b.n) < 0.6).astype(np.uint8) for b in batches]
+    want = np.zeros((1024, 146), dtype=np.uint64)
+    for b, m in zip(batches, masks):
+        O.kmers(b, 150, m, want)
+    np.testing.assert_array_equal(gpu_kmers(150, batches, masks, offset=13), want)
+
+
+def test_kmers_large_synthetic():
+    reads = O.synth(200_000, seed=2, L=150)
+    np.testing.assert_array_equal(gpu_kmers(150, [reads]), O.kmers(reads, 150))
+
+
+def test_kmers_small_lmax_is_empty():
+    reads = O.Reads.from_pairs([(b"ACGTACGT", b"IIIIIIII")])
+    assert gpu_kmers(4, [reads]).size == 0
