@@ -42,10 +42,6 @@ namespace cgr {
 constexpr double kEps = 0.00001;   // old/chaos_game.h:41
 constexpr int kWG = 1024;       // 16 waves share one set of LDS tables (128 KB at k = 7)
 constexpr int kWarm = 128;         // bytes of context replayed to guess a read's entry state
-#ifndef HPGQ_CGR_RING
-#define HPGQ_CGR_RING 4
-#endif
-constexpr int kRing = HPGQ_CGR_RING;   // 8-byte chunks in flight per lane (run_read, warm)
 constexpr int kLdsMaxK = 7;        // 2 x 4^7 x 4 B = 128 KB of LDS tables
 
 typedef unsigned v2u __attribute__((ext_vector_type(2)));
@@ -250,11 +246,9 @@ __device__ __forceinline__ int opaque(int x) {
 }
 
 // Quality bytes around an 8-byte chunk at c: m = [c-8, c+8) and, for K > 9
-// (quality[qpos - K] up to 11 bytes back), lo = [c-16, c-8).  Loaded fresh
-// for every chunk rather than rotated through registers: a loop-carried copy
-// of the newest load makes the loop head wait for it (vmcnt(0)).  Offsets
-// before the buffer read 0 (raw buffer range check); bytes before the read are
-// never used (a word holds K bases of the read).
+// (quality[qpos - K] up to 11 bytes back), lo = [c-16, c-8); cut from the
+// block registers (run_block) rather than rotated through registers: a
+// loop-carried copy of the newest load makes the loop head wait for it.
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 struct QWin {
   v4u m;
@@ -299,61 +293,75 @@ __device__ __forceinline__ void run_chunk(v2u sv, const QWin &q, int left, State
     run_chunk_steps<K, FULL, UNCOND, false>(cl, q, st, cnt, acc, ts, tq, sign, sub, words);
 }
 
-// Run read [a, a+n) from byte p0 (word counter cnt0) with state st.  The
-// next kRing chunks' loads are in flight while a chunk is processed; each
-// buffer register is reloaded right after its chunk is consumed.
+// Run read [a, a+n) from byte p0 (word counter cnt0) with state st, 64 bytes
+// at a time: a lane's block is seq [c, c+64) and quality [c-16, c+64) in
+// 16-byte loads (the first quality piece [c-8, c) for K <= 9), two blocks in
+// flight.  Taking a whole block per visit keeps
+// the lanes' lines from being evicted between 8-byte visits (1024 lanes per
+// CU x 2 streams of 128-byte lines overflow the L2) and quarters the
+// address work per byte.  The [c-16, c) piece is a load of its own: before
+// offset 0 it reads 0, and it then covers only bytes before the read.
+struct Blk {
+  v4u s[4];
+  v4u q[5];
+};
+
+template <int K, bool FULL, bool UNCOND>
+__device__ __forceinline__ void run_block(const Blk &B, int left, State &st, int &cnt,
+                                          uint32_t &acc, uint32_t *ts, uint32_t *tq, uint32_t sign,
+                                          uint32_t sub, uint32_t &words) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    if (__builtin_expect(__ballot(left - 8 * i > 0) == 0ull, 0)) return;   // the wave is done
+    const v2u sv = {B.s[i >> 1][2 * (i & 1)], B.s[i >> 1][2 * (i & 1) + 1]};
+    QWin q;   // dwords 2i+2 .. 2i+5 of quality [c-16, c+64): [c+8i-8, c+8i+8)
+    const int d = 2 * i + 2;
+    q.m = v4u{B.q[d >> 2][d & 3], B.q[(d + 1) >> 2][(d + 1) & 3], B.q[(d + 2) >> 2][(d + 2) & 3],
+              B.q[(d + 3) >> 2][(d + 3) & 3]};
+    q.lo = v2u{B.q[(d - 2) >> 2][(d - 2) & 3], B.q[(d - 1) >> 2][(d - 1) & 3]};
+    run_chunk<K, FULL, UNCOND>(sv, q, left - 8 * i, st, cnt, acc, ts, tq, sign, sub, words);
+  }
+}
+
 template <int K, bool FULL, bool UNCOND>
 __device__ void run_read(const Args &A, const Src &S, int a, int n, int p0, int cnt0, State &st,
                          uint32_t *ts, uint32_t *tq, uint32_t sign, uint32_t &words) {
   const uint32_t sub = A.base_quality * (uint32_t)K;
   int cnt = cnt0;
   uint32_t acc = 0;
-  auto ld_s = [&](int c) { return __builtin_amdgcn_raw_buffer_load_b64(S.rs, (uint32_t)(a + c), 0, 0); };
-  auto ld_q = [&](int c) {
-    QWin q;
-    q.m = v4u{0u, 0u, 0u, 0u};
-    q.lo = v2u{0u, 0u};
-    if (FULL) q.m = __builtin_amdgcn_raw_buffer_load_b128(S.rq, (uint32_t)(a + c - 8), 0, 0);
-    if (FULL && K > 9) q.lo = __builtin_amdgcn_raw_buffer_load_b64(S.rq, (uint32_t)(a + c - 16), 0, 0);
-    return q;
-  };
-  // kRing chunks in flight per lane: a lane enters a new 128-byte line every
-  // 16 chunks and the wave waits for its slowest lane, so some lane takes an
-  // HBM miss in most chunks.  Offsets after the first are laundered: merged
-  // into wider loads, the loop head would wait on the newest loads.
-  v2u sv[kRing];
-  QWin qv[kRing];
+  auto load = [&](int c) {
+    Blk B;
 #pragma unroll
-  for (int i = 0; i < kRing; ++i) {
-    const int o = i ? opaque(p0 + 8 * i) : p0;
-    sv[i] = ld_s(o);
-    qv[i] = ld_q(o);
-  }
-  // a read starting in the buffer's first 8 bytes: its first window would
-  // start before offset 0, and the range check zeroes the whole load — take
-  // [0, 16) and shift it into place (the bytes before 0 are never used)
-  if (FULL && a + p0 < 8) {
-    const v4u t = __builtin_amdgcn_raw_buffer_load_b128(S.rq, 0u, 0, 0);
-    const int sh = 8 * (8 - (a + p0));   // 8..64 bits
-    const uint64_t lo = ((uint64_t)t[1] << 32) | t[0], hi = ((uint64_t)t[3] << 32) | t[2];
-    const uint64_t nlo = sh == 64 ? 0ull : lo << sh;
-    const uint64_t nhi = sh == 64 ? lo : (hi << sh) | (lo >> (64 - sh));
-    qv[0].m = v4u{(uint32_t)nlo, (uint32_t)(nlo >> 32), (uint32_t)nhi, (uint32_t)(nhi >> 32)};
-  }
-  // one exit (chunks past the end are all class 0)
-  for (int c = p0; c < n; c += 8 * kRing) {
+    for (int i = 0; i < 4; ++i)
+      B.s[i] = __builtin_amdgcn_raw_buffer_load_b128(S.rs, (uint32_t)(a + c + 16 * i), 0, 0);
 #pragma unroll
-    for (int i = 0; i < kRing; ++i) {
-      run_chunk<K, FULL, UNCOND>(sv[i], qv[i], n - c - 8 * i, st, cnt, acc, ts, tq, sign, sub, words);
-      sv[i] = ld_s(c + 8 * (i + kRing));
-      qv[i] = ld_q(c + 8 * (i + kRing));
+    for (int i = 1; i < 5; ++i)
+      B.q[i] = FULL ? __builtin_amdgcn_raw_buffer_load_b128(S.rq, (uint32_t)(a + c - 16 + 16 * i), 0, 0)
+                    : v4u{0u, 0u, 0u, 0u};
+    // [c-16, c-8) only for K > 9: a loaded dword that is never read is still
+    // written by its load, and reusing its register makes the wave wait for it
+    if (FULL && K > 9) {
+      B.q[0] = __builtin_amdgcn_raw_buffer_load_b128(S.rq, (uint32_t)(a + c - 16), 0, 0);
+    } else if (FULL) {
+      const v2u h = __builtin_amdgcn_raw_buffer_load_b64(S.rq, (uint32_t)(a + c - 8), 0, 0);
+      B.q[0] = v4u{0u, 0u, h.x, h.y};
+    } else {
+      B.q[0] = v4u{0u, 0u, 0u, 0u};
     }
+    return B;
+  };
+  Blk B0 = load(p0), B1 = load(opaque(p0 + 64));
+  for (int c = p0; c < n; c += 128) {
+    run_block<K, FULL, UNCOND>(B0, n - c, st, cnt, acc, ts, tq, sign, sub, words);
+    B0 = load(c + 128);
+    run_block<K, FULL, UNCOND>(B1, n - c - 64, st, cnt, acc, ts, tq, sign, sub, words);
+    B1 = load(c + 192);
   }
 }
 
 // Context replay, all reads valid: the context of read r is the kWarm bytes
-// [c, ar) before it in seq (reads are contiguous), so every lane runs the same
-// kWarm / 16 iterations.  Away from the clamp, f does not depend on the word
+// [c, ar) before it in seq (reads are contiguous), loaded in one visit (eight
+// 16-byte loads) and replayed in the same 16 chunks by every lane.  Away from the clamp, f does not depend on the word
 // counter, so a chunk only moves f (4 FP64 ops per base); a chunk kHot flags
 // replays byte by byte with the counter rebuilt at its first byte and reset
 // at every read start (warm_exact).
@@ -397,17 +405,13 @@ __device__ State warm_contiguous(const Args &A, const Src &S, const uint8_t *cls
   State st = {half, half};
   const int ar = A.idx[r];
   const int c0 = max(A.idx[0], ar - kWarm);   // at the batch start: exact
-  auto ld = [&](int c) { return __builtin_amdgcn_raw_buffer_load_b64(S.rs, (uint32_t)c, 0, 0); };
-  v2u sv[kRing];   // see run_read
+  static_assert(kWarm == 128, "the context is loaded as 8 x 16 bytes");
+  v4u w[8];   // the whole context in one visit (see run_read)
 #pragma unroll
-  for (int i = 0; i < kRing; ++i) sv[i] = ld(i ? opaque(c0 + 8 * i) : c0);
-  for (int c = c0; c < ar; c += 8 * kRing) {
+  for (int i = 0; i < 8; ++i) w[i] = __builtin_amdgcn_raw_buffer_load_b128(S.rs, (uint32_t)(c0 + 16 * i), 0, 0);
 #pragma unroll
-    for (int i = 0; i < kRing; ++i) {
-      warm_chunk<K>(A, S, cls, r, sv[i], c + 8 * i, ar, st);
-      sv[i] = ld(c + 8 * (i + kRing));
-    }
-  }
+  for (int j = 0; j < 16; ++j)
+    warm_chunk<K>(A, S, cls, r, v2u{w[j >> 1][2 * (j & 1)], w[j >> 1][2 * (j & 1) + 1]}, c0 + 8 * j, ar, st);
   return st;
 }
 

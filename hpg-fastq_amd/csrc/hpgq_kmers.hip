@@ -3,7 +3,7 @@
 // Replaces the per-read kmer fields of fastq_reads_stats (bioinfo-libs,
 // absent) and their merge in the stats consumer, src/stats_fastq.c:384-410
 // (kmer_out->counter += ..., counter_by_pos[k] += ...).  Semantics are
-// build-defined (DESIGN.md §2.6): 5-mers of exact uppercase A/C/G/T, id =
+// build-defined (DESIGN.md §2.5): 5-mers of exact uppercase A/C/G/T, id =
 // sum code_i * 4^(4-i) with A=0 C=1 G=2 T=3 (first base most significant),
 // counted at every start position p <= len-5 of every merged read.  Output:
 // by_pos[1024][lmax-4] u64; the global counter of a k-mer is its row sum.

@@ -290,7 +290,7 @@ int64_t hpgq_cgr_last_replays(hpgq_cgr_t *cg);
 
 /*
  * Build-defined (the per-read k-mer code is in the absent bioinfo-libs;
- * DESIGN.md §2.6): 5-mers of exact uppercase A/C/G/T, id = sum code_i *
+ * DESIGN.md §2.5): 5-mers of exact uppercase A/C/G/T, id = sum code_i *
  * 4^(4-i) with A=0 C=1 G=2 T=3, counted at every start position
  * p <= len-5 (p < lmax-4) of every counted read.  by_pos is
  * [HPGQ_NUM_KMERS][lmax-4] u64 (counter_by_pos); a k-mer's counter is its row

@@ -16,7 +16,7 @@
  *     derived from the call sites and help texts cited inline.
  *     -> "parity unpinned": the reference holds no tests, fixtures or golden
  *        vectors for this path, and its CPU path cannot be built here.
- *   - --kmers (§8f rank 2): build-defined 5-mer counts (DESIGN.md §2.6);
+ *   - --kmers (§8f rank 2): build-defined 5-mer counts (DESIGN.md §2.5);
  *     the per-read k-mer code is in the same absent bioinfo-libs -> unpinned.
  *   - CGR (A7): line-by-line restatement of chaos_game_fill_tables,
  *     old/chaos_game.c:165-267.  The reference file needs an absent header
@@ -384,7 +384,7 @@ int oracle_cgr_fill_batches(int k, int base_quality, const hpgq_batch_t *bs, int
 }
 
 /* ------------------------------------------------------------------ */
-/* stats --kmers: build-defined 5-mer counts (DESIGN.md §2.6; the      */
+/* stats --kmers: build-defined 5-mer counts (DESIGN.md §2.5; the      */
 /* per-read kmers of fastq_reads_stats are in the absent bioinfo-libs, */
 /* merged at src/stats_fastq.c:384-410) -> parity unpinned             */
 /* ------------------------------------------------------------------ */

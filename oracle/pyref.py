@@ -201,7 +201,7 @@ def cgr_fill(k, base_quality, reads, status=None, only_valid=False,
 
 
 def kmers(reads, lmax, mask=None):
-    """stats --kmers, build-defined (DESIGN.md §2.6): {(kmer id, start pos): count}."""
+    """stats --kmers, build-defined (DESIGN.md §2.5): {(kmer id, start pos): count}."""
     code = {"A": 0, "C": 1, "G": 2, "T": 3}
     out = {}
     for r, (s, _q) in enumerate(reads):

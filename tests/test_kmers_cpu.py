@@ -1,6 +1,6 @@
 """--kmers oracle checks (CPU): the C restatement (oracle_kmers) against the
 independent pure-Python one (oracle/pyref.py) and a hand-derived known answer.
-Semantics are build-defined (DESIGN.md §2.6) -> parity unpinned."""
+Semantics are build-defined (DESIGN.md §2.5) -> parity unpinned."""
 import os
 import sys
 

@@ -1,5 +1,5 @@
 """--kmers parity: hpgq_kmers_* (gfx950) vs the oracle's 5-mer counts, bit for
-bit (build-defined semantics, DESIGN.md §2.6 -> parity unpinned)."""
+bit (build-defined semantics, DESIGN.md §2.5 -> parity unpinned)."""
 import numpy as np
 import pytest
 
