@@ -27,9 +27,7 @@ struct hpgq_ctx {
   int nch = 1;
   bool gen = false;               // generic (edit / N / OOR / left-right) kernel variant
   bool tri = false;               // three-reads-per-wave FAST kernel (lmax <= 160)
-  bool tri_edit = false;          // ... with the trim pre-pass (single-end edit)
-  uint32_t *d_trim_tmp = nullptr; // trims when the caller wants none back
-  size_t trim_tmp_cap = 0;
+  bool tri_edit = false;          // ... trimming in its block prologue (single-end edit)
   int grid = 0;
   uint64_t *d_slab = nullptr;     // [grid][nm * clen] per-workgroup partials
   hpgq::ColdParams *d_cold = nullptr;
@@ -127,7 +125,7 @@ static const void *kernel_nch(int nch) {
 }
 
 static const void *kernel_for(int nm, int nch, bool gen, bool tri, bool edit, char *name, size_t cap) {
-  if (tri && edit) {   // single-end edit: trim pre-pass + windows
+  if (tri && edit) {   // single-end edit: trims in the block prologue + windows
     const char *w = std::getenv("HPGQ_TRI_WAVES");
     const int mw = w && std::atoi(w) == 4 ? 4 : 5;
     std::snprintf(name, cap, "hpgq::engine_tri_kernel<%d, false, 1, true>", mw);
@@ -328,7 +326,6 @@ void hpgq_close(hpgq_ctx_t *c) {
   (void)hipFree(c->d_err);
   (void)hipFree(c->d_slab);
   (void)hipFree(c->d_cold);
-  (void)hipFree(c->d_trim_tmp);
   (void)hipFree(c->d_buf);
   (void)hipFree(c->d_mask);
   (void)hipFree(c->d_trim);
@@ -340,21 +337,6 @@ static int launch(hpgq_ctx *c, hpgq::EngineArgs &A) {
   if (A.num_reads <= 0) return HPGQ_OK;
   A.slab = c->d_slab;
   A.err = c->d_err;
-  if (c->tri_edit) {   // trims first (into the caller's trim buffer, else a scratch one)
-    if (!A.trim) {
-      if ((size_t)A.num_reads > c->trim_tmp_cap) {
-        (void)hipFree(c->d_trim_tmp);
-        c->d_trim_tmp = nullptr;
-        c->trim_tmp_cap = 0;
-        const size_t cap = (size_t)A.num_reads + (size_t)A.num_reads / 4 + 1024;
-        if (hipMalloc(&c->d_trim_tmp, cap * 4) != hipSuccess) return HPGQ_E_NOMEM;
-        c->trim_tmp_cap = cap;
-      }
-      A.trim = c->d_trim_tmp;
-    }
-    hpgq::trim_kernel<<<(unsigned)((A.num_reads + 255) / 256), 256, 0, c->stream>>>(A, A.trim);
-    HPGQ_HIP_TRY(hipGetLastError());
-  }
   const int64_t per_block = c->tri ? hpgq::kTriBlock : 64;
   const int64_t nblocks = (A.num_reads + per_block - 1) / per_block;
   const int64_t need = (nblocks + hpgq::kWaves - 1) / hpgq::kWaves;

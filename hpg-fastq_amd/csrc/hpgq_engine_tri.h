@@ -170,24 +170,19 @@ using AddTag = TriTag<false>;
 using SubTag = TriTag<true>;
 
 // MINW: minimum waves per SIMD the register allocation must allow (occupancy)
-// ---- edit (A6) pre-pass for the three-read kernel ---------------------------
-// One thread per read: the leading run of out-of-range qualities within the
+// ---- edit (A6) on the three-read kernel --------------------------------------
+// The trim of one read: the leading run of out-of-range qualities within the
 // first min(edit_left_length, n) bases and the trailing run within the last
 // min(edit_right_length, n - ts), 8 bytes at a time with the
-// SWAR in_range test.  Writes trim[r] = ts | te << 16 — the edit output — and
-// the three-read kernel then reads each window [ts, n - te) directly.
-__global__ void __launch_bounds__(256) trim_kernel(EngineArgs A, uint32_t *trim) {
-  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (r >= A.num_reads) return;
-  const ColdParams &C = *A.cold;
-  const int data_end = uni(A.idx[0][A.num_reads]);
-  const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc(
-      (void *)A.qual[0], (short)0, data_end + kTriSlack, 0x00020000);
-  const int a = A.idx[0][r], n = A.idx[0][r + 1] - a;
-  auto ok8 = [&](int pos, int lo_none_sel) -> uint64_t {   // 0x80 per in-range byte of [pos, pos+8)
-    const v2u w = __builtin_amdgcn_raw_buffer_load_b64(rq, (uint32_t)(a + pos), 0, 0);
+// SWAR in_range test; quality bytes [off, off + n) of rq.  Returns ts | te << 16,
+// the edit output.  Called by the block prologue (one lane per read), so the
+// lines it touches are still in L2 when the block's triples stream the read.
+__device__ __forceinline__ uint32_t trim_word(const ColdParams &C, __amdgpu_buffer_rsrc_t rq,
+                                              int off, int n) {
+  auto ok8 = [&](int pos, bool right) -> uint64_t {   // 0x80 per in-range byte of [pos, pos+8)
+    const v2u w = __builtin_amdgcn_raw_buffer_load_b64(rq, (uint32_t)(off + pos), 0, 0);
     uint32_t lo, hi;
-    if (lo_none_sel == 0) {
+    if (!right) {
       lo = in_range(w.x, C.el_lo4, C.el_hi4, C.el_lo_none, C.el_hi_none, C.el_none_in);
       hi = in_range(w.y, C.el_lo4, C.el_hi4, C.el_lo_none, C.el_hi_none, C.el_none_in);
     } else {
@@ -202,7 +197,7 @@ __global__ void __launch_bounds__(256) trim_kernel(EngineArgs A, uint32_t *trim)
     const int lim = min(C.e_left_len, n);
     ts = lim;
     for (int c = 0; c < lim; c += 8) {
-      const uint64_t ok = ok8(c, 0) & low_bytes(lim - c);
+      const uint64_t ok = ok8(c, false) & low_bytes(lim - c);
       if (ok) {
         ts = c + (__builtin_ctzll(ok) >> 3);
         break;
@@ -215,14 +210,14 @@ __global__ void __launch_bounds__(256) trim_kernel(EngineArgs A, uint32_t *trim)
     te = lim;
     for (int e = n; e > lo; e -= 8) {
       const int st = max(e - 8, lo);
-      const uint64_t ok = ok8(st, 1) & low_bytes(e - st);
+      const uint64_t ok = ok8(st, true) & low_bytes(e - st);
       if (ok) {
         te = n - 1 - (st + ((63 - __builtin_clzll(ok)) >> 3));
         break;
       }
     }
   }
-  trim[r] = (uint32_t)ts | ((uint32_t)te << 16);
+  return (uint32_t)ts | ((uint32_t)te << 16);
 }
 
 template <int M>
@@ -236,7 +231,8 @@ struct MateTag {
 // then mate 2's, each mate with its own accumulators / LDS partials / counter
 // set; the epilogue takes the pair decision (both mates pass) and subtracts
 // failed pairs from both sets.
-// EDIT (NM = 1): trim_kernel ran first; each read is its window [ts, n - te)
+// EDIT (NM = 1): the block prologue trims each read (trim_word, written to
+// A.trim when the caller wants it) and describes it by its window [ts, n - te)
 // (offset + ts, length n - ts - te): stats and filter see the trimmed read.
 template <int MINW, bool UNAL, int NM, bool EDIT>
 __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
@@ -318,8 +314,9 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
     for (int m = 0; m < NM; ++m) {
       int a = A.idx[m][r0 + l], e = A.idx[m][r0 + l + 1];
       nraw = lane < nr ? (uint32_t)(e - a) : 0u;
-      if (EDIT) {   // the trimmed window
-        tw = lane < nr ? A.trim[r0 + l] : 0u;
+      if (EDIT) {   // trim here, then describe the trimmed window
+        tw = lane < nr ? trim_word(*A.cold, rq[m], bq[m] + a, e - a) : 0u;
+        if (A.trim && lane < nr) A.trim[r0 + l] = tw;
         a += (int)(tw & 0xFFFFu);
         e -= (int)(tw >> 16);
         if (e < a) e = a;
