@@ -94,6 +94,21 @@ def test_edit_trim_stats():
     assert c[H.S_NUM_EDITED] > 0
 
 
+@pytest.mark.parametrize("left,right", [(1, 1), (8, 31), (16, 32), (17, 33), (16, 0), (0, 32)])
+def test_edit_window_sizes(left, right):
+    """The trim at the window sizes where the kernel switches from one batch of
+    loads (left <= 16, right <= 32) to the 8-byte loop, on reads as short as 0."""
+    reads = O.synth(12000, seed=40 + left + right, L=150, trunc_pct=60)
+    kw = {}
+    if left:
+        kw.update(left_length=left, left_quality_range="22,")
+    if right:
+        kw.update(right_length=right, right_quality_range="18,36")
+    p = H.edit_params(lmax=150, stats=True, **kw)
+    c = assert_same(p, reads)
+    assert c[H.S_NUM_EDITED] > 0
+
+
 def test_edit_with_filter():
     reads = O.synth(20000, seed=5, L=150, trunc_pct=20)
     p = H.edit_params(lmax=150, stats=True, left_length=40, left_quality_range="30,",
