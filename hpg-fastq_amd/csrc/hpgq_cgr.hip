@@ -59,7 +59,12 @@ struct Args {
   unsigned long long *flags; // [ceil(n/64)] one bit per read
   unsigned long long *sum;   // [ceil(n/4096)] one bit per nonzero flags word
   unsigned long long *replays;
+  const uint32_t *gate;      // stream path: run only when the gate says so (null: always)
 };
+
+__device__ __forceinline__ bool gated_out(const Args &A) {
+  return A.gate && (__builtin_amdgcn_readfirstlane(*A.gate) & 1u) == 0u;
+}
 
 struct Src {
   __amdgpu_buffer_rsrc_t rs, rq;
@@ -469,6 +474,7 @@ __device__ State guess_entry(const Args &A, const Src &S, const uint8_t *cls, in
 
 template <int K>
 __global__ void __launch_bounds__(kWG) cgr_fill_kernel(Args A) {
+  if (gated_out(A)) return;
   constexpr int dim = 1 << K;
   constexpr bool kLds = K <= kLdsMaxK;
   constexpr int cells = dim * dim + 1;   // + the spare cell of the unconditional adds
@@ -517,6 +523,7 @@ __device__ __forceinline__ bool same(double2 a, double2 b) {
 
 // flag r iff its guessed entry state differs (bitwise) from e_{r-1}
 __global__ void __launch_bounds__(256) cgr_check_kernel(Args A) {
+  if (gated_out(A)) return;
   const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const bool f = r > 0 && r < A.num_reads && !same(A.g[r], A.e[r - 1]);
   const unsigned long long b = __ballot(f);
@@ -530,6 +537,10 @@ __global__ void __launch_bounds__(256) cgr_check_kernel(Args A) {
 // one lane: replay flagged reads in order with their true entry states
 template <int K>
 __global__ void __launch_bounds__(64) cgr_fix_kernel(Args A) {
+  if (gated_out(A)) {
+    if (threadIdx.x == 0) *A.replays = 0;
+    return;
+  }
   __shared__ uint8_t cls[256];
   fill_classes(cls, threadIdx.x, 64);
   __syncthreads();
@@ -628,6 +639,46 @@ static const void *fix_for(int k) {
 }  // namespace cgr
 }  // namespace hpgq
 
+#include "hpgq_cgr_stream.h"
+
+namespace hpgq {
+namespace cgr {
+namespace stream {
+
+template <int K>
+struct SKernels {
+  static const void *fill() { return (const void *)cgr_stream_kernel<K>; }
+  static const void *fin() { return (const void *)cgr_stream_finalize_kernel<K>; }
+};
+
+static const void *stream_for(int k) {
+  switch (k) {
+    case 1: return SKernels<1>::fill();
+    case 2: return SKernels<2>::fill();
+    case 3: return SKernels<3>::fill();
+    case 4: return SKernels<4>::fill();
+    case 5: return SKernels<5>::fill();
+    case 6: return SKernels<6>::fill();
+    default: return SKernels<7>::fill();
+  }
+}
+
+static const void *finalize_for(int k) {
+  switch (k) {
+    case 1: return SKernels<1>::fin();
+    case 2: return SKernels<2>::fin();
+    case 3: return SKernels<3>::fin();
+    case 4: return SKernels<4>::fin();
+    case 5: return SKernels<5>::fin();
+    case 6: return SKernels<6>::fin();
+    default: return SKernels<7>::fin();
+  }
+}
+
+}  // namespace stream
+}  // namespace cgr
+}  // namespace hpgq
+
 struct hpgq_cgr {
   int device = 0, k = 7, dim = 128;
   uint32_t base_quality = 33;
@@ -641,6 +692,15 @@ struct hpgq_cgr {
   int grid = 0;
   int64_t last_replays = 0;
   bool pending = false;       // a fill whose replay count was not read back yet
+  // stream path (k <= 7, all reads): see hpgq_cgr_stream.h
+  int path = HPGQ_CGR_PATH_AUTO;
+  bool streamed = false;      // the last fill went through the stream kernels
+  int last_exact = 1;
+  int32_t *d_span_first = nullptr;
+  unsigned long long *d_scratch = nullptr;
+  uint32_t *d_gate = nullptr;
+  size_t s_lds = 0;
+  int s_grid = 0;
 };
 
 static int cgr_ensure(hpgq_cgr *c, int64_t n) {
@@ -696,6 +756,21 @@ int hpgq_cgr_open(hpgq_cgr_t **cg, int device, int k, int base_quality) {
   HPGQ_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, hpgq::cgr::kWG, c->lds));
   HPGQ_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
   c->grid = std::max(1, per_cu) * cus;
+  HPGQ_HIP_TRY(hipMalloc(&c->d_gate, 4));
+  HPGQ_HIP_TRY(hipMemsetAsync(c->d_gate, 0, 4, c->stream));
+  if (k <= hpgq::cgr::stream::kMaxK) {
+    namespace S = hpgq::cgr::stream;
+    HPGQ_HIP_TRY(hipMalloc(&c->d_span_first, S::kMaxSpans * sizeof(int32_t)));
+    HPGQ_HIP_TRY(hipMalloc(&c->d_scratch, cells * 8));
+    HPGQ_HIP_TRY(hipMemsetAsync(c->d_scratch, 0, cells * 8, c->stream));
+    c->s_lds = (cells + 1) * 8 + S::kWaves * 64 * 4;
+    const void *sfn = S::stream_for(k);
+    if (c->s_lds > 64 * 1024)
+      HPGQ_HIP_TRY(hipFuncSetAttribute(sfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->s_lds));
+    int spc = 0;
+    HPGQ_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&spc, sfn, S::kWG, c->s_lds));
+    c->s_grid = std::max(1, spc) * cus;
+  }
   *cg = c;
   return HPGQ_OK;
 }
@@ -712,6 +787,9 @@ void hpgq_cgr_close(hpgq_cgr_t *c) {
   (void)hipFree(c->d_e);
   (void)hipFree(c->d_flags);
   (void)hipFree(c->d_sum);
+  (void)hipFree(c->d_gate);
+  (void)hipFree(c->d_span_first);
+  (void)hipFree(c->d_scratch);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -743,6 +821,36 @@ int hpgq_cgr_fill_device(hpgq_cgr_t *c, const hpgq_batch_t *b, const uint8_t *st
   A.flags = c->d_flags;
   A.sum = c->d_sum;
   A.replays = c->d_replays;
+  A.gate = nullptr;
+  // the stream path: all reads, k <= 7; the exact kernels then run only if it
+  // sets the gate
+  c->streamed = c->path == HPGQ_CGR_PATH_AUTO && mode == HPGQ_CGR_ALL_READS &&
+                c->k <= hpgq::cgr::stream::kMaxK;
+  if (c->streamed) {
+    namespace S = hpgq::cgr::stream;
+    S::SArgs SA;
+    SA.seq = b->seq;
+    SA.qual = b->quality;
+    SA.idx = b->data_indices;
+    SA.num_reads = n;
+    SA.base_quality = c->base_quality;
+    SA.span_first = c->d_span_first;
+    SA.scratch = c->d_scratch;
+    SA.gate = c->d_gate;
+    SA.ts = c->d_ts;
+    SA.tq = c->d_tq;
+    SA.words = c->d_words;
+    void *sargs[] = {&SA};
+    HPGQ_HIP_TRY(hipMemsetAsync(c->d_gate, 0, 4, c->stream));
+    HPGQ_HIP_TRY(hipLaunchKernel((const void *)S::span_first_kernel, dim3((unsigned)((n + 1 + 255) / 256)),
+                                 dim3(256), sargs, 0, c->stream));
+    HPGQ_HIP_TRY(hipLaunchKernel(S::stream_for(c->k), dim3(c->s_grid), dim3(S::kWG), sargs, c->s_lds,
+                                 c->stream));
+    const int cells = 1 << (2 * c->k);
+    HPGQ_HIP_TRY(hipLaunchKernel(S::finalize_for(c->k), dim3((unsigned)((cells + 255) / 256)), dim3(256),
+                                 sargs, 0, c->stream));
+    A.gate = c->d_gate;
+  }
   void *args[] = {&A};
   const int64_t need = (n + hpgq::cgr::kWG - 1) / hpgq::cgr::kWG;
   const int grid = (int)std::min<int64_t>(need, c->grid);
@@ -763,6 +871,9 @@ int hpgq_cgr_sync(hpgq_cgr_t *c) {
     unsigned long long r = 0;
     HPGQ_HIP_TRY(hipMemcpy(&r, c->d_replays, 8, hipMemcpyDeviceToHost));
     c->last_replays = (int64_t)r;
+    uint32_t g = 1;
+    if (c->streamed) HPGQ_HIP_TRY(hipMemcpy(&g, c->d_gate, 4, hipMemcpyDeviceToHost));
+    c->last_exact = (g & hpgq::cgr::stream::GATE_EXACT) ? 1 : 0;
     c->pending = false;
   }
   return HPGQ_OK;
@@ -796,5 +907,13 @@ int hpgq_cgr_read(hpgq_cgr_t *c, uint32_t *table_seq, uint32_t *table_q, uint32_
 void *hpgq_cgr_stream(hpgq_cgr_t *c) { return c ? (void *)c->stream : nullptr; }
 
 int64_t hpgq_cgr_last_replays(hpgq_cgr_t *c) { return c ? c->last_replays : 0; }
+
+int hpgq_cgr_set_path(hpgq_cgr_t *c, int path) {
+  if (!c || (path != HPGQ_CGR_PATH_AUTO && path != HPGQ_CGR_PATH_EXACT)) return HPGQ_E_INVALID;
+  c->path = path;
+  return HPGQ_OK;
+}
+
+int hpgq_cgr_last_exact(hpgq_cgr_t *c) { return c ? c->last_exact : HPGQ_E_INVALID; }
 
 }  // extern "C"

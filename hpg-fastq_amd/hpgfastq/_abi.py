@@ -15,6 +15,7 @@ NUM_SCALARS = 8
  S_NUM_STATS, S_ACC_MEANQ_FX16, S_LONG_READS) = range(7)
 MEANQ_BINS, GC_BINS = 256, 101
 CGR_ALL_READS, CGR_ONLY_VALID_READS = 0, 1
+CGR_PATH_AUTO, CGR_PATH_EXACT = 0, 1
 
 ERRORS = {0: "ok", -1: "invalid argument", -2: "HIP runtime error", -3: "out of memory",
           -4: "read longer than lmax", -5: "no HIP device", -6: "RCCL error",
@@ -114,6 +115,8 @@ _SIGS = [
     ("hpgq_cgr_read", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     ("hpgq_cgr_stream", C.c_void_p, [C.c_void_p]),
     ("hpgq_cgr_last_replays", C.c_int64, [C.c_void_p]),
+    ("hpgq_cgr_set_path", C.c_int, [C.c_void_p, C.c_int]),
+    ("hpgq_cgr_last_exact", C.c_int, [C.c_void_p]),
     ("hpgq_kmers_open", C.c_int, [C.POINTER(C.c_void_p), C.c_int, C.c_int, C.c_void_p]),
     ("hpgq_kmers_close", None, [C.c_void_p]),
     ("hpgq_kmers_count_device", C.c_int, [C.c_void_p, C.POINTER(Batch), C.c_void_p]),

@@ -124,12 +124,13 @@ def summary(counter_set, lmax):
 class ChaosGame:
     """hpgq_cgr: chaos_game_fill_tables on the device (old/chaos_game.c:165)."""
 
-    def __init__(self, k, base_quality=33, device=0):
+    def __init__(self, k, base_quality=33, device=0, path=0):
         self.k = k
         self.dim = 1 << k
         h = C.c_void_p()
         check(lib.hpgq_cgr_open(C.byref(h), device, k, base_quality), "hpgq_cgr_open")
         self._h = h
+        check(lib.hpgq_cgr_set_path(h, path), "hpgq_cgr_set_path")
 
     def close(self):
         if self._h:
@@ -158,6 +159,11 @@ class ChaosGame:
 
     def last_replays(self):
         return int(lib.hpgq_cgr_last_replays(self._h))
+
+    def last_exact(self):
+        """1 if the last synced fill ran the exact double simulation, 0 if the
+        stream pass was proven exact (hpgq_cgr_last_exact)."""
+        return int(lib.hpgq_cgr_last_exact(self._h))
 
     def tables(self):
         cells = self.dim * self.dim

@@ -280,6 +280,21 @@ void *hpgq_cgr_stream(hpgq_cgr_t *cg);
 /* reads the last fill call had to replay sequentially (diagnostic) */
 int64_t hpgq_cgr_last_replays(hpgq_cgr_t *cg);
 
+/*
+ * Path selection.  AUTO (default): for k <= 7 and ALL_READS a coalesced
+ * integer pass computes each word's cell from its own k bases, which is
+ * provably the reference's (int)f cell unless some axis sees a run of
+ * >= 48-k toward-dim moves or the batch holds bytes other than A/C/G/T/N or
+ * qualities >= 128; such a call is redone by the exact double simulation on
+ * the device.  EXACT: always the exact simulation.  Both are bit-identical
+ * to old/chaos_game.c:165-267.
+ */
+#define HPGQ_CGR_PATH_AUTO  0
+#define HPGQ_CGR_PATH_EXACT 1
+int  hpgq_cgr_set_path(hpgq_cgr_t *cg, int path);
+/* 1 if the last (synced) fill ran the exact simulation, 0 if the stream pass sufficed */
+int  hpgq_cgr_last_exact(hpgq_cgr_t *cg);
+
 /* ---------------------------------------------------------------------- */
 /* stats --kmers: 5-mer counts (src/stats_options.c:274, merge              */
 /* src/stats_fastq.c:384-410, report src/stats_report.c:492-563)            */

@@ -27,8 +27,9 @@ def _dev(reads, status=None):
     return t
 
 
-def gpu_cgr(k, batches, statuses=None, mode=H.CGR_ALL_READS, base_quality=33):
-    cg = H.ChaosGame(k, base_quality)
+def gpu_cgr(k, batches, statuses=None, mode=H.CGR_ALL_READS, base_quality=33,
+            path=H.CGR_PATH_AUTO, exact_log=None):
+    cg = H.ChaosGame(k, base_quality, path=path)
     replays = 0
     keep = []
     for i, reads in enumerate(batches):
@@ -40,12 +41,14 @@ def gpu_cgr(k, batches, statuses=None, mode=H.CGR_ALL_READS, base_quality=33):
         cg.fill_device(b, t["status"].data_ptr() if st is not None else None, mode)
         cg.sync()
         replays += cg.last_replays()
+        if exact_log is not None:
+            exact_log.append(cg.last_exact())
     ts, tq, wc = cg.tables()
     cg.close()
     return ts.reshape(-1), tq.reshape(-1), wc, replays
 
 
-def oracle_cgr(k, batches, statuses=None, mode=0, base_quality=33):
+def oracle_cgr(k, batches, statuses=None, mode=0, base_quality=33, path=None, exact_log=None):
     dim = 1 << k
     tables = (np.zeros(dim * dim, np.uint32), np.zeros(dim * dim, np.uint32),
               np.zeros(1, np.uint32))
@@ -85,16 +88,75 @@ def test_cgr_committed_vector_k7():
     assert wc == int(z["word_count"])
 
 
+@pytest.mark.parametrize("path", [H.CGR_PATH_AUTO, H.CGR_PATH_EXACT])
 @pytest.mark.parametrize("k", [1, 3, 5, 7, 8])
-def test_cgr_synthetic_multi_batch(k):
+def test_cgr_synthetic_multi_batch(k, path):
     batches = [O.synth(3000, seed=5 + i, L=250, first=i * 3000) for i in range(3)]
-    assert_cgr(k, batches)
+    log = []
+    assert_cgr(k, batches, path=path, exact_log=log)
+    # random reads: the stream pass is proven exact for k <= 7
+    assert log == [0 if (path == H.CGR_PATH_AUTO and k <= 7) else 1] * 3
 
 
-def test_cgr_large_batch_k7():
+@pytest.mark.parametrize("path", [H.CGR_PATH_AUTO, H.CGR_PATH_EXACT])
+def test_cgr_large_batch_k7(path):
     reads = O.synth(200_000, seed=5, L=250)
-    rep = assert_cgr(7, [reads])
+    log = []
+    rep = assert_cgr(7, [reads], path=path, exact_log=log)
     assert rep == 0   # random context: every speculative entry state is exact
+    assert log == [0 if path == H.CGR_PATH_AUTO else 1]
+
+
+def _run_batch(rng, k, run_len, n=900, split=False):
+    """Random reads with D-move runs of run_len on x (A/T), y (G/T) or both
+    (T), N sprinkled inside the runs (N does not move f), some runs split
+    across two reads (f is carried across reads), at random offsets."""
+    pairs = []
+    alph = {0: b"AT", 1: b"GT", 2: b"T"}
+    i = 0
+    while len(pairs) < n:
+        L = int(rng.integers(30, 300))
+        mix = np.array(rng.choice(list(b"ACGT"), L), np.uint8).tobytes()
+        if i % 5 == 0:
+            ax = (i // 5) % 3
+            run = bytes(rng.choice(list(alph[ax]), run_len).astype(np.uint8))
+            if i % 2:
+                pos = sorted(rng.choice(run_len, 3, replace=False))
+                run = run[:pos[0]] + b"N" + run[pos[0]:pos[1]] + b"NN" + run[pos[1]:]
+            # a Z on that axis on both sides so the run is exactly run_len long
+            z = {0: b"C", 1: b"A", 2: b"C"}[ax]
+            if split:
+                cut = int(rng.integers(1, len(run)))
+                a = mix[: L // 2] + z + run[:cut]
+                b = run[cut:] + z + mix[L // 2:]
+                pairs.append((a, bytes(rng.integers(33, 75, len(a)).astype(np.uint8))))
+                pairs.append((b, bytes(rng.integers(33, 75, len(b)).astype(np.uint8))))
+                i += 1
+                continue
+            off = int(rng.integers(0, L))
+            sq = mix[:off] + z + run + z + mix[off:]
+        else:
+            sq = mix
+        pairs.append((sq, bytes(rng.integers(33, 75, len(sq)).astype(np.uint8))))
+        i += 1
+    return O.Reads.from_pairs(pairs)
+
+
+@pytest.mark.parametrize("split", [False, True])
+@pytest.mark.parametrize("k", [1, 2, 4, 7])
+def test_cgr_stream_threshold_runs(k, split):
+    """Runs of 47-k toward-dim moves stay on the stream path (and match the
+    oracle); runs of 48-k set the gate and the exact simulation redoes the
+    call (hpgq_cgr_stream.h: the cell is provably (int)f below 50-k)."""
+    rng = np.random.default_rng(100 + k + 7 * split)
+    below = _run_batch(rng, k, 47 - k, split=split)
+    at = _run_batch(rng, k, 48 - k, split=split)
+    log = []
+    assert_cgr(k, [below], exact_log=log)
+    assert log == [0]
+    log = []
+    assert_cgr(k, [at], exact_log=log)
+    assert log == [1]
 
 
 def _homopolymer_batch(rng, n=700, L=120):
@@ -118,8 +180,10 @@ def _homopolymer_batch(rng, n=700, L=120):
 
 def test_cgr_homopolymers_replay_exactly():
     rng = np.random.default_rng(3)
-    rep = assert_cgr(7, [_homopolymer_batch(rng)])
+    log = []
+    rep = assert_cgr(7, [_homopolymer_batch(rng)], exact_log=log)
     assert rep >= 0
+    assert log == [1]   # poly-A/T: the stream pass sets the gate
 
 
 @pytest.mark.parametrize("k", [2, 7, 9])
@@ -145,7 +209,9 @@ def test_cgr_edge_bytes_and_lengths():
              (b"RYKMACGTACGTACGT", b"?" * 16)] * 40
     reads = O.Reads.from_pairs(pairs)
     for k in (1, 2, 7, 12):
-        assert_cgr(k, [reads])
+        log = []
+        assert_cgr(k, [reads], exact_log=log)
+        assert log == [1]   # lowercase / IUPAC / qualities >= 128: exact path
 
 
 def test_cgr_only_valid_reads():
@@ -155,10 +221,10 @@ def test_cgr_only_valid_reads():
     assert_cgr(7, [reads], statuses=[status], mode=H.CGR_ONLY_VALID_READS)
 
 
-def test_cgr_absolute_offsets():
+@pytest.mark.parametrize("off", [37, 16384 - 5, 3 * 16384 + 9])
+def test_cgr_absolute_offsets(off):
     """data_indices need not start at 0 (a slice of a larger buffer)."""
     reads = O.synth(2000, seed=4, L=150)
-    off = 37
     seq = np.concatenate([np.full(off, ord("G"), np.uint8), reads.seq])
     qual = np.concatenate([np.full(off, 60, np.uint8), reads.qual])
     shifted = O.Reads(seq, qual, reads.idx + off)
@@ -167,3 +233,41 @@ def test_cgr_absolute_offsets():
     np.testing.assert_array_equal(ts, os_)
     np.testing.assert_array_equal(tq, oq)
     assert wc == ow
+
+
+@pytest.mark.parametrize("L", [1, 5, 16, 17, 63, 150])
+def test_cgr_stream_short_and_ragged_reads(L):
+    """Many reads per 16-byte lane / per tile (the start-bitmap cursor loops),
+    N-only reads (long transparent stretches), ragged lengths, k = 3 and 7."""
+    rng = np.random.default_rng(L)
+    pairs = []
+    for i in range(6000):
+        n = int(rng.integers(0, L + 1))
+        sq = (b"N" * n) if i % 97 == 0 else np.array(rng.choice(list(b"ACGTN"), n, p=[.24, .24, .24, .24, .04]), np.uint8).tobytes()
+        pairs.append((sq, bytes(rng.integers(33, 75, n).astype(np.uint8))))
+    reads = O.Reads.from_pairs(pairs)
+    for k in (3, 7):
+        log = []
+        assert_cgr(k, [reads], exact_log=log)
+        assert log == [0]
+
+
+def test_cgr_stream_long_n_stretch():
+    """A 40 KB stretch of N (several spans with no move at all) between
+    A-runs: the runs on either side are counted as one (N does not move f)."""
+    rng = np.random.default_rng(5)
+    mix = lambda n: np.array(rng.choice(list(b"ACGT"), n), np.uint8).tobytes()  # noqa: E731
+    pairs = [(mix(200), b"I" * 200) for _ in range(50)]
+    pairs.append((mix(50) + b"C" + b"A" * 25, b"I" * 76))
+    pairs += [(b"N" * 200, b"#" * 200) for _ in range(200)]
+    pairs.append((b"A" * 25 + b"C" + mix(50), b"I" * 76))
+    pairs += [(mix(200), b"I" * 200) for _ in range(50)]
+    reads = O.Reads.from_pairs(pairs)
+    log = []
+    assert_cgr(7, [reads], exact_log=log)
+    assert log == [1]   # 50 A's across the N stretch >= 41
+    pairs[50] = (pairs[50][0][:-10] + b"C" * 10, b"I" * 76)   # now 15 + 25 = 40 < 41
+    reads = O.Reads.from_pairs(pairs)
+    log = []
+    assert_cgr(7, [reads], exact_log=log)
+    assert log == [0]
