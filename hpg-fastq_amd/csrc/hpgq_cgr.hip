@@ -35,6 +35,7 @@
 #include "hpgq_common.h"
 
 #include <algorithm>
+#include <vector>
 
 namespace hpgq {
 namespace cgr {
@@ -59,12 +60,7 @@ struct Args {
   unsigned long long *flags; // [ceil(n/64)] one bit per read
   unsigned long long *sum;   // [ceil(n/4096)] one bit per nonzero flags word
   unsigned long long *replays;
-  const uint32_t *gate;      // stream path: run only when the gate says so (null: always)
 };
-
-__device__ __forceinline__ bool gated_out(const Args &A) {
-  return A.gate && (__builtin_amdgcn_readfirstlane(*A.gate) & 1u) == 0u;
-}
 
 struct Src {
   __amdgpu_buffer_rsrc_t rs, rq;
@@ -474,7 +470,6 @@ __device__ State guess_entry(const Args &A, const Src &S, const uint8_t *cls, in
 
 template <int K>
 __global__ void __launch_bounds__(kWG) cgr_fill_kernel(Args A) {
-  if (gated_out(A)) return;
   constexpr int dim = 1 << K;
   constexpr bool kLds = K <= kLdsMaxK;
   constexpr int cells = dim * dim + 1;   // + the spare cell of the unconditional adds
@@ -523,7 +518,6 @@ __device__ __forceinline__ bool same(double2 a, double2 b) {
 
 // flag r iff its guessed entry state differs (bitwise) from e_{r-1}
 __global__ void __launch_bounds__(256) cgr_check_kernel(Args A) {
-  if (gated_out(A)) return;
   const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const bool f = r > 0 && r < A.num_reads && !same(A.g[r], A.e[r - 1]);
   const unsigned long long b = __ballot(f);
@@ -537,10 +531,6 @@ __global__ void __launch_bounds__(256) cgr_check_kernel(Args A) {
 // one lane: replay flagged reads in order with their true entry states
 template <int K>
 __global__ void __launch_bounds__(64) cgr_fix_kernel(Args A) {
-  if (gated_out(A)) {
-    if (threadIdx.x == 0) *A.replays = 0;
-    return;
-  }
   __shared__ uint8_t cls[256];
   fill_classes(cls, threadIdx.x, 64);
   __syncthreads();
@@ -645,33 +635,15 @@ namespace hpgq {
 namespace cgr {
 namespace stream {
 
-template <int K>
-struct SKernels {
-  static const void *fill() { return (const void *)cgr_stream_kernel<K>; }
-  static const void *fin() { return (const void *)cgr_stream_finalize_kernel<K>; }
-};
-
 static const void *stream_for(int k) {
   switch (k) {
-    case 1: return SKernels<1>::fill();
-    case 2: return SKernels<2>::fill();
-    case 3: return SKernels<3>::fill();
-    case 4: return SKernels<4>::fill();
-    case 5: return SKernels<5>::fill();
-    case 6: return SKernels<6>::fill();
-    default: return SKernels<7>::fill();
-  }
-}
-
-static const void *finalize_for(int k) {
-  switch (k) {
-    case 1: return SKernels<1>::fin();
-    case 2: return SKernels<2>::fin();
-    case 3: return SKernels<3>::fin();
-    case 4: return SKernels<4>::fin();
-    case 5: return SKernels<5>::fin();
-    case 6: return SKernels<6>::fin();
-    default: return SKernels<7>::fin();
+    case 1: return (const void *)cgr_stream_kernel<1>;
+    case 2: return (const void *)cgr_stream_kernel<2>;
+    case 3: return (const void *)cgr_stream_kernel<3>;
+    case 4: return (const void *)cgr_stream_kernel<4>;
+    case 5: return (const void *)cgr_stream_kernel<5>;
+    case 6: return (const void *)cgr_stream_kernel<6>;
+    default: return (const void *)cgr_stream_kernel<7>;
   }
 }
 
@@ -691,15 +663,17 @@ struct hpgq_cgr {
   size_t lds = 0;
   int grid = 0;
   int64_t last_replays = 0;
-  bool pending = false;       // a fill whose replay count was not read back yet
-  // stream path (k <= 7, all reads): see hpgq_cgr_stream.h
+  // stream path (k <= 7, all reads; hpgq_cgr_stream.h).  Each streamed fill
+  // gets a gate/done slot; the exact simulation of a fill whose gate is set
+  // runs at the next sync (the batch must stay valid until then, as for any
+  // asynchronous fill).
   int path = HPGQ_CGR_PATH_AUTO;
-  bool streamed = false;      // the last fill went through the stream kernels
-  int last_exact = 1;
   int32_t *d_span_first = nullptr;
   unsigned long long *d_scratch = nullptr;
-  uint32_t *d_gate = nullptr;
-  size_t s_lds = 0;
+  uint32_t *d_slots = nullptr;            // [kSlots][2]: gate, done
+  std::vector<hpgq_batch_t> pending;      // streamed fills not synced yet (slot = index)
+  bool ran_exact = false;                 // an exact simulation ran since the last sync
+  int last_exact = 0;
   int s_grid = 0;
 };
 
@@ -720,6 +694,41 @@ static int cgr_ensure(hpgq_cgr *c, int64_t n) {
       hipMalloc(&c->d_flags, nw * 8) != hipSuccess || hipMalloc(&c->d_sum, ns * 8) != hipSuccess)
     return HPGQ_E_NOMEM;
   c->cap = cap;
+  return HPGQ_OK;
+}
+
+// the exact double simulation of one call (cgr_fill / check / fix)
+static int cgr_exact(hpgq_cgr *c, const hpgq_batch_t *b, const uint8_t *status, int mode) {
+  int rc = cgr_ensure(c, b->num_reads);
+  if (rc) return rc;
+  const int64_t n = b->num_reads;
+  const int64_t nw = (n + 63) / 64, ns = (nw + 63) / 64;
+  HPGQ_HIP_TRY(hipMemsetAsync(c->d_sum, 0, ns * 8, c->stream));
+  hpgq::cgr::Args A;
+  A.seq = b->seq;
+  A.qual = b->quality;
+  A.idx = b->data_indices;
+  A.status = status;
+  A.mode = mode;
+  A.num_reads = n;
+  A.base_quality = c->base_quality;
+  A.ts = c->d_ts;
+  A.tq = c->d_tq;
+  A.words = c->d_words;
+  A.g = c->d_g;
+  A.e = c->d_e;
+  A.flags = c->d_flags;
+  A.sum = c->d_sum;
+  A.replays = c->d_replays;
+  void *args[] = {&A};
+  const int64_t need = (n + hpgq::cgr::kWG - 1) / hpgq::cgr::kWG;
+  const int grid = (int)std::min<int64_t>(need, c->grid);
+  HPGQ_HIP_TRY(hipLaunchKernel(hpgq::cgr::fill_for(c->k), dim3(grid), dim3(hpgq::cgr::kWG), args,
+                               c->lds, c->stream));
+  HPGQ_HIP_TRY(hipLaunchKernel((const void *)hpgq::cgr::cgr_check_kernel, dim3((unsigned)((n + 255) / 256)),
+                               dim3(256), args, 0, c->stream));
+  HPGQ_HIP_TRY(hipLaunchKernel(hpgq::cgr::fix_for(c->k), dim3(1), dim3(64), args, 0, c->stream));
+  c->ran_exact = true;
   return HPGQ_OK;
 }
 
@@ -756,20 +765,17 @@ int hpgq_cgr_open(hpgq_cgr_t **cg, int device, int k, int base_quality) {
   HPGQ_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, hpgq::cgr::kWG, c->lds));
   HPGQ_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
   c->grid = std::max(1, per_cu) * cus;
-  HPGQ_HIP_TRY(hipMalloc(&c->d_gate, 4));
-  HPGQ_HIP_TRY(hipMemsetAsync(c->d_gate, 0, 4, c->stream));
   if (k <= hpgq::cgr::stream::kMaxK) {
     namespace S = hpgq::cgr::stream;
     HPGQ_HIP_TRY(hipMalloc(&c->d_span_first, S::kMaxSpans * sizeof(int32_t)));
     HPGQ_HIP_TRY(hipMalloc(&c->d_scratch, cells * 8));
     HPGQ_HIP_TRY(hipMemsetAsync(c->d_scratch, 0, cells * 8, c->stream));
-    c->s_lds = (cells + 1) * 8 + S::kWaves * 64 * 4;
-    const void *sfn = S::stream_for(k);
-    if (c->s_lds > 64 * 1024)
-      HPGQ_HIP_TRY(hipFuncSetAttribute(sfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)c->s_lds));
+    HPGQ_HIP_TRY(hipMalloc(&c->d_slots, S::kSlots * 2 * sizeof(uint32_t)));
+    HPGQ_HIP_TRY(hipMemsetAsync(c->d_slots, 0, S::kSlots * 2 * sizeof(uint32_t), c->stream));
     int spc = 0;
-    HPGQ_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&spc, sfn, S::kWG, c->s_lds));
+    HPGQ_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&spc, S::stream_for(k), S::kWG, 0));
     c->s_grid = std::max(1, spc) * cus;
+    c->pending.reserve(S::kSlots);
   }
   *cg = c;
   return HPGQ_OK;
@@ -787,9 +793,9 @@ void hpgq_cgr_close(hpgq_cgr_t *c) {
   (void)hipFree(c->d_e);
   (void)hipFree(c->d_flags);
   (void)hipFree(c->d_sum);
-  (void)hipFree(c->d_gate);
   (void)hipFree(c->d_span_first);
   (void)hipFree(c->d_scratch);
+  (void)hipFree(c->d_slots);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -800,66 +806,33 @@ int hpgq_cgr_fill_device(hpgq_cgr_t *c, const hpgq_batch_t *b, const uint8_t *st
   if (b->num_reads == 0) return HPGQ_OK;
   if (!b->seq || !b->quality || !b->data_indices) return HPGQ_E_INVALID;
   HPGQ_HIP_TRY(hipSetDevice(c->device));
-  int rc = cgr_ensure(c, b->num_reads);
-  if (rc) return rc;
-  const int64_t n = b->num_reads;
-  const int64_t nw = (n + 63) / 64, ns = (nw + 63) / 64;
-  HPGQ_HIP_TRY(hipMemsetAsync(c->d_sum, 0, ns * 8, c->stream));
-  hpgq::cgr::Args A;
-  A.seq = b->seq;
-  A.qual = b->quality;
-  A.idx = b->data_indices;
-  A.status = status;
-  A.mode = mode;
-  A.num_reads = n;
-  A.base_quality = c->base_quality;
-  A.ts = c->d_ts;
-  A.tq = c->d_tq;
-  A.words = c->d_words;
-  A.g = c->d_g;
-  A.e = c->d_e;
-  A.flags = c->d_flags;
-  A.sum = c->d_sum;
-  A.replays = c->d_replays;
-  A.gate = nullptr;
-  // the stream path: all reads, k <= 7; the exact kernels then run only if it
-  // sets the gate
-  c->streamed = c->path == HPGQ_CGR_PATH_AUTO && mode == HPGQ_CGR_ALL_READS &&
-                c->k <= hpgq::cgr::stream::kMaxK;
-  if (c->streamed) {
-    namespace S = hpgq::cgr::stream;
-    S::SArgs SA;
-    SA.seq = b->seq;
-    SA.qual = b->quality;
-    SA.idx = b->data_indices;
-    SA.num_reads = n;
-    SA.base_quality = c->base_quality;
-    SA.span_first = c->d_span_first;
-    SA.scratch = c->d_scratch;
-    SA.gate = c->d_gate;
-    SA.ts = c->d_ts;
-    SA.tq = c->d_tq;
-    SA.words = c->d_words;
-    void *sargs[] = {&SA};
-    HPGQ_HIP_TRY(hipMemsetAsync(c->d_gate, 0, 4, c->stream));
-    HPGQ_HIP_TRY(hipLaunchKernel((const void *)S::span_first_kernel, dim3((unsigned)((n + 1 + 255) / 256)),
-                                 dim3(256), sargs, 0, c->stream));
-    HPGQ_HIP_TRY(hipLaunchKernel(S::stream_for(c->k), dim3(c->s_grid), dim3(S::kWG), sargs, c->s_lds,
-                                 c->stream));
-    const int cells = 1 << (2 * c->k);
-    HPGQ_HIP_TRY(hipLaunchKernel(S::finalize_for(c->k), dim3((unsigned)((cells + 255) / 256)), dim3(256),
-                                 sargs, 0, c->stream));
-    A.gate = c->d_gate;
+  const bool streamed = c->path == HPGQ_CGR_PATH_AUTO && mode == HPGQ_CGR_ALL_READS &&
+                        c->k <= hpgq::cgr::stream::kMaxK;
+  if (!streamed) return cgr_exact(c, b, status, mode);
+  namespace S = hpgq::cgr::stream;
+  if ((int)c->pending.size() == S::kSlots) {   // out of slots: settle the ones in flight
+    int rc = hpgq_cgr_sync(c);
+    if (rc) return rc;
   }
-  void *args[] = {&A};
-  const int64_t need = (n + hpgq::cgr::kWG - 1) / hpgq::cgr::kWG;
-  const int grid = (int)std::min<int64_t>(need, c->grid);
-  HPGQ_HIP_TRY(hipLaunchKernel(hpgq::cgr::fill_for(c->k), dim3(grid), dim3(hpgq::cgr::kWG), args,
-                               c->lds, c->stream));
-  HPGQ_HIP_TRY(hipLaunchKernel((const void *)hpgq::cgr::cgr_check_kernel, dim3((unsigned)((n + 255) / 256)),
-                               dim3(256), args, 0, c->stream));
-  HPGQ_HIP_TRY(hipLaunchKernel(hpgq::cgr::fix_for(c->k), dim3(1), dim3(64), args, 0, c->stream));
-  c->pending = true;
+  const int slot = (int)c->pending.size();
+  S::SArgs SA;
+  SA.seq = b->seq;
+  SA.qual = b->quality;
+  SA.idx = b->data_indices;
+  SA.num_reads = b->num_reads;
+  SA.base_quality = c->base_quality;
+  SA.span_first = c->d_span_first;
+  SA.scratch = c->d_scratch;
+  SA.gate = c->d_slots + 2 * slot;
+  SA.done = c->d_slots + 2 * slot + 1;
+  SA.ts = c->d_ts;
+  SA.tq = c->d_tq;
+  SA.words = c->d_words;
+  void *sargs[] = {&SA};
+  HPGQ_HIP_TRY(hipLaunchKernel((const void *)S::span_first_kernel,
+                               dim3((unsigned)((b->num_reads + 1 + 255) / 256)), dim3(256), sargs, 0, c->stream));
+  HPGQ_HIP_TRY(hipLaunchKernel(S::stream_for(c->k), dim3(c->s_grid), dim3(S::kWG), sargs, 0, c->stream));
+  c->pending.push_back(*b);
   return HPGQ_OK;
 }
 
@@ -867,22 +840,36 @@ int hpgq_cgr_sync(hpgq_cgr_t *c) {
   if (!c) return HPGQ_E_INVALID;
   HPGQ_HIP_TRY(hipSetDevice(c->device));
   HPGQ_HIP_TRY(hipStreamSynchronize(c->stream));
-  if (c->pending) {
+  if (!c->pending.empty()) {
+    // streamed fills whose gate is set: the exact simulation, in fill order
+    std::vector<uint32_t> slots(2 * c->pending.size());
+    HPGQ_HIP_TRY(hipMemcpy(slots.data(), c->d_slots, slots.size() * 4, hipMemcpyDeviceToHost));
+    std::vector<hpgq_batch_t> todo;
+    todo.swap(c->pending);
+    for (size_t i = 0; i < todo.size(); ++i)
+      if (slots[2 * i] & hpgq::cgr::stream::GATE_EXACT) {
+        int rc = cgr_exact(c, &todo[i], nullptr, HPGQ_CGR_ALL_READS);
+        if (rc) return rc;
+      }
+    HPGQ_HIP_TRY(hipStreamSynchronize(c->stream));
+  }
+  if (c->ran_exact) {
     unsigned long long r = 0;
     HPGQ_HIP_TRY(hipMemcpy(&r, c->d_replays, 8, hipMemcpyDeviceToHost));
     c->last_replays = (int64_t)r;
-    uint32_t g = 1;
-    if (c->streamed) HPGQ_HIP_TRY(hipMemcpy(&g, c->d_gate, 4, hipMemcpyDeviceToHost));
-    c->last_exact = (g & hpgq::cgr::stream::GATE_EXACT) ? 1 : 0;
-    c->pending = false;
+  } else {
+    c->last_replays = 0;
   }
+  c->last_exact = c->ran_exact ? 1 : 0;
+  c->ran_exact = false;
   return HPGQ_OK;
 }
 
 int hpgq_cgr_reset(hpgq_cgr_t *c) {
   if (!c) return HPGQ_E_INVALID;
+  int rc = hpgq_cgr_sync(c);   // fills before the reset settle first
+  if (rc) return rc;
   const size_t cells = (size_t)c->dim * c->dim;
-  HPGQ_HIP_TRY(hipSetDevice(c->device));
   HPGQ_HIP_TRY(hipMemsetAsync(c->d_ts, 0, cells * 4, c->stream));
   HPGQ_HIP_TRY(hipMemsetAsync(c->d_tq, 0, cells * 4, c->stream));
   HPGQ_HIP_TRY(hipMemsetAsync(c->d_words, 0, 8, c->stream));

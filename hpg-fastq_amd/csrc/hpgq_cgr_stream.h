@@ -36,18 +36,20 @@
 // sets the gate and the exact kernels redo the whole call.
 //
 // Layout: the bytes [idx[0], idx[n]) are cut into spans of kSpan bytes; a
-// wave takes a span as 16 tiles of 1 KB, a lane 16 contiguous bytes of seq
-// and of quality per tile (one 16-byte load each, fully coalesced).  The K-1
-// bytes of context come from the neighbouring lane by DPP (lane 0: the last
-// lane of the previous tile, or a broadcast load at the span start).  Read
-// starts inside a tile are scattered into a per-wave LDS bitmap from the
-// read offsets the wave walks with a cursor.  Words go to the workgroup's
-// LDS table (u64 per cell: count | quality sum << 32, one ds_add_u64 per
-// byte; a byte that ends no word adds to a spare cell), flushed to a global
-// u64 scratch table that the finalize kernel moves into the reference
-// layout.  A run of >= kRun D-moves covers >= 32 whole bytes, so it contains
-// a 16-byte lane with no Z on that axis: only tiles holding such a lane (or
-// entered with a long open run) are scanned exactly, lane by lane.
+// wave takes a span as tiles of 2 KB, a lane 32 contiguous bytes of seq and
+// of quality per tile (16-byte loads, the next tile's in flight while this
+// one is counted).  The K-1 bytes of context come from the neighbouring lane
+// by DPP (lane 0: the last lane of the previous tile, or a broadcast load at
+// the span start).  Read starts inside a tile are scattered into a per-wave
+// LDS bitmap from the read offsets the wave walks with a cursor.  Words go to
+// the workgroup's LDS table (u64 per cell: count | quality sum << 32, one
+// ds_add_u64 per byte; a byte that ends no word adds to a spare cell),
+// flushed to a global u64 scratch table; the last workgroup to finish moves
+// it into the reference layout (or discards it when the gate is set).  A run
+// of >= kRun (>= 41) D-moves covers a whole aligned 16-byte chunk with no Z
+// on that axis; a tile whose chunks all hold a Z on both axes can only hold
+// runs of <= 30, so only tiles with a Z-free chunk (or entered with a long
+// open run) are scanned exactly, lane by lane.
 #pragma once
 
 namespace hpgq {
@@ -56,11 +58,17 @@ namespace stream {
 
 constexpr int kWaves = 16;
 constexpr int kWG = kWaves * 64;
-constexpr int kTile = 1024;                  // bytes per wave tile: 64 lanes x 16
-constexpr int kSpanTiles = 16;
-constexpr int kSpan = kTile * kSpanTiles;    // bytes per span (16 KB)
+#ifndef HPGQ_CGR_LANE_BYTES
+#define HPGQ_CGR_LANE_BYTES 32
+#endif
+constexpr int kLaneBytes = HPGQ_CGR_LANE_BYTES;   // 16 or 32
+constexpr int kNdw = kLaneBytes / 4;
+constexpr int kTile = 64 * kLaneBytes;       // bytes per wave tile (2 KB)
+constexpr int kSpanLog = 14;
+constexpr int kSpan = 1 << kSpanLog;         // bytes per span (16 KB, 8 tiles)
 constexpr int kMaxK = 7;                     // 4^7 u64 cells = 128 KB of LDS
 constexpr int64_t kMaxSpans = ((int64_t)1 << 31) / kSpan + 2;
+constexpr int kSlots = 256;                  // fills in flight between two syncs
 
 constexpr uint32_t GATE_EXACT = 1;   // the exact kernels must run
 
@@ -77,38 +85,36 @@ struct SArgs {
   const int32_t *idx;
   int64_t num_reads;
   uint32_t base_quality;
-  int32_t *span_first;              // [kMaxSpans] first read with idx[r] >= span start - 16
+  int32_t *span_first;              // [kMaxSpans] first read with idx[r] >= span start - 32
   unsigned long long *scratch;      // [4^K] count | quality sum << 32
-  uint32_t *gate;                   // GATE_EXACT when the batch needs the exact path
+  uint32_t *gate;                   // this fill's slot: GATE_EXACT when it needs the exact path
+  uint32_t *done;                   // this fill's slot: workgroups finished
   uint32_t *ts, *tq;                // final tables [dim][dim]
   unsigned long long *words;
 };
 
-__device__ __forceinline__ int32_t batch_lo(const SArgs &A) {
-  return __builtin_amdgcn_readfirstlane(A.idx[0]);
-}
-__device__ __forceinline__ int32_t batch_hi(const SArgs &A) {
-  return __builtin_amdgcn_readfirstlane(A.idx[A.num_reads]);
-}
-
 // spans start at a0 = idx[0] rounded down to 16 bytes
 __device__ __forceinline__ int64_t nspans(int32_t a0, int32_t b1) {
-  return b1 > a0 ? ((int64_t)b1 - a0 + kSpan - 1) / kSpan : 0;
+  return b1 > a0 ? ((int64_t)b1 - a0 + kSpan - 1) >> kSpanLog : 0;
 }
 
-// span_first[s] = the first read r with idx[r] >= a0 + s*kSpan - 16: thread r
-// writes the spans whose (start - 16) lies in (idx[r-1], idx[r]]
+// span_first[s] = the first read r with idx[r] >= a0 + s*kSpan - 32: thread r
+// writes the spans whose (start - 32) lies in (idx[r-1], idx[r]]; thread 0
+// also clears this fill's gate and done slots
 __global__ void __launch_bounds__(256) span_first_kernel(SArgs A) {
   const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (r == 0) {
+    *A.gate = 0u;
+    *A.done = 0u;
+  }
   if (r > A.num_reads) return;
   const int32_t b0 = A.idx[0], b1 = A.idx[A.num_reads];
   const int32_t a0 = b0 & ~15;
   const int64_t ns = nspans(a0, b1);
-  const int64_t hi = (int64_t)A.idx[r] + 16 - a0;   // s*kSpan <= hi
-  const int64_t lo = r == 0 ? -1 : (int64_t)A.idx[r - 1] + 16 - a0;   // s*kSpan > lo
-  int64_t s0 = lo < 0 ? 0 : lo / kSpan + 1;
-  int64_t s1 = hi < 0 ? -1 : hi / kSpan;
-  if (r == A.num_reads) s1 = ns - 1;   // spans past the last start: the end sentinel
+  const int64_t hi = (int64_t)A.idx[r] + 32 - a0;   // s*kSpan <= hi
+  const int64_t lo = r == 0 ? -1 : (int64_t)A.idx[r - 1] + 32 - a0;   // s*kSpan > lo
+  const int64_t s0 = lo < 0 ? 0 : (lo >> kSpanLog) + 1;
+  const int64_t s1 = r == A.num_reads ? ns - 1 : (hi >> kSpanLog);   // past the last start: the end sentinel
   for (int64_t s = s0; s <= s1 && s < ns; ++s) A.span_first[s] = (int32_t)r;
 }
 
@@ -116,40 +122,41 @@ __device__ __forceinline__ uint32_t dpp_shr1(uint32_t old, uint32_t v) {   // la
   return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x138, 0xF, 0xF, false);
 }
 
-// sum of the 4 bytes of x (v_sad_u8 against 0) plus c
-__device__ __forceinline__ uint32_t sad4(uint32_t x, uint32_t c) {
-  return __builtin_amdgcn_sad_u8(x, 0u, c);
-}
-
-// 16 bytes of seq: LUT lookups, exactness and per-lane summaries
+// a lane's bytes of seq: LUT lookups, exactness and per-lane summaries
 struct Cls {
-  uint32_t xy[4];   // per byte: (x | y << 1) << 3
-  uint32_t v;       // bit j: byte j is A/C/G/T
-  uint32_t zany;    // OR of per-byte Z bits (bit0 x, bit1 y) over the bytes
-  uint32_t bad;     // nonzero: a byte that is not exactly A/C/G/T/N
+  uint32_t xy[kNdw];   // per byte: (x | y << 1) << 3
+  uint32_t v;          // bit j: byte j is A/C/G/T
+  uint32_t zlo, zhi;   // OR of per-byte Z bits (bit0 x, bit1 y) over the first / last 16 bytes
+  uint32_t bad;        // nonzero: a byte that is not exactly A/C/G/T/N
 };
 
-__device__ __forceinline__ Cls classify(const uint32_t s[4]) {
+__device__ __forceinline__ Cls classify(const uint32_t s[kNdw]) {
   Cls c;
-  uint32_t bad = 0, z = 0, v0 = 0, v1 = 0;
+  uint32_t bad = 0, zl = 0, zh = 0, vp[kNdw / 2];
 #pragma unroll
-  for (int d = 0; d < 4; ++d) {
+  for (int d = 0; d < kNdw / 2; ++d) vp[d] = 0u;
+#pragma unroll
+  for (int d = 0; d < kNdw; ++d) {
     const uint32_t code = s[d] & 0x07070707u;
     bad |= s[d] ^ __builtin_amdgcn_perm(hpgq::cgr::kExHi, hpgq::cgr::kExLo, code);
     c.xy[d] = __builtin_amdgcn_perm(kXYHi, kXYLo, code);
-    z |= __builtin_amdgcn_perm(kZHi, kZLo, code);
-    // gather the V bit of byte j to bit j: byte values 1,2,4,8 (<< 4 for the odd dword), summed
+    const uint32_t z = __builtin_amdgcn_perm(kZHi, kZLo, code);
+    if (d < 4) zl |= z;
+    if (d >= kNdw - 4) zh |= z;
+    // gather the V bit of byte j to bit j: byte weights 1,2,4,8 (<< 4 for odd dwords), v_sad_u8 sums
     const uint32_t vb = __builtin_amdgcn_perm(kVHi, kVLo, code) & ((d & 1) ? 0x80402010u : 0x08040201u);
-    if (d < 2) v0 = sad4(vb, v0);
-    else v1 = sad4(vb, v1);
+    vp[d >> 1] = __builtin_amdgcn_sad_u8(vb, 0u, vp[d >> 1]);
   }
-  c.v = v0 | (v1 << 8);
-  c.zany = z;
+  c.v = 0;
+#pragma unroll
+  for (int d = 0; d < kNdw / 2; ++d) c.v |= vp[d] << (8 * d);
+  c.zlo = zl;
+  c.zhi = zh;
   c.bad = bad;
   return c;
 }
 
-// per-lane run summary of one axis over its 16 bytes (rare path)
+// per-lane run summary of one axis over its 32 bytes (rare path)
 struct RunSum {
   uint32_t pfx, sfx, cnt, hz;
 };
@@ -158,7 +165,7 @@ template <int AX>
 __device__ __forceinline__ RunSum run_sum(const Cls &c) {
   RunSum r = {0u, 0u, 0u, 0u};
 #pragma unroll
-  for (int j = 0; j < 16; ++j) {
+  for (int j = 0; j < kLaneBytes; ++j) {
     if (!((c.v >> j) & 1u)) continue;
     const uint32_t d = (c.xy[j >> 2] >> (8 * (j & 3) + 3 + AX)) & 1u;
     if (d) {
@@ -211,20 +218,56 @@ __device__ uint32_t run_before(const SArgs &A, int32_t b0, int32_t at, uint32_t 
   return run;
 }
 
-// read starts in [base, base + 16*64): bits into the wave's LDS bitmap sc[64],
-// advancing the cursor r past them
-__device__ __forceinline__ void scatter_starts(const SArgs &A, uint32_t *sc, int64_t &r,
+// the idx window a wave walks: lane j holds idx[r + j] (0x7FFFFFFF past the
+// end); the load is unconditional (clamped index) so that no branch splits the
+// compiler's view of the loads in flight
+__device__ __forceinline__ int32_t idx_window(const SArgs &A, int64_t r, int lane) {
+  const int64_t j = r + lane;
+  const int32_t v = A.idx[j <= A.num_reads ? j : A.num_reads];
+  return j <= A.num_reads ? v : 0x7FFFFFFF;
+}
+
+// read starts in [base, limit) (limit - base <= 64 * kLaneBytes): bits into
+// the wave's LDS bitmap sc[64], advancing the cursor r past them.  iw is the
+// window at r (loaded ahead by the caller); it comes back as the window at
+// the new r, its load in flight.
+__device__ __forceinline__ void scatter_starts(const SArgs &A, uint32_t *sc, int64_t &r, int32_t &iw,
                                                int32_t base, int32_t limit, int lane) {
-  for (;;) {
-    const int64_t j = r + lane;
-    const int32_t iw = j <= A.num_reads ? A.idx[j] : 0x7FFFFFFF;
-    const bool in = iw < limit;
-    const unsigned long long b = __ballot(in);
-    const uint32_t o = (uint32_t)(iw - base);
-    if (in && o < 16u * 64u) atomicOr(&sc[o >> 4], 1u << (o & 15));   // o < 1024 unless idx is unsorted
-    const int c = __popcll(b);
+  auto put = [&](int32_t x) {
+    const bool in = x < limit;
+    const uint32_t o = (uint32_t)(x - base);
+    if (in && o < 64u * kLaneBytes) atomicOr(&sc[o / kLaneBytes], 1u << (o % kLaneBytes));   // o in range unless idx is unsorted
+    const int c = __popcll(__ballot(in));
     r += c;
-    if (c < 64) break;
+    return c;
+  };
+  if (__builtin_expect(put(iw) == 64, 0)) {   // rare: more than 64 starts in the tile
+    int c;
+    do {
+      c = put(idx_window(A, r, lane));
+    } while (c == 64);
+  }
+  iw = idx_window(A, r, lane);
+}
+
+// a lane's bytes at o (o >= 0) from a buffer descriptor; bytes past the end read 0
+__device__ __forceinline__ void load32(__amdgpu_buffer_rsrc_t rsrc, int32_t o, uint32_t w[kNdw]) {
+#pragma unroll
+  for (int h = 0; h < kNdw / 4; ++h) {
+    const v4u a = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (uint32_t)o + 16u * h, 0, 0);
+    w[4 * h] = a[0]; w[4 * h + 1] = a[1]; w[4 * h + 2] = a[2]; w[4 * h + 3] = a[3];
+  }
+}
+
+// bytes outside [lo, hi) -> 'N' (no move, no word) and quality 0
+__device__ __forceinline__ void mask_range(int32_t o, int32_t lo, int32_t hi, uint32_t sw[kNdw], uint32_t qw[kNdw]) {
+#pragma unroll
+  for (int j = 0; j < kLaneBytes; ++j) {
+    const int32_t p = o + j;
+    if (p >= lo && p < hi) continue;
+    const uint32_t sh = 8 * (j & 3);
+    sw[j >> 2] = (sw[j >> 2] & ~(0xFFu << sh)) | (0x4Eu << sh);
+    qw[j >> 2] &= ~(0xFFu << sh);
   }
 }
 
@@ -235,104 +278,93 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
   constexpr uint32_t M = (uint32_t)(cells - 1) << 3;   // cell byte address mask
   constexpr uint32_t SPARE = (uint32_t)cells << 3;      // the spare cell
   constexpr uint32_t kRun = 48 - K;
-  extern __shared__ __attribute__((aligned(16))) unsigned long long tab[];   // cells + 1, then sc
-  uint32_t *scb = reinterpret_cast<uint32_t *>(tab + cells + 1);
+  __shared__ unsigned long long tab[cells + 1];
+  __shared__ uint32_t scb[kWaves * 2 * 64];   // per wave: two start bitmaps (this tile, next tile)
+  __shared__ uint32_t last;
   for (int i = threadIdx.x; i < cells + 1; i += kWG) tab[i] = 0ull;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  uint32_t *sc = scb + 64 * wid;
+  uint32_t *sc = scb + 128 * wid;
   sc[lane] = 0u;
+  sc[64 + lane] = 0u;
   __syncthreads();
 
-  const int32_t b0 = batch_lo(A), b1 = batch_hi(A);
+  const int32_t b0 = __builtin_amdgcn_readfirstlane(A.idx[0]);
+  const int32_t b1 = __builtin_amdgcn_readfirstlane(A.idx[A.num_reads]);
   const int32_t a0 = b0 & ~15;
   const int64_t ns = nspans(a0, b1);
   const int64_t gw = (int64_t)blockIdx.x * kWaves + wid, nwav = (int64_t)gridDim.x * kWaves;
-  // the range check is per dword: a dword that straddles b1 must still load
-  // (HPGQ_DEVICE_SLACK readable bytes past the data; bytes >= b1 are masked)
-  const __amdgpu_buffer_rsrc_t rs =
-      __builtin_amdgcn_make_buffer_rsrc((void *)A.seq, (short)0, b1 + HPGQ_DEVICE_SLACK, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rq =
-      __builtin_amdgcn_make_buffer_rsrc((void *)A.qual, (short)0, b1 + HPGQ_DEVICE_SLACK, 0x00020000);
   bool risky = false;
 
   for (int64_t s = gw; s < ns; s += nwav) {
-    const int32_t t0 = a0 + (int32_t)(s * kSpan);
+    const int32_t t0 = a0 + (int32_t)(s << kSpanLog);
     const int32_t tend = (int32_t)min((int64_t)t0 + kSpan, (int64_t)b1);
+    // descriptors ending at the span: the prefetch past its last tile reads
+    // zeros without touching memory.  The range check is per dword, so a dword
+    // straddling the end still loads (HPGQ_DEVICE_SLACK readable bytes; bytes
+    // >= tend are masked)
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void *)A.seq, (short)0, tend + HPGQ_DEVICE_SLACK, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rq =
+        __builtin_amdgcn_make_buffer_rsrc((void *)A.qual, (short)0, tend + HPGQ_DEVICE_SLACK, 0x00020000);
     int64_t r = A.span_first[s];
-    // ---- context: the 16 bytes before the span, the same on every lane
-    uint32_t pxy2, pxy3, pq2, pq3, pv, pS;
+    int32_t iw = idx_window(A, r, lane);
+    // ---- context: the kLaneBytes bytes before the span, the same on every lane
+    uint32_t pxy6, pxy7, pq6, pq7, pv, pS;   // the previous lane's last two dwords, V and starts
     // the run open at the tile start per axis: exact when eknown, else at
     // most 15 (the last 16 bytes hold a Z on both axes) and walked back for
     // only when a tile needs the exact scan
     uint32_t einx = 15, einy = 15;
     bool eknown = false;
     {
-      const int32_t c0 = t0 - 16;
-      v4u sv = {0x4E4E4E4Eu, 0x4E4E4E4Eu, 0x4E4E4E4Eu, 0x4E4E4E4Eu};   // 'N': no move, no word
-      v4u qv = {0u, 0u, 0u, 0u};
-      if (c0 >= b0) {
-        sv = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)c0, 0, 0);
-        qv = __builtin_amdgcn_raw_buffer_load_b128(rq, (uint32_t)c0, 0, 0);
-      } else if (t0 > b0) {   // partly before the batch: byte-wise
-        uint32_t w[4] = {0x4E4E4E4Eu, 0x4E4E4E4Eu, 0x4E4E4E4Eu, 0x4E4E4E4Eu}, q[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const int32_t p = c0 + j;
-          if (p < b0) continue;
-          const uint32_t sh = 8 * (j & 3);
-          w[j >> 2] = (w[j >> 2] & ~(0xFFu << sh)) | ((uint32_t)(uint8_t)A.seq[p] << sh);
-          q[j >> 2] |= (uint32_t)(uint8_t)A.qual[p] << sh;
-        }
-        sv = v4u{w[0], w[1], w[2], w[3]};
-        qv = v4u{q[0], q[1], q[2], q[3]};
-      }
-      const uint32_t sa[4] = {sv[0], sv[1], sv[2], sv[3]};
-      const Cls c = classify(sa);
-      pxy2 = c.xy[2];
-      pxy3 = c.xy[3];
-      pq2 = qv[2];
-      pq3 = qv[3];
+      const int32_t c0 = t0 - kLaneBytes;
+      uint32_t sw[kNdw], qw[kNdw];
+      load32(rs, max(c0, 0), sw);
+      load32(rq, max(c0, 0), qw);
+      if (c0 < b0) mask_range(c0, b0, t0, sw, qw);
+      const Cls c = classify(sw);
+      pxy6 = c.xy[kNdw - 2];
+      pxy7 = c.xy[kNdw - 1];
+      pq6 = qw[kNdw - 2];
+      pq7 = qw[kNdw - 1];
       pv = c.v;
-      if (c.bad || ((qv[0] | qv[1] | qv[2] | qv[3]) & 0x80808080u)) risky = true;
-      // read starts in [c0, t0)
-      scatter_starts(A, sc, r, c0, t0, lane);
+      scatter_starts(A, sc, r, iw, c0, t0, lane);
       __builtin_amdgcn_wave_barrier();
       pS = __builtin_amdgcn_readfirstlane(sc[0]);
       __builtin_amdgcn_wave_barrier();
       sc[0] = 0u;
-      if (!(c.zany & 0x01010101u) || !(c.zany & 0x02020202u)) {
+      if (!(c.zhi & 0x01010101u) || !(c.zhi & 0x02020202u)) {
         einx = run_before<0>(A, b0, t0, kRun);
         einy = run_before<1>(A, b0, t0, kRun);
         eknown = true;
       }
     }
-    // ---- tiles
-    for (int32_t t = t0; t < tend; t += kTile) {
-      const int32_t o = t + 16 * lane;
-      v4u sv = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)o, 0, 0);
-      v4u qv = __builtin_amdgcn_raw_buffer_load_b128(rq, (uint32_t)o, 0, 0);
-      scatter_starts(A, sc, r, t, t + kTile, lane);
-      uint32_t sw[4] = {sv[0], sv[1], sv[2], sv[3]};
-      uint32_t qw[4] = {qv[0], qv[1], qv[2], qv[3]};
-      if (t < b0 || t + kTile > tend) {   // edge tile: bytes outside [b0, b1) -> 'N', quality 0
+    // ---- tiles, unrolled by two with A/B registers: the next tile's bytes
+    // and read-start bits are fetched while this one is counted (the bitmap
+    // read then waits behind this tile's table adds, not in front of them),
+    // the idx window one scatter ahead
+    auto tile = [&](const int32_t t, uint32_t (&sw)[kNdw], uint32_t (&qw)[kNdw], const uint32_t so) {
+      const int32_t o = t + kLaneBytes * lane;
+#if HPGQ_CGR_ABL == 4   // timing probe only: loads and start bitmaps, no counting
+      {
+        uint32_t x = so;
 #pragma unroll
-        for (int j = 0; j < 16; ++j) {
-          const int32_t p = o + j;
-          if (p >= b0 && p < b1 && p < tend) continue;
-          const uint32_t sh = 8 * (j & 3);
-          sw[j >> 2] = (sw[j >> 2] & ~(0xFFu << sh)) | (0x4Eu << sh);
-          qw[j >> 2] &= ~(0xFFu << sh);
-        }
+        for (int d = 0; d < kNdw; ++d) x ^= sw[d] ^ qw[d];
+        if (__builtin_expect(x == 0x12345678u, 0)) risky = true;
+        return;
       }
+#endif
+      if (t < b0 || t + kTile > tend) mask_range(o, b0, tend, sw, qw);   // edge tiles
       const Cls c = classify(sw);
-      __builtin_amdgcn_wave_barrier();
-      const uint32_t so = sc[lane];
-      __builtin_amdgcn_wave_barrier();
-      sc[lane] = 0u;
+      uint32_t qor = 0;
+#pragma unroll
+      for (int d = 0; d < kNdw; ++d) qor |= qw[d];
       // flags: unsupported bytes
-      if (__ballot(c.bad != 0u || ((qw[0] | qw[1] | qw[2] | qw[3]) & 0x80808080u) != 0u)) risky = true;
-      // runs: a lane without a Z on an axis, or a long run entering the tile
-      const bool zfree = !(c.zany & 0x01010101u) || !(c.zany & 0x02020202u);
+      if (__ballot(c.bad != 0u || (qor & 0x80808080u) != 0u)) risky = true;
+      // runs: a 16-byte chunk without a Z on an axis, or a long run entering the tile
+      const uint32_t zand = c.zlo & c.zhi;
+      const bool zfree = !(zand & 0x01010101u) || !(zand & 0x02020202u) ||
+                         !(c.zlo & 0x01010101u) || !(c.zlo & 0x02020202u) ||
+                         !(c.zhi & 0x01010101u) || !(c.zhi & 0x02020202u);
       if (__builtin_expect(__ballot(zfree) != 0ull || einx > 16 || einy > 16, 0)) {
         if (!eknown) {
           einx = run_before<0>(A, b0, t, kRun);
@@ -346,15 +378,16 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
         eknown = false;
       }
       // neighbours (lane 0: the previous tile's last lane / the span context)
-      const uint32_t nxy2 = dpp_shr1(pxy2, c.xy[2]), nxy3 = dpp_shr1(pxy3, c.xy[3]);
-      const uint32_t nq2 = dpp_shr1(pq2, qw[2]), nq3 = dpp_shr1(pq3, qw[3]);
+      const uint32_t nxy6 = dpp_shr1(pxy6, c.xy[kNdw - 2]), nxy7 = dpp_shr1(pxy7, c.xy[kNdw - 1]);
+      const uint32_t nq6 = dpp_shr1(pq6, qw[kNdw - 2]), nq7 = dpp_shr1(pq7, qw[kNdw - 1]);
       const uint32_t nv = dpp_shr1(pv, c.v), nS = dpp_shr1(pS, so);
       // emission: bytes [i-K+1, i] all A/C/G/T and no read start in (i-K+1, i]
-      const uint32_t V32 = nv | (c.v << 16), S32 = nS | (so << 16);
       uint32_t E;
       {
-        const uint32_t W = V32 & ~S32;
-        uint32_t R = W;
+        // 64-bit frame: the previous lane's bytes just below bit 32, this lane's from bit 32
+        const uint64_t V = ((uint64_t)c.v << 32) | ((uint64_t)nv << (32 - kLaneBytes));
+        const uint64_t W = V & ~(((uint64_t)so << 32) | ((uint64_t)nS << (32 - kLaneBytes)));
+        uint64_t R = W;
         int have = 1;
 #pragma unroll
         for (int step = 0; step < 4; ++step) {
@@ -364,41 +397,71 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
             have += sh;
           }
         }
-        E = (K == 1 ? V32 : R & (V32 << (K - 1))) >> 16;
+        E = (uint32_t)((K == 1 ? V : R & (V << (K - 1))) >> 32);
       }
-      // the code window and the quality sum at byte 15 of the previous lane
+      // the code window and the quality sum at the previous lane's last byte
       uint32_t w = 0, acc = 0;
 #pragma unroll
-      for (int j = 16 - (K - 1); j < 16; ++j) {
-        const uint32_t xw = j < 12 ? nxy2 : nxy3;
-        w = (w << 2) | __builtin_amdgcn_ubfe(xw, 8 * (j & 3), 5);
-      }
+      for (int j = kLaneBytes - (K - 1); j < kLaneBytes; ++j)
+        w = ((w << 2) | __builtin_amdgcn_perm(0u, j < kLaneBytes - 4 ? nxy6 : nxy7, 0x0C0C0C00u | (j & 3))) & M;
 #pragma unroll
-      for (int j = 16 - K; j < 16; ++j) {
-        const uint32_t qx = j < 12 ? nq2 : nq3;
-        acc += __builtin_amdgcn_ubfe(qx, 8 * (j & 3), 8);
-      }
+      for (int j = kLaneBytes - K; j < kLaneBytes; ++j)
+        acc += __builtin_amdgcn_ubfe(j < kLaneBytes - 4 ? nq6 : nq7, 8 * (j & 3), 8);
       // one ds_add_u64 per byte: count | quality sum << 32 (spare cell: no word)
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
-        w = (w << 2) | __builtin_amdgcn_ubfe(c.xy[j >> 2], 8 * (j & 3), 5);
+      for (int j = 0; j < kLaneBytes; ++j) {
+        w = ((w << 2) | __builtin_amdgcn_perm(0u, c.xy[j >> 2], 0x0C0C0C00u | (j & 3))) & M;
         const int jo = j - K;   // the byte leaving the quality window
         const uint32_t qold = jo >= 0 ? __builtin_amdgcn_ubfe(qw[jo >> 2], 8 * (jo & 3), 8)
-                                      : __builtin_amdgcn_ubfe(jo + 16 < 12 ? nq2 : nq3, 8 * ((jo + 16) & 3), 8);
+                                      : __builtin_amdgcn_ubfe(jo + kLaneBytes < kLaneBytes - 4 ? nq6 : nq7, 8 * (jo & 3), 8);
         acc = acc + __builtin_amdgcn_ubfe(qw[j >> 2], 8 * (j & 3), 8) - qold;
-        const uint32_t e = (uint32_t)__builtin_amdgcn_sbfe((int)E, j, 1);
-        const uint32_t addr = (e & w & M) | (~e & SPARE);
+        // addr = E bit j ? w : SPARE (v_bfe_i32 + v_bfi_b32; left to itself the
+        // compiler spends three instructions on it)
+        uint32_t e, addr;
+        asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(e) : "v"(E), "i"(j));
+        asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(addr) : "v"(e), "v"(w), "s"(SPARE));
         const unsigned long long inc = ((unsigned long long)acc << 32) | 1ull;
+#if HPGQ_CGR_ABL == 3   // timing probe only: no table adds
+        if (__builtin_expect(addr == 0xFFFFFFFFu, 0))
+#endif
         atomicAdd(reinterpret_cast<unsigned long long *>(reinterpret_cast<char *>(tab) + addr), inc);
       }
       // carry the last lane to the next tile's lane 0
-      pxy2 = __builtin_amdgcn_readlane(c.xy[2], 63);
-      pxy3 = __builtin_amdgcn_readlane(c.xy[3], 63);
-      pq2 = __builtin_amdgcn_readlane(qw[2], 63);
-      pq3 = __builtin_amdgcn_readlane(qw[3], 63);
+      pxy6 = __builtin_amdgcn_readlane(c.xy[kNdw - 2], 63);
+      pxy7 = __builtin_amdgcn_readlane(c.xy[kNdw - 1], 63);
+      pq6 = __builtin_amdgcn_readlane(qw[kNdw - 2], 63);
+      pq7 = __builtin_amdgcn_readlane(qw[kNdw - 1], 63);
       pv = __builtin_amdgcn_readlane(c.v, 63);
       pS = __builtin_amdgcn_readlane(so, 63);
+    };
+    uint32_t sA[kNdw], qA[kNdw], sB[kNdw], qB[kNdw];
+    load32(rs, t0 + kLaneBytes * lane, sA);
+    load32(rq, t0 + kLaneBytes * lane, qA);
+    scatter_starts(A, sc, r, iw, t0, t0 + kTile, lane);
+    uint32_t soA = sc[lane], soB;
+    // straight-line halves (no branch around a load: the compiler then counts
+    // the loads in flight exactly and the tile waits only for its own bytes);
+    // past the span the loads read zeros and the bitmaps are cleared below
+    for (int32_t t = t0;; t += 2 * kTile) {
+      const int32_t tb = t + kTile;
+      scatter_starts(A, sc + 64, r, iw, tb, tb + kTile, lane);
+      soB = sc[64 + lane];
+      load32(rs, tb + kLaneBytes * lane, sB);
+      load32(rq, tb + kLaneBytes * lane, qB);
+      sc[lane] = 0u;
+      tile(t, sA, qA, soA);
+      if (tb >= tend) break;
+      const int32_t ta = tb + kTile;
+      scatter_starts(A, sc, r, iw, ta, ta + kTile, lane);
+      soA = sc[lane];
+      load32(rs, ta + kLaneBytes * lane, sA);
+      load32(rq, ta + kLaneBytes * lane, qA);
+      sc[64 + lane] = 0u;
+      tile(tb, sB, qB, soB);
+      if (ta >= tend) break;
     }
+    sc[lane] = 0u;
+    sc[64 + lane] = 0u;
   }
   if (__ballot(risky) && lane == 0) atomicOr(A.gate, GATE_EXACT);
   __syncthreads();
@@ -406,37 +469,47 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
     const unsigned long long v = tab[i];
     if (v) atomicAdd(&A.scratch[i], v);
   }
-}
-
-// scratch (code order) -> the reference's tables [co_x][co_y], or just clear
-// it when the gate sends the batch to the exact path
-template <int K>
-__global__ void __launch_bounds__(256) cgr_stream_finalize_kernel(SArgs A) {
-  constexpr int cells = 1 << (2 * K);
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  const bool exact = (*A.gate & GATE_EXACT) != 0u;
+  // the last workgroup moves the scratch table into the reference layout
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(A.done, 1u) == gridDim.x - 1 ? 1u : 0u;
+  __syncthreads();
+  if (!last) return;
+  // acquire: this CU's L1 is invalidated, the loads below see the other
+  // workgroups' adds (performed at L2) and independent loads stay pipelined
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  const bool exact = (__hip_atomic_load(A.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & GATE_EXACT) != 0u;
   unsigned long long cnt = 0;
-  if (i < cells) {
-    const unsigned long long v = A.scratch[i];
-    A.scratch[i] = 0ull;
-    if (!exact && v) {
-      // code bits 2a / 2a+1 = x / y of the base `a` steps back; the newest is
-      // the MSB of co_x / co_y
-      uint32_t cx = 0, cy = 0;
+  constexpr int kPer = (cells + kWG - 1) / kWG;
+  unsigned long long vals[kPer];
 #pragma unroll
-      for (int a = 0; a < K; ++a) {
-        cx |= ((uint32_t)(i >> (2 * a)) & 1u) << (K - 1 - a);
-        cy |= ((uint32_t)(i >> (2 * a + 1)) & 1u) << (K - 1 - a);
-      }
-      const uint32_t c = (uint32_t)v, q = (uint32_t)(v >> 32);
-      const uint32_t cell = (cx << K) | cy;
-      A.ts[cell] += c;
-      A.tq[cell] += q - c * A.base_quality * (uint32_t)K;
-      cnt = c;
+  for (int u = 0; u < kPer; ++u) {
+    const int i = threadIdx.x + u * kWG;
+    vals[u] = i < cells ? A.scratch[i] : 0ull;
+  }
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int i = threadIdx.x + u * kWG;
+    const unsigned long long v = vals[u];
+    if (!v) continue;
+    A.scratch[i] = 0ull;
+    if (exact) continue;
+    // code bits 2a / 2a+1 = x / y of the base `a` steps back; the newest is
+    // the MSB of co_x / co_y
+    uint32_t cx = 0, cy = 0;
+#pragma unroll
+    for (int a = 0; a < K; ++a) {
+      cx |= ((uint32_t)(i >> (2 * a)) & 1u) << (K - 1 - a);
+      cy |= ((uint32_t)(i >> (2 * a + 1)) & 1u) << (K - 1 - a);
     }
+    const uint32_t cn = (uint32_t)v, q = (uint32_t)(v >> 32);
+    const uint32_t cell = (cx << K) | cy;
+    A.ts[cell] += cn;
+    A.tq[cell] += q - cn * A.base_quality * (uint32_t)K;
+    cnt += cn;
   }
   for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
-  if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(A.words, cnt);
+  if (lane == 0 && cnt) atomicAdd(A.words, cnt);
 }
 
 }  // namespace stream

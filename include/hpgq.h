@@ -292,7 +292,11 @@ int64_t hpgq_cgr_last_replays(hpgq_cgr_t *cg);
 #define HPGQ_CGR_PATH_AUTO  0
 #define HPGQ_CGR_PATH_EXACT 1
 int  hpgq_cgr_set_path(hpgq_cgr_t *cg, int path);
-/* 1 if the last (synced) fill ran the exact simulation, 0 if the stream pass sufficed */
+/* 1 if a fill since the previous sync ran the exact simulation, 0 if the
+ * stream pass sufficed for all of them (read after hpgq_cgr_sync).  A
+ * streamed fill whose gate is set is simulated exactly inside the next
+ * hpgq_cgr_sync / hpgq_cgr_read / hpgq_cgr_reset, so its batch must stay
+ * valid until then (as for any asynchronous fill). */
 int  hpgq_cgr_last_exact(hpgq_cgr_t *cg);
 
 /* ---------------------------------------------------------------------- */
