@@ -199,7 +199,7 @@ def main():
 
     if cgr:
         eng = H.ChaosGame(7, 33, device=local)
-        kernel_name = "hpgq::cgr::cgr_fill_kernel<7> (+check, fix)"
+        kernel_name = "hpgq::cgr::stream::cgr_stream_kernel<7> (+span_first)"
         # algorithmic bytes per read: seq + quality + offset (tables stay in LDS)
         alg = [nb for (_n, _m, nb) in batches]
         red = torch.zeros(2 * 128 * 128 + 1, dtype=torch.int64, device=dev) if world > 1 else None

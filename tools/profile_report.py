@@ -27,7 +27,7 @@ OUT = os.path.join(ROOT, "profiles")
 KERNELS = {"c2": ("engine_tri_kernel", "engine_kernel", "trim_kernel"),
            "c3": ("engine_tri_kernel", "engine_kernel", "trim_kernel"),
            "c4": ("engine_tri_kernel", "engine_kernel", "trim_kernel"),
-           "c5": ("cgr_fill_kernel", "cgr_check_kernel", "cgr_fix_kernel")}
+           "c5": ("cgr_stream_kernel", "span_first_kernel")}
 
 
 def counters(sub, kerns):
