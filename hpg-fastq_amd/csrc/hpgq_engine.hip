@@ -26,7 +26,8 @@ struct hpgq_ctx {
   const void *kfn = nullptr;
   int nch = 1;
   bool gen = false;               // generic (edit / N / OOR / left-right) kernel variant
-  bool tri = false;               // three-reads-per-wave FAST kernel (lmax <= 160)
+  bool tri = false;               // segmented FAST kernel (lmax <= 160)
+  bool hex = false;               // ... in its 16-byte-lane geometry (lmax <= 156)
   bool tri_edit = false;          // ... trimming in its block prologue (single-end edit)
   int grid = 0;
   uint64_t *d_slab = nullptr;     // [grid][nm * clen] per-workgroup partials
@@ -124,30 +125,42 @@ static const void *kernel_nch(int nch) {
   }
 }
 
-static const void *kernel_for(int nm, int nch, bool gen, bool tri, bool edit, char *name, size_t cap) {
-  if (tri && edit) {   // single-end edit: trims in the block prologue + windows
-    const char *w = std::getenv("HPGQ_TRI_WAVES");
-    const int mw = w && std::atoi(w) == 4 ? 4 : 5;
-    std::snprintf(name, cap, "hpgq::engine_tri_kernel<%d, false, 1, true>", mw);
-    return mw == 4 ? (const void *)hpgq::engine_tri_kernel<4, false, 1, true>
-                   : (const void *)hpgq::engine_tri_kernel<5, false, 1, true>;
+template <int NW>
+static const void *tri_for(int mw, bool un, int nm, bool edit) {
+  using hpgq::engine_tri_kernel;
+  if (edit) return mw <= 4 ? (const void *)engine_tri_kernel<4, false, 1, true, NW>
+                           : (const void *)engine_tri_kernel<5, false, 1, true, NW>;
+  if constexpr (NW == 2) {
+    if (nm == 2) {   // paired-end (tri geometry: two mates' accumulators do not fit hex's registers)
+      if (mw <= 4) return (const void *)engine_tri_kernel<4, false, 2, false, 2>;
+      if (mw == 5) return (const void *)engine_tri_kernel<5, false, 2, false, 2>;
+      return (const void *)engine_tri_kernel<6, false, 2, false, 2>;
+    }
+    if (un) {
+      if (mw <= 4) return (const void *)engine_tri_kernel<4, true, 1, false, 2>;
+      if (mw == 5) return (const void *)engine_tri_kernel<5, true, 1, false, 2>;
+      return (const void *)engine_tri_kernel<6, true, 1, false, 2>;
+    }
   }
+  if (mw <= 4) return (const void *)engine_tri_kernel<4, false, 1, false, NW>;
+  if (mw == 5) return (const void *)engine_tri_kernel<5, false, 1, false, NW>;
+  return (const void *)engine_tri_kernel<6, false, 1, false, NW>;
+}
+
+// tri: the segmented kernel (hpgq_engine_tri.h), hex selects its 16-byte-lane geometry
+static const void *kernel_for(int nm, int nch, bool gen, bool tri, bool hex, bool edit, char *name, size_t cap) {
   if (tri) {
     const char *w = std::getenv("HPGQ_TRI_WAVES");      // occupancy experiment knob
-    const char *u = std::getenv("HPGQ_TRI_UNALIGNED");  // load-scheme experiment knob
-    int mw = w ? std::atoi(w) : (nm == 2 ? 4 : 5);   // spill-free occupancy per variant
+    const char *u = std::getenv("HPGQ_TRI_UNALIGNED");  // load-scheme experiment knob (tri only)
+    const int nw = hex ? 4 : 2;
+    int mw = w ? std::atoi(w) : (hex ? 4 : (nm == 2 ? 4 : 5));   // spill-free occupancy per variant
     mw = mw <= 4 ? 4 : (mw == 5 ? 5 : 6);
-    const bool un = u && std::atoi(u) != 0;
-    if (nm == 2) {   // paired-end: aligned loads only
-      std::snprintf(name, cap, "hpgq::engine_tri_kernel<%d, false, 2, false>", mw);
-      if (mw <= 4) return (const void *)hpgq::engine_tri_kernel<4, false, 2, false>;
-      if (mw == 5) return (const void *)hpgq::engine_tri_kernel<5, false, 2, false>;
-      return (const void *)hpgq::engine_tri_kernel<6, false, 2, false>;
-    }
-    std::snprintf(name, cap, "hpgq::engine_tri_kernel<%d, %s, 1, false>", mw, un ? "true" : "false");
-    if (mw <= 4) return un ? (const void *)hpgq::engine_tri_kernel<4, true, 1, false> : (const void *)hpgq::engine_tri_kernel<4, false, 1, false>;
-    if (mw == 5) return un ? (const void *)hpgq::engine_tri_kernel<5, true, 1, false> : (const void *)hpgq::engine_tri_kernel<5, false, 1, false>;
-    return un ? (const void *)hpgq::engine_tri_kernel<6, true, 1, false> : (const void *)hpgq::engine_tri_kernel<6, false, 1, false>;
+    if (hex) mw = 4;   // 116-123 VGPRs
+    if (edit && mw > 5) mw = 5;
+    const bool un = !hex && !edit && nm == 1 && u && std::atoi(u) != 0;
+    std::snprintf(name, cap, "hpgq::engine_tri_kernel<%d, %s, %d, %s, %d>", mw, un ? "true" : "false", edit ? 1 : nm,
+                  edit ? "true" : "false", nw);
+    return hex ? tri_for<4>(mw, un, nm, edit) : tri_for<2>(mw, un, nm, edit);
   }
   std::snprintf(name, cap, "hpgq::engine_kernel<%d, %d, %s>", nm, nch == 1 ? 1 : (nch == 2 ? 2 : 5),
                 gen ? "true" : "false");
@@ -273,6 +286,8 @@ int hpgq_open(hpgq_ctx_t **out, int device, const hpgq_params_t *p) {
     c->tri = !filter_extras && (!edit || c->nm == 1) && p->lmax <= hpgq::kTriPos &&
              !(force && std::strcmp(force, "single") == 0);
     c->tri_edit = c->tri && edit;
+    const char *geo = std::getenv("HPGQ_TRI_GEO");   // "tri" forces the 8-byte-lane geometry
+    c->hex = c->tri && c->nm == 1 && p->lmax <= hpgq::kHexPos && !(geo && std::strcmp(geo, "tri") == 0);
   }
   {
     const int hlen = p->lmax + 1 + HPGQ_MEANQ_BINS + HPGQ_GC_BINS;
@@ -294,7 +309,7 @@ int hpgq_open(hpgq_ctx_t **out, int device, const hpgq_params_t *p) {
   HPGQ_HIP_TRY(hipMemsetAsync(c->d_err, 0, sizeof(int32_t), c->stream));
   int cus = 0;
   HPGQ_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-  const void *kfn = kernel_for(c->nm, c->nch, c->gen, c->tri, c->tri_edit, c->kname, sizeof(c->kname));
+  const void *kfn = kernel_for(c->nm, c->nch, c->gen, c->tri, c->hex, c->tri_edit, c->kname, sizeof(c->kname));
   c->kfn = kfn;
   if (c->lds_bytes > 64 * 1024)
     HPGQ_HIP_TRY(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -337,7 +352,7 @@ static int launch(hpgq_ctx *c, hpgq::EngineArgs &A) {
   if (A.num_reads <= 0) return HPGQ_OK;
   A.slab = c->d_slab;
   A.err = c->d_err;
-  const int64_t per_block = c->tri ? hpgq::kTriBlock : 64;
+  const int64_t per_block = c->tri ? (c->hex ? hpgq::kHexBlock : hpgq::kTriBlock) : 64;
   const int64_t nblocks = (A.num_reads + per_block - 1) / per_block;
   const int64_t need = (nblocks + hpgq::kWaves - 1) / hpgq::kWaves;
   const int grid = (int)std::min<int64_t>(need, c->grid);

@@ -39,11 +39,38 @@
 
 namespace hpgq {
 
-constexpr int kTriW = 21;       // lanes per segment
-constexpr int kTriPos = 160;    // positions per segment (20 owning lanes x 8)
-constexpr int kTriBlock = 54;   // reads per block (18 triples)
-constexpr int kTriU = 3;        // triples per pipeline group (6 groups per full block)
+constexpr int kTriPos = 160;    // positions per segment (tri: 20 owning lanes x 8)
+constexpr int kHexPos = 156;    // hex: 10 lanes x 16, the last lane's realignment stops at 156
 constexpr int kTriSlack = 8;    // readable bytes past the data end the loads may touch
+
+// Segment geometry by dwords per lane (NW):
+//   NW = 2 ("tri"): 3 segments of 21 lanes, 20 owning 8 positions (8-byte loads);
+//                   lane 20 loads the continuation its neighbour's realignment needs
+//   NW = 4 ("hex"): 6 segments of 10 lanes, each owning 16 positions (16-byte loads:
+//                   1 KB per wave-load, ~10 % more streaming rate than the tri shape,
+//                   tools/ubench/stream_rates.hip); lanes 60-63 idle; reads <= 156
+// kBlock reads (<= 64: lane j <-> read j in the epilogue) in steps of kSegs reads,
+// kU steps per pipeline group, an even number of groups per block.
+template <int NW>
+struct Geo;
+template <>
+struct Geo<2> {
+  static constexpr int kSegs = 3, kSegW = 21, kOwn = 20, kBlock = 54, kU = 3, kPos = kTriPos;
+};
+template <>
+struct Geo<4> {
+  static constexpr int kSegs = 6, kSegW = 10, kOwn = 10, kBlock = 48, kU = 2, kPos = kHexPos;
+};
+constexpr int kTriBlock = Geo<2>::kBlock;
+constexpr int kHexBlock = Geo<4>::kBlock;
+
+template <int NW>
+constexpr uint64_t not_seg_first_mask() {   // lanes j with j % kSegs != 0
+  uint64_t m = 0;
+  for (int j = 0; j < 64; ++j)
+    if (j % Geo<NW>::kSegs) m |= 1ull << j;
+  return m;
+}
 constexpr int kNibbleEvery = 15;   // 4-bit counters
 constexpr int kByteEvery = 255;    // 8-bit counters
 
@@ -58,9 +85,10 @@ constexpr uint32_t kATHi = 0x00000010u;   // T -> 0x10
 typedef unsigned v2u __attribute__((ext_vector_type(2)));
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
+template <int NW>
 struct TriPending {
-  v2u s, q;        // the lane's 8 bytes of seq / quality (raw dwords if aligned loads)
-  uint32_t n;      // its read's length (| als << 16 | alq << 20 if aligned loads)
+  uint32_t s[NW], q[NW];   // the lane's 4*NW bytes of seq / quality (raw dwords if aligned loads)
+  uint32_t n;              // its read's length (| als << 16 | alq << 20 if aligned loads)
 };
 
 __device__ __forceinline__ uint32_t next_lane0(uint32_t v) {   // lane i <- lane i+1, lane 63 <- 0
@@ -78,12 +106,13 @@ __device__ __forceinline__ uint32_t wave_scan(uint32_t v) {
   return v;
 }
 
-// masks of the lane's two words: bytes at positions < n (nv = n - p0)
-__device__ __forceinline__ void tri_masks(int nv, uint32_t &m0, uint32_t &m1) {
-  const int e = 32 - 8 * nv;   // right shift of 0x00000000FFFFFFFF giving m0
+// masks of the lane's NW words: bytes at positions < n (nv = n - p0)
+template <int NW>
+__device__ __forceinline__ void tri_masks(int nv, uint32_t (&m)[NW]) {
+  const int e = 32 - 8 * nv;   // right shift of 0x00000000FFFFFFFF giving m[0]
   const uint64_t ones = 0xFFFFFFFFull;
-  m0 = (uint32_t)(ones >> min(max(e, 0), 32));
-  m1 = (uint32_t)(ones >> min(max(e + 32, 0), 32));
+#pragma unroll
+  for (int w = 0; w < NW; ++w) m[w] = (uint32_t)(ones >> min(max(e + 32 * w, 0), 32));
 }
 
 // 0xFF in every byte of d that is non-zero
@@ -92,13 +121,14 @@ __device__ __forceinline__ uint32_t nonzero_bytes(uint32_t d) {
   return (nz >> 7) * 0xFFu;
 }
 
+template <int NW>
 struct TriAcc {
-  uint32_t n4[2][2];   // [word][C|G<<4, A|T<<4]: nibble per position
-  uint32_t c8[2][4];   // [word][A, C, G, T]: byte per position
-  uint32_t q02[2], q13[2];   // quality 16-bit pairs (positions 0,2 / 1,3 of the word)
+  uint32_t n4[NW][2];   // [word][C|G<<4, A|T<<4]: nibble per position
+  uint32_t c8[NW][4];   // [word][A, C, G, T]: byte per position
+  uint32_t q02[NW], q13[NW];   // quality 16-bit pairs (positions 0,2 / 1,3 of the word)
   __device__ __forceinline__ void zero() {
 #pragma unroll
-    for (int w = 0; w < 2; ++w) {
+    for (int w = 0; w < NW; ++w) {
       n4[w][0] = n4[w][1] = 0;
       c8[w][0] = c8[w][1] = c8[w][2] = c8[w][3] = 0;
       q02[w] = q13[w] = 0;
@@ -107,7 +137,7 @@ struct TriAcc {
   // nibbles -> bytes (every <= 15 triples and before any subtraction)
   __device__ __forceinline__ void widen() {
 #pragma unroll
-    for (int w = 0; w < 2; ++w) {
+    for (int w = 0; w < NW; ++w) {
       c8[w][1] += n4[w][0] & 0x0F0F0F0Fu;
       c8[w][2] += (n4[w][0] >> 4) & 0x0F0F0F0Fu;
       c8[w][0] += n4[w][1] & 0x0F0F0F0Fu;
@@ -121,7 +151,7 @@ struct TriAcc {
     // loop's registers (hipcc would hoist them as loop invariants and spill)
     asm volatile("" : "+v"(p0), "+s"(lmax), "+s"(pos_acc));
 #pragma unroll
-    for (int w = 0; w < 2; ++w) {
+    for (int w = 0; w < NW; ++w) {
       const uint32_t qv[4] = {q02[w] & 0xFFFFu, q13[w] & 0xFFFFu, q02[w] >> 16, q13[w] >> 16};
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -278,20 +308,23 @@ struct MateTag {
 // EDIT (NM = 1): the block prologue trims each read (trim_word, written to
 // A.trim when the caller wants it) and describes it by its window [ts, n - te)
 // (offset + ts, length n - ts - te): stats and filter see the trimmed read.
-template <int MINW, bool UNAL, int NM, bool EDIT>
+template <int MINW, bool UNAL, int NM, bool EDIT, int NW>
 __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
   static_assert(!EDIT || NM == 1, "edit on the three-read kernel is single-end");
+  static_assert(!UNAL || NW == 2, "unaligned loads: tri only");
+  using G = Geo<NW>;
+  constexpr int kSegs = G::kSegs, kSegW = G::kSegW, kBlock = G::kBlock, kU = G::kU;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = uni(tid >> 6);
   const int lmax = A.lmax;
   const int hlen = lmax + 1 + HPGQ_MEANQ_BINS + HPGQ_GC_BINS;
-  const int seg = lane / kTriW;                 // 0..2, lane 63 -> 3 (idle)
-  const int ls = lane - seg * kTriW;            // 0..20
-  const bool owner = seg < 3 && ls < 20;
-  const int p0 = owner ? 8 * ls : (1 << 26);   // first position of this lane (8*p0 fits int32)
-  const uint32_t lane8 = 8u * (uint32_t)ls;
+  const int seg = min(lane / kSegW, kSegs);     // kSegs: idle lanes (tri: 63; hex: 60-63)
+  const int ls = lane - seg * kSegW;
+  const bool owner = seg < kSegs && ls < G::kOwn;
+  const int p0 = owner ? 4 * NW * ls : (1 << 26);   // first position of this lane (8*p0 fits int32)
+  const uint32_t lane8 = 4u * NW * (uint32_t)ls;   // byte offset of this lane's window
   const bool stats = A.flags & F_STATS, filter = A.flags & F_FILTER;
   // raw-sum bounds: pass iff min_len <= n <= max_len and lo_r*n <= S <= hi_r*n
   const int lo_r = A.min_q + A.phred, hi_r = A.max_q + A.phred;
@@ -331,7 +364,7 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
     rq[m] = __builtin_amdgcn_make_buffer_rsrc((void *)(pq - bq[m]), (short)0,
                                               bq[m] + data_end + kTriSlack, 0x00020000);
   }
-  TriAcc acc[NM];
+  TriAcc<NW> acc[NM];
 #pragma unroll
   for (int m = 0; m < NM; ++m) acc[m].zero();
   int since_flush = 0;   // triples per mate added since the last LDS flush (a byte grows <= 1 per triple)
@@ -343,7 +376,7 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
     for (int k = 0; k < 7; ++k) cnt[m][k] = 0;
   }
 
-  const int64_t nblocks = (A.num_reads + kTriBlock - 1) / kTriBlock;
+  const int64_t nblocks = (A.num_reads + kBlock - 1) / kBlock;
   const int64_t gw = (int64_t)blockIdx.x * kWaves + wave;
   const int64_t nw = (int64_t)gridDim.x * kWaves;
 
@@ -351,8 +384,8 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
   // lanes >= nr get length 0, so whatever gathers them contributes nothing.
   // Returns this lane's lengths (the epilogue needs them).
   auto load_block = [&](int64_t blk, int tb, uint32_t (&len)[NM], uint32_t &tw, uint32_t &nraw) {
-    const int64_t r0 = blk * kTriBlock;
-    const int nr = (int)min((int64_t)kTriBlock, A.num_reads - r0);
+    const int64_t r0 = blk * kBlock;
+    const int nr = (int)min((int64_t)kBlock, A.num_reads - r0);
     const int l = min(lane, nr - 1);
 #pragma unroll
     for (int m = 0; m < NM; ++m) {
@@ -376,82 +409,99 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
     __builtin_amdgcn_wave_barrier();   // other lanes read them (LDS is in order per wave)
   };
   // lane -> its segment's read (entry `src` of mate m's read table tb)
-  auto gather = [&](int m, int tb, int src, TriPending &pd) {
+  auto gather = [&](int m, int tb, int src, TriPending<NW> &pd) {
     const v4u rec = *reinterpret_cast<const v4u *>(tab(m, tb) + 4 * src);
     pd.n = rec.z;
-    pd.s = __builtin_amdgcn_raw_buffer_load_b64(rs[m], rec.x + lane8, 0, 0);
-    pd.q = __builtin_amdgcn_raw_buffer_load_b64(rq[m], rec.y + lane8, 0, 0);
+    if (NW == 2) {
+      const v2u a = __builtin_amdgcn_raw_buffer_load_b64(rs[m], rec.x + lane8, 0, 0);
+      const v2u b = __builtin_amdgcn_raw_buffer_load_b64(rq[m], rec.y + lane8, 0, 0);
+      pd.s[0] = a.x; pd.s[1] = a.y; pd.q[0] = b.x; pd.q[1] = b.y;
+    } else {
+      const v4u a = __builtin_amdgcn_raw_buffer_load_b128(rs[m], rec.x + lane8, 0, 0);
+      const v4u b = __builtin_amdgcn_raw_buffer_load_b128(rq[m], rec.y + lane8, 0, 0);
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        pd.s[w] = a[w & 3];
+        pd.q[w] = b[w & 3];
+      }
+    }
   };
 
-  TriPending grp[2][kTriU];
-  // issue group g (kTriU triples) of mate m; triples past the block end
-  // gather lane 63 (length 0), so they add nothing
+  TriPending<NW> grp[2][kU];
+  // issue group g (kU steps) of mate m; steps past the block end gather
+  // lane 63 (length 0), so they add nothing
   auto load_group = [&](int m, int tb, int nt, int g, int slot) {
 #pragma unroll
-    for (int u = 0; u < kTriU; ++u) {
-      const int t = g * kTriU + u;
-      gather(m, tb, t < nt ? min(3 * t + seg, 63) : 63, grp[slot][u]);
+    for (int u = 0; u < kU; ++u) {
+      const int t = g * kU + u;
+      gather(m, tb, t < nt ? min(kSegs * t + seg, 63) : 63, grp[slot][u]);
     }
   };
 
   // one triple: per-lane partial (raw quality | G+C << 18); adds (SUB = false)
   // or removes (SUB = true) the lane's positions from mate m's counters
-  auto account = [&](auto mtag, const TriPending &pd, bool count, auto sub_tag) -> uint32_t {
+  auto account = [&](auto mtag, const TriPending<NW> &pd, bool count, auto sub_tag) -> uint32_t {
     constexpr int m = decltype(mtag)::value;
     constexpr bool SUB = decltype(sub_tag)::value;
-    uint32_t s0 = pd.s.x, s1 = pd.s.y, q0 = pd.q.x, q1 = pd.q.y;
-    if (!UNAL) {
+    uint32_t sw[NW], qw[NW];
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      sw[w] = pd.s[w];
+      qw[w] = pd.q[w];
+    }
+    if (!UNAL) {   // realign: word w = bytes [al, al+4) of raw words w, w+1 (the last from lane+1)
       const uint32_t als = (pd.n >> 16) & 3u, alq = (pd.n >> 20) & 3u;
-      s0 = __builtin_amdgcn_alignbyte(pd.s.y, pd.s.x, als);
-      s1 = __builtin_amdgcn_alignbyte(next_lane0(pd.s.x), pd.s.y, als);
-      q0 = __builtin_amdgcn_alignbyte(pd.q.y, pd.q.x, alq);
-      q1 = __builtin_amdgcn_alignbyte(next_lane0(pd.q.x), pd.q.y, alq);
-    }
-    uint32_t m0, m1;
-    tri_masks((int)(pd.n & 0xFFFFu) - p0, m0, m1);
-    const uint32_t qm0 = q0 & m0, qm1 = q1 & m1;
-    uint32_t bad = 0;
-    uint32_t c0 = tri_codes(s0, m0, bad);
-    uint32_t c1 = tri_codes(s1, m1, bad);
-    if (__builtin_expect(bad != 0, 0)) {
-      const uint32_t sign = SUB ? 0xFFFFFFFFu : 1u;
-      c0 = tri_fix(s0, m0, c0, other(m), count ? lmax : 0, p0, sign);
-      c1 = tri_fix(s1, m1, c1, other(m), count ? lmax : 0, p0 + 4, sign);
-    }
-    const uint32_t cg0 = __builtin_amdgcn_perm(kCGHi, kCGLo, c0);
-    const uint32_t cg1 = __builtin_amdgcn_perm(kCGHi, kCGLo, c1);
-    if (count) {
-      TriAcc &ac = acc[m];
-      const uint32_t at0 = __builtin_amdgcn_perm(kATHi, kATLo, c0);
-      const uint32_t at1 = __builtin_amdgcn_perm(kATHi, kATLo, c1);
-      const uint32_t h0 = __builtin_amdgcn_perm(0u, qm0, 0x0C030C01u);   // bytes 1, 3
-      const uint32_t h1 = __builtin_amdgcn_perm(0u, qm1, 0x0C030C01u);
-      if (SUB) {
-        ac.c8[0][1] -= cg0 & 0x0F0F0F0Fu;
-        ac.c8[0][2] -= (cg0 >> 4) & 0x0F0F0F0Fu;
-        ac.c8[0][0] -= at0 & 0x0F0F0F0Fu;
-        ac.c8[0][3] -= (at0 >> 4) & 0x0F0F0F0Fu;
-        ac.c8[1][1] -= cg1 & 0x0F0F0F0Fu;
-        ac.c8[1][2] -= (cg1 >> 4) & 0x0F0F0F0Fu;
-        ac.c8[1][0] -= at1 & 0x0F0F0F0Fu;
-        ac.c8[1][3] -= (at1 >> 4) & 0x0F0F0F0Fu;
-        ac.q02[0] -= qm0 & 0x00FF00FFu;
-        ac.q13[0] -= h0;
-        ac.q02[1] -= qm1 & 0x00FF00FFu;
-        ac.q13[1] -= h1;
-      } else {
-        ac.n4[0][0] += cg0;
-        ac.n4[0][1] += at0;
-        ac.n4[1][0] += cg1;
-        ac.n4[1][1] += at1;
-        ac.q02[0] += qm0 & 0x00FF00FFu;
-        ac.q13[0] += h0;
-        ac.q02[1] += qm1 & 0x00FF00FFu;
-        ac.q13[1] += h1;
+      const uint32_t ns = next_lane0(pd.s[0]), nq = next_lane0(pd.q[0]);
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        sw[w] = __builtin_amdgcn_alignbyte(w + 1 < NW ? pd.s[(w + 1) % NW] : ns, pd.s[w], als);
+        qw[w] = __builtin_amdgcn_alignbyte(w + 1 < NW ? pd.q[(w + 1) % NW] : nq, pd.q[w], alq);
       }
     }
-    const uint32_t gc = (uint32_t)__builtin_popcount(cg1) + (uint32_t)__builtin_popcount(cg0);
-    const uint32_t qs = __builtin_amdgcn_sad_u8(qm1, 0u, __builtin_amdgcn_sad_u8(qm0, 0u, 0u));
+    uint32_t mk[NW];
+    tri_masks<NW>((int)(pd.n & 0xFFFFu) - p0, mk);
+    uint32_t qm[NW], cd[NW];
+    uint32_t bad = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      qm[w] = qw[w] & mk[w];
+      cd[w] = tri_codes(sw[w], mk[w], bad);
+    }
+    if (__builtin_expect(bad != 0, 0)) {
+      const uint32_t sign = SUB ? 0xFFFFFFFFu : 1u;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) cd[w] = tri_fix(sw[w], mk[w], cd[w], other(m), count ? lmax : 0, p0 + 4 * w, sign);
+    }
+    uint32_t cg[NW];
+#pragma unroll
+    for (int w = 0; w < NW; ++w) cg[w] = __builtin_amdgcn_perm(kCGHi, kCGLo, cd[w]);
+    if (count) {
+      TriAcc<NW> &ac = acc[m];
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        const uint32_t at = __builtin_amdgcn_perm(kATHi, kATLo, cd[w]);
+        const uint32_t h = __builtin_amdgcn_perm(0u, qm[w], 0x0C030C01u);   // bytes 1, 3
+        if (SUB) {
+          ac.c8[w][1] -= cg[w] & 0x0F0F0F0Fu;
+          ac.c8[w][2] -= (cg[w] >> 4) & 0x0F0F0F0Fu;
+          ac.c8[w][0] -= at & 0x0F0F0F0Fu;
+          ac.c8[w][3] -= (at >> 4) & 0x0F0F0F0Fu;
+          ac.q02[w] -= qm[w] & 0x00FF00FFu;
+          ac.q13[w] -= h;
+        } else {
+          ac.n4[w][0] += cg[w];
+          ac.n4[w][1] += at;
+          ac.q02[w] += qm[w] & 0x00FF00FFu;
+          ac.q13[w] += h;
+        }
+      }
+    }
+    uint32_t gc = 0, qs = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      gc += (uint32_t)__builtin_popcount(cg[w]);
+      qs = __builtin_amdgcn_sad_u8(qm[w], 0u, qs);
+    }
     return qs + (gc << 18);
   };
 
@@ -461,37 +511,37 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
   int64_t blk = gw;
   if (blk < nblocks) {
     load_block(blk, tb, len, tw, nraw);
-    const int nr0 = (int)min((int64_t)kTriBlock, A.num_reads - blk * kTriBlock);
-    load_group(0, tb, (nr0 + 2) / 3, 0, 0);
+    const int nr0 = (int)min((int64_t)kBlock, A.num_reads - blk * kBlock);
+    load_group(0, tb, (nr0 + kSegs - 1) / kSegs, 0, 0);
   }
-  const uint64_t not_seg_first = 0x6DB6DB6DB6DB6DB6ull;   // lanes j with j % 3 != 0
+  constexpr uint64_t not_seg_first = not_seg_first_mask<NW>();   // lanes j with j % kSegs != 0
   for (; blk < nblocks; blk += nw) {
-    const int64_t r0 = blk * kTriBlock;
-    const int nr = (int)min((int64_t)kTriBlock, A.num_reads - r0);
-    const int nt = (nr + 2) / 3;
+    const int64_t r0 = blk * kBlock;
+    const int nr = (int)min((int64_t)kBlock, A.num_reads - r0);
+    const int nt = (nr + kSegs - 1) / kSegs;
     const int64_t nblk = blk + nw < nblocks ? blk + nw : blk;   // next block (or self)
-    const int nnt = ((int)min((int64_t)kTriBlock, A.num_reads - nblk * kTriBlock) + 2) / 3;
+    const int nnt = ((int)min((int64_t)kBlock, A.num_reads - nblk * kBlock) + kSegs - 1) / kSegs;
     load_block(nblk, tb ^ 1, lenn, twn, nrawn);
-    if (stats && since_flush > kByteEvery - kTriBlock / 3) {   // keep every byte <= 255
+    if (stats && since_flush > kByteEvery - kBlock / kSegs) {   // keep every byte <= 255
 #pragma unroll
       for (int m = 0; m < NM; ++m) acc[m].flush(pos_acc(m), lmax, p0);
       since_flush = 0;
     }
     // an even number of groups per mate, so every mate (and block) starts in
     // slot 0 (the padding group gathers length-0 reads)
-    const int ngroups = ((nt + kTriU - 1) / kTriU + 1) & ~1;
+    const int ngroups = ((nt + kU - 1) / kU + 1) & ~1;
 
     auto run_mate = [&](auto mtag) {
       constexpr int m = decltype(mtag)::value;
       auto process_group = [&](int g, int slot) {
 #pragma unroll
-        for (int u = 0; u < kTriU; ++u) {
-          const int t = g * kTriU + u;
+        for (int u = 0; u < kU; ++u) {
+          const int t = g * kU + u;
           // every read is added; failed ones are taken out in the block epilogue
           const uint32_t x = account(MateTag<m>{}, grp[slot][u], stats, AddTag{});
           const uint32_t P = wave_scan(x);
-          // segment ends (lanes 20, 41, 62) -> wends[3t + seg], no wait needed
-          if (ls == 20 && seg < 3 && t < nt) wends(m)[3 * t + seg] = P;
+          // segment ends (the last lane of each segment) -> wends[kSegs t + seg], no wait needed
+          if (ls == kSegW - 1 && seg < kSegs && t < nt) wends(m)[kSegs * t + seg] = P;
         }
       };
       // after this mate's last group: the next mate's first group, or the next block's
@@ -506,7 +556,7 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
         else load_next_unit(0);
         process_group(g + 1, 1);
         // nibbles hold at most 15 triples: widen after groups 0-3 and at the end
-        static_assert(4 * kTriU <= kNibbleEvery && kTriBlock / 3 - 4 * kTriU <= kNibbleEvery, "");
+        static_assert(4 * kU <= kNibbleEvery && kBlock / kSegs - 4 * kU <= kNibbleEvery, "");
         if (stats && g == 2) acc[m].widen();
       }
       if (stats) acc[m].widen();
@@ -522,8 +572,8 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
     bool pass = valid;
 #pragma unroll
     for (int m = 0; m < NM; ++m) {
-      // per-read sums: difference of consecutive segment ends within a triple
-      // (wends[3t + k] = inclusive wave prefix at the end of segment k)
+      // per-read sums: difference of consecutive segment ends within a step
+      // (wends[kSegs t + k] = inclusive wave prefix at the end of segment k)
       const uint32_t ends = valid ? wends(m)[lane] : 0u;
       const uint32_t prev = __builtin_amdgcn_mov_dpp(ends, 0x138, 0xF, 0xF, true);   // lane j-1
       r1[m] = ends - (((not_seg_first >> lane) & 1u) ? prev : 0u);
@@ -562,22 +612,37 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
       }
     }
     if (stats) {
-      // take the failed reads (pairs: both mates) back out, a triple at a time
-      auto sub_mate = [&](auto mtag) {
-        constexpr int m = decltype(mtag)::value;
-        uint64_t fl = failed;
-        while (fl) {
-          const int j = (int)__builtin_ctzll(fl);
-          const int t = j / 3;
-          const uint32_t fbits = (uint32_t)(fl >> (3 * t)) & 7u;
-          fl &= ~(7ull << (3 * t));
-          TriPending pd;
-          gather(m, tb, ((fbits >> (seg & 3)) & 1u) ? min(3 * t + seg, 63) : 63, pd);
-          (void)account(MateTag<m>{}, pd, true, SubTag{});
+      // take the failed reads (pairs: both mates) back out.  A read must leave
+      // through the segment it entered by (its lanes' byte counters hold it;
+      // another segment's could borrow), so the failed reads of each segment
+      // class (j % kSegs) are listed by rank and step k takes the k-th of every
+      // class at once: max-per-class steps instead of one per step holding a
+      // failure.  The segment ends are consumed: mate 0's wends holds the list.
+      uint32_t *flist = wends(0);
+      constexpr uint64_t cls0 = ~not_seg_first;   // lanes j with j % kSegs == 0
+      const int cls = lane % kSegs;
+      const uint64_t below = (1ull << lane) - 1ull;
+      const int rank = __builtin_popcountll(failed & (cls0 << cls) & below);
+      __builtin_amdgcn_wave_barrier();
+      if (valid && !pass) flist[min(rank * kSegs + cls, 63)] = (uint32_t)lane;
+      __builtin_amdgcn_wave_barrier();
+      int nsub = 0, mycnt = 0;
+#pragma unroll
+      for (int c = 0; c < kSegs; ++c) {
+        const int n = __builtin_popcountll(failed & (cls0 << c));
+        nsub = max(nsub, n);
+        if (c == seg) mycnt = n;
+      }
+      for (int k = 0; k < nsub; ++k) {
+        const int src = seg < kSegs && k < mycnt ? (int)flist[min(k * kSegs + seg, 63)] : 63;
+        TriPending<NW> pd;
+        gather(0, tb, src, pd);
+        (void)account(MateTag<0>{}, pd, true, SubTag{});
+        if (NM == 2) {
+          gather(NM - 1, tb, src, pd);
+          (void)account(MateTag<NM - 1>{}, pd, true, SubTag{});
         }
-      };
-      sub_mate(MateTag<0>{});
-      if (NM == 2) sub_mate(MateTag<NM - 1>{});
+      }
     }
 #pragma unroll
     for (int m = 0; m < NM; ++m) len[m] = lenn[m];

@@ -47,14 +47,28 @@ STATS_CASES = {
 }
 
 
-@pytest.fixture(params=["auto", "single"])
+@pytest.fixture(params=["auto", "tri", "single"])
 def kernel_choice(request, monkeypatch):
-    """Run a test with the default kernel choice and with the one-read-per-wave
-    kernel forced (HPGQ_KERNEL=single), so both FAST kernels meet the oracle."""
+    """Run a test with the default kernel choice (the segmented kernel in its
+    16-byte-lane "hex" geometry where lmax <= 156), with its 8-byte-lane "tri"
+    geometry forced (HPGQ_TRI_GEO=tri) and with the one-read-per-wave kernel
+    forced (HPGQ_KERNEL=single), so every FAST kernel meets the oracle."""
+    monkeypatch.delenv("HPGQ_KERNEL", raising=False)
+    monkeypatch.delenv("HPGQ_TRI_GEO", raising=False)
     if request.param == "single":
         monkeypatch.setenv("HPGQ_KERNEL", "single")
+    elif request.param == "tri":
+        monkeypatch.setenv("HPGQ_TRI_GEO", "tri")
+    return request.param
+
+
+@pytest.fixture(params=["auto", "tri"])
+def geo_choice(request, monkeypatch):
+    """The segmented kernel's two geometries (edit runs on both)."""
+    if request.param == "tri":
+        monkeypatch.setenv("HPGQ_TRI_GEO", "tri")
     else:
-        monkeypatch.delenv("HPGQ_KERNEL", raising=False)
+        monkeypatch.delenv("HPGQ_TRI_GEO", raising=False)
     return request.param
 
 
@@ -66,7 +80,7 @@ def test_stats_filter_synthetic(name, kernel_choice):
     assert c[H.S_NUM_INPUT] == reads.n
 
 
-@pytest.mark.parametrize("L,lmax", [(160, 160), (150, 150), (60, 64), (3, 8)])
+@pytest.mark.parametrize("L,lmax", [(160, 160), (157, 157), (156, 156), (150, 150), (60, 64), (3, 8)])
 def test_tri_kernel_lengths(L, lmax, kernel_choice):
     reads = O.synth(7001, seed=12, L=L, trunc_pct=40, n_per_1024=30)
     p = H.stats_params(lmax=lmax, read_quality_range="18,", read_length_range="2,")
@@ -86,7 +100,7 @@ def test_read_lengths(L, lmax):
     assert_same(p, reads)
 
 
-def test_edit_trim_stats():
+def test_edit_trim_stats(geo_choice):
     reads = O.synth(20000, seed=4, L=150, trunc_pct=5)
     p = H.edit_params(lmax=150, stats=True, left_length=10, left_quality_range="20,",
                       right_length=30, right_quality_range="20,")
@@ -95,7 +109,7 @@ def test_edit_trim_stats():
 
 
 @pytest.mark.parametrize("left,right", [(1, 1), (8, 31), (16, 32), (17, 33), (16, 0), (0, 32)])
-def test_edit_window_sizes(left, right):
+def test_edit_window_sizes(left, right, geo_choice):
     """The trim at the window sizes where the kernel switches from one batch of
     loads (left <= 16, right <= 32) to the 8-byte loop, on reads as short as 0."""
     reads = O.synth(12000, seed=40 + left + right, L=150, trunc_pct=60)
@@ -109,7 +123,7 @@ def test_edit_window_sizes(left, right):
     assert c[H.S_NUM_EDITED] > 0
 
 
-def test_edit_with_filter():
+def test_edit_with_filter(geo_choice):
     reads = O.synth(20000, seed=5, L=150, trunc_pct=20)
     p = H.edit_params(lmax=150, stats=True, left_length=40, left_quality_range="30,",
                       right_length=60, right_quality_range="25,38",
@@ -160,7 +174,7 @@ def test_edge_reads(name, kernel_choice):
     assert_same(p, reads)
 
 
-def test_edge_reads_edit_phred64():
+def test_edge_reads_edit_phred64(geo_choice):
     reads = O.Reads.from_pairs(_edge_reads() * 5)
     p = H.edit_params(lmax=150, stats=True, quality_encoding="phred64", left_length=5,
                       left_quality_range="0,10", right_length=7, right_quality_range="3,",
