@@ -206,6 +206,7 @@ const char *hpgq_strerror(int code) {
     case HPGQ_E_RCCL: return "RCCL error";
     case HPGQ_E_STATE: return "invalid ctx state";
     case HPGQ_E_FORMAT: return "malformed FASTQ text";
+    case HPGQ_E_IO: return "file i/o error";
     default: return "unknown error";
   }
 }

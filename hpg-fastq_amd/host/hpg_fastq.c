@@ -98,6 +98,8 @@ int main(int argc, char **argv) {
   }
   free(counters);
   free(r.kmers);
+  free(r.cg_seq);
+  free(r.cg_q);
   cli_free(o);
   return rc;
 }

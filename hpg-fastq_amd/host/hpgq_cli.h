@@ -31,6 +31,9 @@ typedef struct {
   char *quality_encoding_name;
   int quality_encoding_value;
   int kmers_on;
+  /* chaos game (old/main_hpg_fastq_old.c:185-189: --cg | --chaos-game, --k, --gs-filename) */
+  int cg_on, k_cg;
+  char *gs_filename;
   /* filter / trim options, NO_VALUE (-1) when unset (src/stats_options.c:18-40) */
   char *read_length_range, *read_quality_range, *left_quality_range, *right_quality_range;
   int min_read_length, max_read_length, min_read_quality, max_read_quality;
@@ -64,6 +67,9 @@ typedef struct {
   double seconds, fastq_bytes;
   uint64_t *kmers;          /* --kmers: by_pos [HPGQ_NUM_KMERS][kmers_npos] (malloc'd) */
   int kmers_npos;
+  uint32_t *cg_seq, *cg_q;  /* --cg: table_seq / table_q [dim*dim] (malloc'd) */
+  uint32_t cg_words;        /* fq_word_count */
+  int cg_exact_calls;       /* chaos-game calls the exact simulation redid */
 } cli_result_t;
 
 int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, cli_result_t *res);

@@ -72,7 +72,12 @@ static void usage(const cli_options_t *o) {
   printf("  --num-threads=<int>             Number of threads (file readers)\n");
   printf("  --batch-size=<int>              Batch size (accepted; batches are --chunk-mb of text)\n");
   printf("  --quality-encoding=<string>     Encoding for quality scores: phred33, phred64\n");
-  if (o->command == CMD_STATS) printf("  --kmers                         Enable k-mers analysis (5-mer)\n");
+  if (o->command == CMD_STATS) {
+    printf("  --kmers                         Enable k-mers analysis (5-mer)\n");
+    printf("  --cg, --chaos-game              Genomic signature (chaos game) tables and images\n");
+    printf("  --k=<int>                       Chaos game word size (1-12, default 7)\n");
+    printf("  --gs-filename=<file>            Reference genomic signature: difference table and image\n");
+  }
   printf("  --read-length-range=<string>    Read length range, eg. 80,110\n");
   printf("  --read-quality-range=<string>   Read quality range, eg. 20,40\n");
   printf("  --left-length=<int>             Number of leftmost nucleotides to take into account to %s\n",
@@ -104,7 +109,7 @@ static int exists(const char *path) {
 enum {
   O_THREADS = 1000, O_BATCH, O_QENC, O_KMERS, O_LRANGE, O_QRANGE, O_LLEN, O_LQRANGE, O_RLEN,
   O_RQRANGE, O_MAXN, O_MAXOOQ, O_GPU, O_LMAX, O_CHUNK, O_PRINT, O_COUNTERS, O_QUIET,
-  O_KMERSOUT
+  O_KMERSOUT, O_CG, O_KCG, O_GS
 };
 
 cli_options_t *cli_parse(int command, const char *exec_name, int argc, char **argv) {
@@ -122,6 +127,7 @@ cli_options_t *cli_parse(int command, const char *exec_name, int argc, char **ar
   o->max_N = o->max_out_of_quality = HPGQ_NO_VALUE;
   o->lmax = HPGQ_LMAX_LIMIT;
   o->chunk_mb = 256;
+  o->k_cg = 7;   /* DEFAULT_K_IN_CHAOS_GAME */
   static const struct option longopts[] = {
       {"help", no_argument, 0, 'h'},
       {"fastq-file", required_argument, 0, 'f'},
@@ -130,6 +136,10 @@ cli_options_t *cli_parse(int command, const char *exec_name, int argc, char **ar
       {"batch-size", required_argument, 0, O_BATCH},
       {"quality-encoding", required_argument, 0, O_QENC},
       {"kmers", no_argument, 0, O_KMERS},
+      {"cg", no_argument, 0, O_CG},
+      {"chaos-game", no_argument, 0, O_CG},
+      {"k", required_argument, 0, O_KCG},
+      {"gs-filename", required_argument, 0, O_GS},
       {"read-length-range", required_argument, 0, O_LRANGE},
       {"read-quality-range", required_argument, 0, O_QRANGE},
       {"left-length", required_argument, 0, O_LLEN},
@@ -161,6 +171,12 @@ cli_options_t *cli_parse(int command, const char *exec_name, int argc, char **ar
         if (command != CMD_STATS) usage(o);
         o->kmers_on = 1;
         break;
+      case O_CG:
+        if (command != CMD_STATS) usage(o);
+        o->cg_on = 1;
+        break;
+      case O_KCG: o->k_cg = atoi(optarg); break;
+      case O_GS: o->gs_filename = strdup(optarg); break;
       case O_LRANGE: o->read_length_range = strdup(optarg); break;
       case O_QRANGE: o->read_quality_range = strdup(optarg); break;
       case O_LLEN: o->left_length = atoi(optarg); break;
@@ -220,6 +236,14 @@ cli_options_t *cli_parse(int command, const char *exec_name, int argc, char **ar
     exit(-1);
   }
   if (o->num_threads < 1) o->num_threads = 1;
+  if (o->cg_on && (o->k_cg < 1 || o->k_cg > 12)) {
+    printf("\nError: --k must be in 1..12\n");
+    exit(-1);
+  }
+  if (o->gs_filename && !exists(o->gs_filename)) {
+    printf("\nError: Genomic signature file not found !\n");
+    usage(o);
+  }
   /* filter_on (src/stats_options.c:177-213; edit's ignores left/right,
    * src/edit_options.c:190-215) */
   int n = 0;
@@ -271,6 +295,11 @@ void cli_display(const cli_options_t *o) {
   if (o->max_out_of_quality != HPGQ_NO_VALUE && o->read_quality_range)
     printf("\tMax. out of quality : %i nucletotides\n", o->max_out_of_quality), shown++;
   if (!shown) printf("\tNone.\n");
+  if (o->cg_on) {
+    printf("\nChaos game options\n");
+    printf("\tWord size (k)       : %d\n", o->k_cg);
+    printf("\tGenomic signature   : %s\n", o->gs_filename ? o->gs_filename : "(none)");
+  }
   printf("\nArchitecture options\n");
   printf("\tGPU                 : %d (gfx950)\n", o->device);
   printf("\tReader threads      : %d\n", o->num_threads);
@@ -341,5 +370,6 @@ void cli_free(cli_options_t *o) {
   free(o->right_quality_range);
   free(o->counters_out);
   free(o->kmers_out);
+  free(o->gs_filename);
   free(o);
 }

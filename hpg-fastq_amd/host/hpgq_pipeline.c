@@ -281,11 +281,16 @@ int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, 
   hpgq_ctx_t *ctx = NULL;
   hpgq_parser_t *ps = NULL;
   hpgq_kmers_t *km = NULL;
+  hpgq_cgr_t *cg = NULL;
   int rc = hpgq_open(&ctx, o->device, p);
   if (rc == 0) rc = hpgq_parser_open(&ps, o->device, hpgq_stream(ctx));
   /* --kmers counts the reads the stats merge (passed ones when filtering,
    * src/stats_fastq.c:268-272,384-410) on the engine's stream, after it */
   if (rc == 0 && o->kmers_on) rc = hpgq_kmers_open(&km, o->device, p->lmax, hpgq_stream(ctx));
+  /* --cg: chaos_game_fill_tables per parsed chunk (one call = one chunk), the
+   * base quality from --quality-encoding; with a filter only the passed reads
+   * (ONLY_VALID_READS with the mask as read_status, old/chaos_game.c:188) */
+  if (rc == 0 && o->cg_on) rc = hpgq_cgr_open(&cg, o->device, o->k_cg, p->phred);
   const size_t chunk = (size_t)o->chunk_mb << 20;
   for (int i = 0; i < NSLOTS && rc == 0; ++i) {
     P.slot[i].cap = chunk + MAX_CARRY;
@@ -297,7 +302,7 @@ int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, 
   size_t dcap = 0;
   const int writes = o->command != CMD_STATS;
   const int edit = o->command == CMD_EDIT;
-  const int need_mask = writes || (km && o->filter_on);
+  const int need_mask = writes || ((km || cg) && o->filter_on);
   if (rc == 0 && writes) {
     char path[4096];
     snprintf(path, sizeof(path), "%s/%s.fq", o->out_dirname, edit ? "edit" : "passed");
@@ -347,6 +352,12 @@ int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, 
         if (rc == 0) rc = hpgq_parse_records(ps, s->rec_start, s->seq_start, s->plus_start, s->qual_start);
       }
       if (rc == 0) rc = hpgq_sync(ctx);
+      if (rc == 0 && cg) {   /* after the parse and the mask; settled before the next parse reuses b */
+        rc = hpgq_cgr_fill_device(cg, &b, o->filter_on ? d_mask : NULL,
+                                  o->filter_on ? HPGQ_CGR_ONLY_VALID_READS : HPGQ_CGR_ALL_READS);
+        if (rc == 0) rc = hpgq_cgr_sync(cg);
+        if (rc == 0) res->cg_exact_calls += hpgq_cgr_last_exact(cg);
+      }
       res->num_reads += (uint64_t)b.num_reads;
     } else if (rc == 0) {
       s->nreads = 0;
@@ -368,6 +379,12 @@ int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, 
     res->kmers_npos = p->lmax > HPGQ_KMER_K - 1 ? p->lmax - (HPGQ_KMER_K - 1) : 0;
     res->kmers = calloc(hpgq_kmers_size(km) + 1, sizeof(uint64_t));
     rc = res->kmers ? hpgq_kmers_read(km, res->kmers, hpgq_kmers_size(km)) : HPGQ_E_NOMEM;
+  }
+  if (rc == 0 && cg) {
+    const size_t cells = (size_t)1 << (2 * o->k_cg);
+    res->cg_seq = calloc(cells, sizeof(uint32_t));
+    res->cg_q = calloc(cells, sizeof(uint32_t));
+    rc = res->cg_seq && res->cg_q ? hpgq_cgr_read(cg, res->cg_seq, res->cg_q, &res->cg_words) : HPGQ_E_NOMEM;
   }
   res->seconds = now_s() - t0;
   if (rc == 0) {
@@ -394,6 +411,7 @@ done:
   free(P.carry);
   hpgq_parser_close(ps);
   hpgq_kmers_close(km);
+  hpgq_cgr_close(cg);
   hpgq_close(ctx);
   close(P.fd);
   return rc;

@@ -90,6 +90,48 @@ static int report_kmers(const cli_options_t *o, const char *base, const cli_resu
   return 0;
 }
 
+/* --cg: chaos_game_calculate_table_dif / validate / write_table_images
+ * (old/chaos_game.c:320-472) on the device tables: <in>_k=<k>_FG.pgm,
+ * _QQ.pgm, with --gs-filename _FG_dif.pgm, and <in>.chaos_game.txt with the
+ * word count, norms and the difference table's range, mean and deviation */
+static int report_cg(const cli_options_t *o, const char *base, const cli_result_t *res) {
+  const int k = o->k_cg;
+  const size_t cells = (size_t)1 << (2 * k);
+  int32_t *dif = NULL, hi = 0, lo = 0;
+  uint32_t *gs = NULL, ref_words = 0;
+  double mean = 0.0, sd = 0.0;
+  int rc = 0;
+  if (o->gs_filename) {
+    gs = calloc(cells, sizeof(uint32_t));
+    dif = calloc(cells, sizeof(int32_t));
+    rc = gs && dif ? hpgq_cgr_load_gs(o->gs_filename, k, gs, &ref_words) : HPGQ_E_NOMEM;
+    if (rc == 0) rc = hpgq_cgr_table_dif(k, res->cg_seq, res->cg_words, gs, ref_words, dif, &hi, &lo);
+    if (rc == 0) rc = hpgq_cgr_dif_stats(k, dif, &mean, &sd);
+  }
+  FILE *f = rc == 0 ? open_out(o, base, "chaos_game.txt") : NULL;
+  if (f) {
+    const double mem = (double)cells;
+    fprintf(f, "Chaos game (genomic signature), k = %d, %dx%d\n", k, 1 << k, 1 << k);
+    fprintf(f, "Words read in FastQ file: %u\n", res->cg_words);
+    if (res->cg_words) fprintf(f, "Fastq file normalization ratio = %12.6f\n", 128.0 / (res->cg_words / mem));
+    if (o->gs_filename) {
+      fprintf(f, "Genomic signature file: %s (%u words)\n", o->gs_filename, ref_words);
+      if (ref_words) fprintf(f, "Genomic signature normalization ratio = %12.6f\n", 128.0 / (ref_words / mem));
+      fprintf(f, "Interval of variation of diff matrix values = [%d, %d]\n", hi, lo);
+      fprintf(f, "Diff matrix mean = %f, standard deviation = %f\n", mean, sd);
+    }
+    fprintf(f, "Calls redone by the exact double simulation: %d\n", res->cg_exact_calls);
+    fclose(f);
+  } else if (rc == 0) {
+    rc = HPGQ_E_IO;
+  }
+  if (rc == 0 && res->cg_words)
+    rc = hpgq_cgr_write_images(o->out_dirname, o->in_filename, k, res->cg_seq, res->cg_q, res->cg_words, dif);
+  free(gs);
+  free(dif);
+  return rc;
+}
+
 int cli_report(const cli_options_t *o, const hpgq_params_t *p, const uint64_t *c,
                const cli_result_t *res) {
   const int lmax = p->lmax, phred = p->phred;
@@ -178,6 +220,10 @@ int cli_report(const cli_options_t *o, const hpgq_params_t *p, const uint64_t *c
     return -1;
   }
   free(krows);
+  if (res && res->cg_seq && report_cg(o, base, res)) {
+    free(cnt);
+    return -1;
+  }
 
   if ((f = open_out(o, base, "length.histogram.data"))) {
     for (int i = 1; i <= maxlen; i++) fprintf(f, "%i\t%lu\n", i, (unsigned long)hl[i]);

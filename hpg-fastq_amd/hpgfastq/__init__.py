@@ -13,4 +13,6 @@ from ._abi import (  # noqa: F401
     counters_len, layout, check, params_default, exported_symbols,
 )
 from .engine import Engine, ChaosGame, Kmers, Parser, summary, complete_prefix  # noqa: F401
+from .engine import (cgr_write_gs, cgr_load_gs, cgr_table_dif, cgr_dif_stats,  # noqa: F401
+                     cgr_normalize_quality, cgr_write_pgm, cgr_write_images)
 from .options import parse_range, filter_params, edit_params, stats_params  # noqa: F401

@@ -117,6 +117,15 @@ _SIGS = [
     ("hpgq_cgr_last_replays", C.c_int64, [C.c_void_p]),
     ("hpgq_cgr_set_path", C.c_int, [C.c_void_p, C.c_int]),
     ("hpgq_cgr_last_exact", C.c_int, [C.c_void_p]),
+    ("hpgq_cgr_load_gs", C.c_int, [C.c_char_p, C.c_int, C.c_void_p, C.c_void_p]),
+    ("hpgq_cgr_write_gs", C.c_int, [C.c_char_p, C.c_int, C.c_void_p, C.c_uint32]),
+    ("hpgq_cgr_table_dif", C.c_int, [C.c_int, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32,
+                                     C.c_void_p, C.c_void_p, C.c_void_p]),
+    ("hpgq_cgr_dif_stats", C.c_int, [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]),
+    ("hpgq_cgr_normalize_quality", C.c_int, [C.c_int, C.c_void_p, C.c_void_p]),
+    ("hpgq_cgr_write_pgm", C.c_int, [C.c_char_p, C.c_int, C.c_void_p, C.c_double]),
+    ("hpgq_cgr_write_images", C.c_int, [C.c_char_p, C.c_char_p, C.c_int, C.c_void_p, C.c_void_p,
+                                        C.c_uint32, C.c_void_p]),
     ("hpgq_kmers_open", C.c_int, [C.POINTER(C.c_void_p), C.c_int, C.c_int, C.c_void_p]),
     ("hpgq_kmers_close", None, [C.c_void_p]),
     ("hpgq_kmers_count_device", C.c_int, [C.c_void_p, C.POINTER(Batch), C.c_void_p]),

@@ -174,6 +174,60 @@ class ChaosGame:
         return ts.reshape(self.dim, self.dim), tq.reshape(self.dim, self.dim), int(wc[0])
 
 
+def cgr_write_gs(path, k, table, word_count):
+    """hpgq_cgr_write_gs: a genomic-signature file (header_gs_t + dim*dim u32)."""
+    t = np.ascontiguousarray(table, dtype=np.uint32).reshape(-1)
+    check(lib.hpgq_cgr_write_gs(path.encode(), k, _ptr(t), word_count), "hpgq_cgr_write_gs")
+
+
+def cgr_load_gs(path, k):
+    """hpgq_cgr_load_gs -> (table u32 [dim*dim], ref_word_count)."""
+    t = np.zeros(1 << (2 * k), dtype=np.uint32)
+    w = np.zeros(1, dtype=np.uint32)
+    check(lib.hpgq_cgr_load_gs(path.encode(), k, _ptr(t), _ptr(w)), "hpgq_cgr_load_gs")
+    return t, int(w[0])
+
+
+def cgr_table_dif(k, table_seq, fq_words, table_gs, ref_words):
+    """hpgq_cgr_table_dif -> (int32 table_dif, highest, lowest)."""
+    ts = np.ascontiguousarray(table_seq, dtype=np.uint32).reshape(-1)
+    tg = np.ascontiguousarray(table_gs, dtype=np.uint32).reshape(-1)
+    d = np.zeros(ts.size, dtype=np.int32)
+    hl = np.zeros(2, dtype=np.int32)
+    check(lib.hpgq_cgr_table_dif(k, _ptr(ts), fq_words, _ptr(tg), ref_words, _ptr(d),
+                                 _ptr(hl), hl.ctypes.data + 4), "hpgq_cgr_table_dif")
+    return d, int(hl[0]), int(hl[1])
+
+
+def cgr_dif_stats(k, table_dif):
+    d = np.ascontiguousarray(table_dif, dtype=np.int32).reshape(-1)
+    ms = np.zeros(2, dtype=np.float64)
+    check(lib.hpgq_cgr_dif_stats(k, _ptr(d), _ptr(ms), ms.ctypes.data + 8), "hpgq_cgr_dif_stats")
+    return float(ms[0]), float(ms[1])
+
+
+def cgr_normalize_quality(k, table_seq, table_q):
+    ts = np.ascontiguousarray(table_seq, dtype=np.uint32).reshape(-1)
+    tq = np.array(table_q, dtype=np.uint32).reshape(-1)
+    check(lib.hpgq_cgr_normalize_quality(k, _ptr(ts), _ptr(tq)), "hpgq_cgr_normalize_quality")
+    return tq
+
+
+def cgr_write_pgm(path, k, table, norm):
+    t = np.ascontiguousarray(table, dtype=np.uint32).reshape(-1)
+    check(lib.hpgq_cgr_write_pgm(path.encode(), k, _ptr(t), norm), "hpgq_cgr_write_pgm")
+
+
+def cgr_write_images(report_dir, fq_path, k, table_seq, table_q, fq_words, table_dif=None):
+    """hpgq_cgr_write_images: <dir>/<fq>_k=<k>_FG.pgm, _QQ.pgm (+ _FG_dif.pgm)."""
+    ts = np.ascontiguousarray(table_seq, dtype=np.uint32).reshape(-1)
+    tq = np.array(table_q, dtype=np.uint32).reshape(-1)
+    d = None if table_dif is None else np.ascontiguousarray(table_dif, dtype=np.int32).reshape(-1)
+    check(lib.hpgq_cgr_write_images(report_dir.encode(), fq_path.encode(), k, _ptr(ts), _ptr(tq),
+                                    fq_words, _ptr(d) if d is not None else None),
+          "hpgq_cgr_write_images")
+
+
 class Kmers:
     """hpgq_kmers: `stats --kmers` 5-mer counts per start position
     (merge src/stats_fastq.c:384-410; build-defined per-read rule)."""

@@ -63,6 +63,7 @@ extern "C" {
 #define HPGQ_E_RCCL            (-6)   /* RCCL communicator / collective error */
 #define HPGQ_E_STATE           (-7)   /* call not valid in this ctx state     */
 #define HPGQ_E_FORMAT          (-8)   /* malformed FASTQ text                 */
+#define HPGQ_E_IO              (-9)   /* file open / read / write failed      */
 
 /* ---------------------------------------------------------------------- */
 /* batch                                                                  */
@@ -298,6 +299,34 @@ int  hpgq_cgr_set_path(hpgq_cgr_t *cg, int path);
  * hpgq_cgr_sync / hpgq_cgr_read / hpgq_cgr_reset, so its batch must stay
  * valid until then (as for any asynchronous fill). */
 int  hpgq_cgr_last_exact(hpgq_cgr_t *cg);
+
+/*
+ * CGR post-processing on the host (O(4^k), old/chaos_game.c:269-593); tables
+ * are row-major [co_x][co_y] of dim*dim cells as hpgq_cgr_read returns them.
+ *   genomic-signature (GS) file = header_gs_t (old/chaos_game.h:65-70: char
+ *   gs_filename[180], u32 word_size_k, dim_x, dim_y, ref_word_count) + the
+ *   dim*dim u32 table.
+ */
+#define HPGQ_GS_HEADER_BYTES 196
+/* chaos_game_load_table_gs_direct (:297-318) */
+int  hpgq_cgr_load_gs(const char *path, int k, uint32_t *table_gs, uint32_t *ref_word_count);
+/* header_gs_init (:43-50) + the table: writes a GS file for a reference */
+int  hpgq_cgr_write_gs(const char *path, int k, const uint32_t *table, uint32_t word_count);
+/* chaos_game_calculate_table_dif (:320-373): int table_dif = seq*128/(fq/4^k) - gs*128/(ref/4^k) */
+int  hpgq_cgr_table_dif(int k, const uint32_t *table_seq, uint32_t fq_word_count,
+                        const uint32_t *table_gs, uint32_t ref_word_count, int32_t *table_dif,
+                        int32_t *highest, int32_t *lowest);
+/* chaos_game_validate_table_dif (:375-408): mean and standard deviation of table_dif */
+int  hpgq_cgr_dif_stats(int k, const int32_t *table_dif, double *mean, double *std_dev);
+/* chaos_game_normalize_quality_table_ (:487-502), in place */
+int  hpgq_cgr_normalize_quality(int k, const uint32_t *table_seq, uint32_t *table_q);
+/* chaos_game_generate_pgm_file_ (:521-593) */
+int  hpgq_cgr_write_pgm(const char *path, int k, const uint32_t *table, double norm);
+/* chaos_game_write_table_images (:410-472): <dir>/<fq file>_k=<k>_FG.pgm, _QQ.pgm
+ * (normalises table_q in place) and, when table_dif is given, _FG_dif.pgm */
+int  hpgq_cgr_write_images(const char *report_dir, const char *fq_path, int k,
+                           const uint32_t *table_seq, uint32_t *table_q, uint32_t fq_word_count,
+                           const int32_t *table_dif);
 
 /* ---------------------------------------------------------------------- */
 /* stats --kmers: 5-mer counts (src/stats_options.c:274, merge              */

@@ -12,6 +12,8 @@ Reference lines followed:
   edit options        src/edit_fastq.c:148-151, src/edit_options.c:280-283
   chaos game          old/chaos_game.c:165-267
   --kmers merge       src/stats_fastq.c:384-410 (per-read k-mers: build-defined)
+  CGR post-processing old/chaos_game.c:269-593 (cgr_* below; C float/double/int
+                      conversions spelled out with numpy scalars)
 """
 
 NUM_SCALARS = 8
@@ -223,3 +225,63 @@ def kmers(reads, lmax, mask=None):
 def kmer_string(kid):
     """id -> 5 letters, first base most significant (kmers_string, src/stats_fastq.c:479)."""
     return "".join("ACGT"[(kid >> (2 * (4 - i))) & 3] for i in range(5))
+
+
+# ---- CGR post-processing (old/chaos_game.c:269-593) -------------------------
+GS_HEADER_BYTES = 196   # header_gs_t, old/chaos_game.h:65-70
+
+
+def cgr_gs_bytes(table, k, word_count, name=b""):
+    """A GS file: header_gs_t {char[180], k, dim_x, dim_y, ref_word_count} + u32 table."""
+    import struct
+    dim = 1 << k
+    return (name[:179].ljust(180, b"\0") + struct.pack("<4I", k, dim, dim, word_count) +
+            b"".join(struct.pack("<I", int(v) & 0xFFFFFFFF) for v in table))
+
+
+def cgr_table_dif(k, table_seq, fq_words, table_gs, ref_words):
+    """chaos_game_calculate_table_dif (:320-373): int(seq*fq_norm - gs*gs_norm)."""
+    mem = 1 << (2 * k)
+    fq_norm = 128.0 / (1.0 * fq_words / mem)
+    gs_norm = 128.0 / (1.0 * ref_words / mem)
+    dif = [int(float(a) * fq_norm - float(b) * gs_norm) for a, b in zip(table_seq, table_gs)]
+    hi, lo = -32768, 32768   # (:342-343)
+    for v in dif:
+        hi = max(hi, v)
+        lo = min(lo, v)
+    return dif, hi, lo
+
+
+def cgr_dif_stats(table_dif):
+    """chaos_game_validate_table_dif (:375-408), accumulators zeroed (quirk Q12)."""
+    n = float(len(table_dif))
+    m = 0.0
+    for v in table_dif:
+        m += v
+    m /= n
+    s = 0.0
+    for v in table_dif:
+        s += (v - m) ** 2
+    return m, (s / n) ** 0.5
+
+
+def cgr_normalize_quality(k, table_seq, table_q):
+    """chaos_game_normalize_quality_table_ (:487-502): q / k / count (unsigned division)."""
+    return [(q // k) // c if c > 0 else 0 for c, q in zip(table_seq, table_q)]
+
+
+def cgr_pgm(k, table, norm):
+    """chaos_game_generate_pgm_file_ (:521-593): bytes of the binary PGM."""
+    import numpy as np
+    dim = 1 << k
+    redim = 128 if k < 7 else dim
+    zoom = 1 << (7 - k) if k < 7 else 1
+    img = bytearray(redim * redim)
+    for i in range(dim):
+        for j in range(dim):
+            v = np.float32(np.float32(table[i * dim + j]) * np.float64(norm))   # float * double -> float
+            px = int(v) & 0xFF                                                      # (int), then (uchar)
+            for ii in range(zoom):
+                for jj in range(zoom):
+                    img[(i * zoom + ii) * redim + j * zoom + jj] = px
+    return b"P5\n%d %d\n255\n" % (redim, redim) + bytes(img)

@@ -136,3 +136,43 @@ def test_cli_stats_kmers(tmp_path, filt):
     summ = (out / "in.fq.summary.txt").read_text()
     assert "K-mers (top 20)" in summ and f"\t{names[order[0]]}\t\t{int(tot[order[0]])}" in summ
     del rng
+
+
+@pytest.mark.parametrize("filtered", [False, True])
+def test_cli_chaos_game(tmp_path, filtered):
+    """stats --cg --k 5 --gs-filename: the device tables (one call: the file is
+    one parse unit) against the oracle, then the old tool's images and the
+    difference-table summary (old/chaos_game.c:320-472) against the Python
+    restatement."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    import pyref as R
+    k = 5
+    reads = O.synth(8000, seed=31, L=150)
+    fq = _write(tmp_path, reads, name="cg.fq")
+    ref = O.synth(3000, seed=32, L=200)
+    rts, _rtq, rwc = O.cgr(k, ref, 33)
+    gs = tmp_path / "ref.gs"
+    H.cgr_write_gs(str(gs), k, rts, int(rwc[0]))
+    out = tmp_path / "out"
+    out.mkdir()
+    args = ["stats", "-f", fq, "-o", out, "--cg", "--k", k, "--gs-filename", gs, "--lmax", 150,
+            "--quiet"]
+    status = None
+    if filtered:
+        args += ["--read-quality-range", "20,"]
+        p = H.stats_params(lmax=150, read_quality_range="20,")
+        status, _, _ = O.run(p, reads)
+    run_cli(args)
+    ts, tq, wc = O.cgr(k, reads, 33, status=status, mode=1 if filtered else 0)
+    wc = int(wc[0])
+    mem = 1 << (2 * k)
+    assert (out / "cg.fq_k=5_FG.pgm").read_bytes() == R.cgr_pgm(k, ts.tolist(), 128.0 / (wc / mem))
+    qn = R.cgr_normalize_quality(k, ts.tolist(), tq.tolist())
+    assert (out / "cg.fq_k=5_QQ.pgm").read_bytes() == R.cgr_pgm(k, qn, 256.0 / 62)
+    dif, hi, lo = R.cgr_table_dif(k, ts.tolist(), wc, rts.tolist(), int(rwc[0]))
+    absd = [min(abs(v), 255) for v in dif]
+    assert (out / "cg.fq_k=5_FG_dif.pgm").read_bytes() == R.cgr_pgm(k, absd, 1.0)
+    txt = (out / "cg.fq.chaos_game.txt").read_text()
+    assert f"Words read in FastQ file: {wc}" in txt
+    assert f"Interval of variation of diff matrix values = [{hi}, {lo}]" in txt
