@@ -130,6 +130,9 @@ static const void *tri_for(int mw, bool un, int nm, bool edit) {
   using hpgq::engine_tri_kernel;
   if (edit) return mw <= 4 ? (const void *)engine_tri_kernel<4, false, 1, true, NW>
                            : (const void *)engine_tri_kernel<5, false, 1, true, NW>;
+  if constexpr (NW == 4) {
+    if (un && !edit) return (const void *)engine_tri_kernel<4, true, 1, false, 4>;
+  }
   if constexpr (NW == 2) {
     if (nm == 2) {   // paired-end (tri geometry: two mates' accumulators do not fit hex's registers)
       if (mw <= 4) return (const void *)engine_tri_kernel<4, false, 2, false, 2>;
@@ -157,7 +160,7 @@ static const void *kernel_for(int nm, int nch, bool gen, bool tri, bool hex, boo
     mw = mw <= 4 ? 4 : (mw == 5 ? 5 : 6);
     if (hex) mw = 4;   // 116-123 VGPRs
     if (edit && mw > 5) mw = 5;
-    const bool un = !hex && !edit && nm == 1 && u && std::atoi(u) != 0;
+    const bool un = !edit && nm == 1 && u && std::atoi(u) != 0;
     std::snprintf(name, cap, "hpgq::engine_tri_kernel<%d, %s, %d, %s, %d>", mw, un ? "true" : "false", edit ? 1 : nm,
                   edit ? "true" : "false", nw);
     return hex ? tri_for<4>(mw, un, nm, edit) : tri_for<2>(mw, un, nm, edit);
@@ -298,7 +301,7 @@ int hpgq_open(hpgq_ctx_t **out, int device, const hpgq_params_t *p) {
     // the three-read kernel: per mate [6][lmax] + hist + scalars, and per wave
     // and mate two read tables (2 x 1 KB) + segment ends (256 B)
     const size_t mate_words = (size_t)6 * p->lmax + (((size_t)hlen + 1) & ~(size_t)1) + 2 * HPGQ_NUM_SCALARS;
-    const size_t tri_lds = (size_t)c->nm * mate_words * 4 + 16 +
+    const size_t tri_lds = (size_t)c->nm * mate_words * 4 + 16 + 17 * 16 +   // + the byte-mask table
                            (size_t)hpgq::kWaves * c->nm * (2 * 256 + 64) * 4;
     if (tri_lds > c->lds_bytes) c->lds_bytes = tri_lds;
   }

@@ -172,8 +172,10 @@ struct TriAcc {
 // codes of a masked word; marks bytes that are not exactly A/C/G/T/N
 __device__ __forceinline__ uint32_t tri_codes(uint32_t s, uint32_t m, uint32_t &bad) {
   const uint32_t codes = s & m & 0x07070707u;
+#if HPGQ_TRI_ABL != 1   // (1: timing probe only, no exactness check)
   const uint32_t ex = __builtin_amdgcn_perm(kX7Hi, kX7Lo, codes);
   bad |= (s ^ ex) & m;
+#endif
   return codes;
 }
 
@@ -311,7 +313,6 @@ struct MateTag {
 template <int MINW, bool UNAL, int NM, bool EDIT, int NW>
 __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
   static_assert(!EDIT || NM == 1, "edit on the three-read kernel is single-end");
-  static_assert(!UNAL || NW == 2, "unaligned loads: tri only");
   using G = Geo<NW>;
   constexpr int kSegs = G::kSegs, kSegW = G::kSegW, kBlock = G::kBlock, kU = G::kU;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -347,6 +348,13 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
   uint32_t *wtab = base + tab_words + wave * kWaveWords;
   auto tab = [&](int m, int tb) { return wtab + m * (2 * 256 + 64) + tb * 256; };
   auto wends = [&](int m) { return wtab + m * (2 * 256 + 64) + 2 * 256; };
+  // byte masks by valid-byte count c = clamp(n - p0, 0, 4 NW): mtab[c][w]
+  // (one LDS read per step instead of a clamp and a 64-bit shift per word)
+  uint32_t *mtab = base + tab_words + kWaves * kWaveWords;   // 16 B aligned
+  for (int i = tid; i < (4 * NW + 1) * NW; i += kWG) {
+    const int nb = min(max(i / NW - 4 * (i % NW), 0), 4);
+    mtab[i] = nb == 4 ? 0xFFFFFFFFu : (1u << (8 * nb)) - 1u;
+  }
   for (int i = tid; i < NM * mate_words; i += kWG) base[i] = 0;
   __syncthreads();
 
@@ -459,7 +467,23 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
       }
     }
     uint32_t mk[NW];
-    tri_masks<NW>((int)(pd.n & 0xFFFFu) - p0, mk);
+#ifndef HPGQ_TRI_MTAB
+#define HPGQ_TRI_MTAB 1
+#endif
+    if (!HPGQ_TRI_MTAB) {
+      tri_masks<NW>((int)(pd.n & 0xFFFFu) - p0, mk);
+    } else {
+      const int c = min(max((int)(pd.n & 0xFFFFu) - p0, 0), 4 * NW);
+      if (NW == 4) {
+        const v4u t = *reinterpret_cast<const v4u *>(mtab + 4 * c);
+#pragma unroll
+        for (int w = 0; w < NW; ++w) mk[w] = t[w & 3];
+      } else {
+        const v2u t = *reinterpret_cast<const v2u *>(mtab + 2 * c);
+#pragma unroll
+        for (int w = 0; w < NW; ++w) mk[w] = t[w & 1];
+      }
+    }
     uint32_t qm[NW], cd[NW];
     uint32_t bad = 0;
 #pragma unroll
