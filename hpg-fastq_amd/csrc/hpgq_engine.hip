@@ -132,6 +132,7 @@ static const void *tri_for(int mw, bool un, int nm, bool edit) {
                            : (const void *)engine_tri_kernel<5, false, 1, true, NW>;
   if constexpr (NW == 4) {
     if (un && !edit) return (const void *)engine_tri_kernel<4, true, 1, false, 4>;
+    if (nm == 2) return (const void *)engine_tri_kernel<3, false, 2, false, 4>;   // 3 waves/SIMD: two mates' accumulators
   }
   if constexpr (NW == 2) {
     if (nm == 2) {   // paired-end (tri geometry: two mates' accumulators do not fit hex's registers)
@@ -158,7 +159,7 @@ static const void *kernel_for(int nm, int nch, bool gen, bool tri, bool hex, boo
     const int nw = hex ? 4 : 2;
     int mw = w ? std::atoi(w) : (hex ? 4 : (nm == 2 ? 4 : 5));   // spill-free occupancy per variant
     mw = mw <= 4 ? 4 : (mw == 5 ? 5 : 6);
-    if (hex) mw = 4;   // 116-123 VGPRs
+    if (hex) mw = nm == 2 ? 3 : 4;   // 116-123 VGPRs (SE)
     if (edit && mw > 5) mw = 5;
     const bool un = !edit && nm == 1 && u && std::atoi(u) != 0;
     std::snprintf(name, cap, "hpgq::engine_tri_kernel<%d, %s, %d, %s, %d>", mw, un ? "true" : "false", edit ? 1 : nm,
@@ -291,7 +292,8 @@ int hpgq_open(hpgq_ctx_t **out, int device, const hpgq_params_t *p) {
              !(force && std::strcmp(force, "single") == 0);
     c->tri_edit = c->tri && edit;
     const char *geo = std::getenv("HPGQ_TRI_GEO");   // "tri" forces the 8-byte-lane geometry
-    c->hex = c->tri && c->nm == 1 && p->lmax <= hpgq::kHexPos && !(geo && std::strcmp(geo, "tri") == 0);
+    c->hex = c->tri && p->lmax <= hpgq::kHexPos &&
+             !(geo && std::strcmp(geo, "tri") == 0);
   }
   {
     const int hlen = p->lmax + 1 + HPGQ_MEANQ_BINS + HPGQ_GC_BINS;

@@ -131,7 +131,7 @@ def test_edit_with_filter(geo_choice):
     assert_same(p, reads)
 
 
-def test_paired_end():
+def test_paired_end(geo_choice):
     r1 = O.synth(10000, seed=6, L=150, trunc_pct=5, mate=0)
     r2 = O.synth(10000, seed=6, L=150, trunc_pct=5, mate=1)
     assert np.array_equal(np.diff(r1.idx), np.diff(r2.idx))
@@ -142,7 +142,7 @@ def test_paired_end():
     assert c[H.S_NUM_PASSED] == c[ln + H.S_NUM_PASSED]
 
 
-def test_paired_edit():
+def test_paired_edit(geo_choice):
     r1 = O.synth(5000, seed=8, L=150, mate=0)
     r2 = O.synth(5000, seed=8, L=150, mate=1)
     p = H.edit_params(lmax=150, stats=True, left_length=10, left_quality_range="20,",
