@@ -282,7 +282,8 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
   __shared__ uint32_t scb[kWaves * 2 * 64];   // per wave: two start bitmaps (this tile, next tile)
   __shared__ uint32_t last;
   for (int i = threadIdx.x; i < cells + 1; i += kWG) tab[i] = 0ull;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: spans, tiles and buffer descriptors stay scalar
   uint32_t *sc = scb + 128 * wid;
   sc[lane] = 0u;
   sc[64 + lane] = 0u;
@@ -418,8 +419,13 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
         // addr = E bit j ? w : SPARE (v_bfe_i32 + v_bfi_b32; left to itself the
         // compiler spends three instructions on it)
         uint32_t e, addr;
+#if HPGQ_CGR_ABL == 5   // timing probe only: no emission select
+        addr = w;
+        (void)e;
+#else
         asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(e) : "v"(E), "i"(j));
         asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(addr) : "v"(e), "v"(w), "s"(SPARE));
+#endif
         const unsigned long long inc = ((unsigned long long)acc << 32) | 1ull;
 #if HPGQ_CGR_ABL == 3   // timing probe only: no table adds
         if (__builtin_expect(addr == 0xFFFFFFFFu, 0))
