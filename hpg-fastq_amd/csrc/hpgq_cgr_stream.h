@@ -64,7 +64,10 @@ constexpr int kWG = kWaves * 64;
 constexpr int kLaneBytes = HPGQ_CGR_LANE_BYTES;   // 16 or 32
 constexpr int kNdw = kLaneBytes / 4;
 constexpr int kTile = 64 * kLaneBytes;       // bytes per wave tile (2 KB)
-constexpr int kSpanLog = 14;
+#ifndef HPGQ_CGR_SPAN_LOG
+#define HPGQ_CGR_SPAN_LOG 14
+#endif
+constexpr int kSpanLog = HPGQ_CGR_SPAN_LOG;
 constexpr int kSpan = 1 << kSpanLog;         // bytes per span (16 KB, 8 tiles)
 constexpr int kMaxK = 7;                     // 4^7 u64 cells = 128 KB of LDS
 constexpr int64_t kMaxSpans = ((int64_t)1 << 31) / kSpan + 2;
@@ -230,9 +233,11 @@ __device__ __forceinline__ int32_t idx_window(const SArgs &A, int64_t r, int lan
 // read starts in [base, limit) (limit - base <= 64 * kLaneBytes): bits into
 // the wave's LDS bitmap sc[64], advancing the cursor r past them.  iw is the
 // window at r (loaded ahead by the caller); it comes back as the window at
-// the new r, its load in flight.
+// the new r, its load in flight.  hop: the tile is its span's last, so the
+// cursor moves on to rn (the next span's first read) instead.
 __device__ __forceinline__ void scatter_starts(const SArgs &A, uint32_t *sc, int64_t &r, int32_t &iw,
-                                               int32_t base, int32_t limit, int lane) {
+                                               int32_t base, int32_t limit, int lane, bool hop = false,
+                                               int64_t rn = 0) {
   auto put = [&](int32_t x) {
     const bool in = x < limit;
     const uint32_t o = (uint32_t)(x - base);
@@ -247,14 +252,15 @@ __device__ __forceinline__ void scatter_starts(const SArgs &A, uint32_t *sc, int
       c = put(idx_window(A, r, lane));
     } while (c == 64);
   }
+  if (hop) r = rn;
   iw = idx_window(A, r, lane);
 }
 
 // a lane's bytes at o (o >= 0) from a buffer descriptor; bytes past the end read 0
-__device__ __forceinline__ void load32(__amdgpu_buffer_rsrc_t rsrc, int32_t o, uint32_t w[kNdw]) {
+__device__ __forceinline__ void load32(__amdgpu_buffer_rsrc_t rsrc, uint32_t o, uint32_t w[kNdw]) {
 #pragma unroll
   for (int h = 0; h < kNdw / 4; ++h) {
-    const v4u a = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (uint32_t)o + 16u * h, 0, 0);
+    const v4u a = __builtin_amdgcn_raw_buffer_load_b128(rsrc, o + 16u * h, 0, 0);
     w[4 * h] = a[0]; w[4 * h + 1] = a[1]; w[4 * h + 2] = a[2]; w[4 * h + 3] = a[3];
   }
 }
@@ -279,14 +285,15 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
   constexpr uint32_t SPARE = (uint32_t)cells << 3;      // the spare cell
   constexpr uint32_t kRun = 48 - K;
   __shared__ unsigned long long tab[cells + 1];
-  __shared__ uint32_t scb[kWaves * 2 * 64];   // per wave: two start bitmaps (this tile, next tile)
+  __shared__ uint32_t scb[kWaves * 3 * 64];   // per wave: two start bitmaps (this tile, next tile) + context
   __shared__ uint32_t last;
   for (int i = threadIdx.x; i < cells + 1; i += kWG) tab[i] = 0ull;
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: spans, tiles and buffer descriptors stay scalar
-  uint32_t *sc = scb + 128 * wid;
+  uint32_t *sc = scb + 192 * wid;
   sc[lane] = 0u;
   sc[64 + lane] = 0u;
+  sc[128 + lane] = 0u;
   __syncthreads();
 
   const int32_t b0 = __builtin_amdgcn_readfirstlane(A.idx[0]);
@@ -296,54 +303,67 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
   const int64_t gw = (int64_t)blockIdx.x * kWaves + wid, nwav = (int64_t)gridDim.x * kWaves;
   bool risky = false;
 
-  for (int64_t s = gw; s < ns; s += nwav) {
-    const int32_t t0 = a0 + (int32_t)(s << kSpanLog);
-    const int32_t tend = (int32_t)min((int64_t)t0 + kSpan, (int64_t)b1);
-    // descriptors ending at the span: the prefetch past its last tile reads
-    // zeros without touching memory.  The range check is per dword, so a dword
-    // straddling the end still loads (HPGQ_DEVICE_SLACK readable bytes; bytes
-    // >= tend are masked)
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc((void *)A.seq, (short)0, tend + HPGQ_DEVICE_SLACK, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rq =
-        __builtin_amdgcn_make_buffer_rsrc((void *)A.qual, (short)0, tend + HPGQ_DEVICE_SLACK, 0x00020000);
-    int64_t r = A.span_first[s];
-    int32_t iw = idx_window(A, r, lane);
-    // ---- context: the kLaneBytes bytes before the span, the same on every lane
+  // one descriptor pair per call: offsets past b1 + slack read zeros without
+  // memory traffic (the context loads of tiles that enter no span, the
+  // prefetch past a wave's last span); a tile crossing b1 is masked.  The
+  // range check is per dword, so a dword straddling b1 still loads
+  // (HPGQ_DEVICE_SLACK readable bytes).
+  const uint32_t nrec = (uint32_t)b1 + HPGQ_DEVICE_SLACK;
+  const uint32_t kPast = nrec;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)A.seq, (short)0, nrec, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc((void *)A.qual, (short)0, nrec, 0x00020000);
+  // span cursors through the scalar cache (read-only here)
+  const __attribute__((address_space(4))) int32_t *sfirst =
+      (const __attribute__((address_space(4))) int32_t *)A.span_first;
+  uint32_t *scx = sc + 128;   // the context bitmap: starts in the 32 bytes before a span
+
+  // The wave's spans s = gw, gw + nwav, ... form one tile stream: the next
+  // tile's bytes, read-start bits and (entering a span) context are fetched
+  // while this tile is counted, across span boundaries too, so a span start
+  // costs no memory round trip.  The cursor of the next span (rn) is read at
+  // span entry and taken over when the span's last tile is scattered.
+  if (gw < ns) {
+    int64_t s = gw;
     uint32_t pxy6, pxy7, pq6, pq7, pv, pS;   // the previous lane's last two dwords, V and starts
     // the run open at the tile start per axis: exact when eknown, else at
     // most 15 (the last 16 bytes hold a Z on both axes) and walked back for
     // only when a tile needs the exact scan
     uint32_t einx = 15, einy = 15;
     bool eknown = false;
-    {
-      const int32_t c0 = t0 - kLaneBytes;
-      uint32_t sw[kNdw], qw[kNdw];
-      load32(rs, max(c0, 0), sw);
-      load32(rq, max(c0, 0), qw);
-      if (c0 < b0) mask_range(c0, b0, t0, sw, qw);
+    // span entry: the 16 bytes before t0 (all 'N' before the batch) and the
+    // read starts among the 32 before it
+    auto enter = [&](const uint32_t (&cs)[4], const uint32_t (&cq)[2], const uint32_t ps, const int32_t t0) {
+      uint32_t sw[kNdw];
+#pragma unroll
+      for (int d = 0; d < kNdw; ++d) sw[d] = d < kNdw - 4 ? 0x4E4E4E4Eu : cs[d - (kNdw - 4)];
       const Cls c = classify(sw);
-      pxy6 = c.xy[kNdw - 2];
-      pxy7 = c.xy[kNdw - 1];
-      pq6 = qw[kNdw - 2];
-      pq7 = qw[kNdw - 1];
-      pv = c.v;
-      scatter_starts(A, sc, r, iw, c0, t0, lane);
-      __builtin_amdgcn_wave_barrier();
-      pS = __builtin_amdgcn_readfirstlane(sc[0]);
-      __builtin_amdgcn_wave_barrier();
-      sc[0] = 0u;
+      pxy6 = __builtin_amdgcn_readfirstlane(c.xy[kNdw - 2]);
+      pxy7 = __builtin_amdgcn_readfirstlane(c.xy[kNdw - 1]);
+      pq6 = __builtin_amdgcn_readfirstlane(cq[0]);
+      pq7 = __builtin_amdgcn_readfirstlane(cq[1]);
+      pv = __builtin_amdgcn_readfirstlane(c.v);
+      pS = ps;
+      einx = einy = 15;
+      eknown = false;
       if (!(c.zhi & 0x01010101u) || !(c.zhi & 0x02020202u)) {
         einx = run_before<0>(A, b0, t0, kRun);
         einy = run_before<1>(A, b0, t0, kRun);
         eknown = true;
       }
-    }
-    // ---- tiles, unrolled by two with A/B registers: the next tile's bytes
-    // and read-start bits are fetched while this one is counted (the bitmap
-    // read then waits behind this tile's table adds, not in front of them),
-    // the idx window one scatter ahead
-    auto tile = [&](const int32_t t, uint32_t (&sw)[kNdw], uint32_t (&qw)[kNdw], const uint32_t so) {
+    };
+    auto ctx_starts = [&](int64_t &r, int32_t &iw, const int32_t t0) {
+      scatter_starts(A, scx, r, iw, t0 - kLaneBytes, t0, lane);
+      __builtin_amdgcn_wave_barrier();
+      const uint32_t ps = __builtin_amdgcn_readfirstlane(scx[0]);
+      __builtin_amdgcn_wave_barrier();
+      scx[0] = 0u;
+      return ps;
+    };
+    // mid: runs between the tile's set-up and its table adds (the next tile's
+    // start scatter: its LDS read then waits behind the previous tile's adds,
+    // long drained, rather than behind this one's)
+    auto tile = [&](const int32_t t, const int32_t tend, uint32_t (&sw)[kNdw], uint32_t (&qw)[kNdw],
+                    const uint32_t so, auto &&mid) {
       const int32_t o = t + kLaneBytes * lane;
 #if HPGQ_CGR_ABL == 4   // timing probe only: loads and start bitmaps, no counting
       {
@@ -351,6 +371,7 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
 #pragma unroll
         for (int d = 0; d < kNdw; ++d) x ^= sw[d] ^ qw[d];
         if (__builtin_expect(x == 0x12345678u, 0)) risky = true;
+        mid();
         return;
       }
 #endif
@@ -408,6 +429,7 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
 #pragma unroll
       for (int j = kLaneBytes - K; j < kLaneBytes; ++j)
         acc += __builtin_amdgcn_ubfe(j < kLaneBytes - 4 ? nq6 : nq7, 8 * (j & 3), 8);
+      mid();
       // one ds_add_u64 per byte: count | quality sum << 32 (spare cell: no word)
 #pragma unroll
       for (int j = 0; j < kLaneBytes; ++j) {
@@ -440,31 +462,68 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
       pv = __builtin_amdgcn_readlane(c.v, 63);
       pS = __builtin_amdgcn_readlane(so, 63);
     };
-    uint32_t sA[kNdw], qA[kNdw], sB[kNdw], qB[kNdw];
-    load32(rs, t0 + kLaneBytes * lane, sA);
-    load32(rq, t0 + kLaneBytes * lane, qA);
-    scatter_starts(A, sc, r, iw, t0, t0 + kTile, lane);
-    uint32_t soA = sc[lane], soB;
-    // straight-line halves (no branch around a load: the compiler then counts
-    // the loads in flight exactly and the tile waits only for its own bytes);
-    // past the span the loads read zeros and the bitmaps are cleared below
-    for (int32_t t = t0;; t += 2 * kTile) {
-      const int32_t tb = t + kTile;
-      scatter_starts(A, sc + 64, r, iw, tb, tb + kTile, lane);
-      soB = sc[64 + lane];
-      load32(rs, tb + kLaneBytes * lane, sB);
-      load32(rq, tb + kLaneBytes * lane, qB);
-      sc[lane] = 0u;
-      tile(t, sA, qA, soA);
-      if (tb >= tend) break;
-      const int32_t ta = tb + kTile;
-      scatter_starts(A, sc, r, iw, ta, ta + kTile, lane);
-      soA = sc[lane];
-      load32(rs, ta + kLaneBytes * lane, sA);
-      load32(rq, ta + kLaneBytes * lane, qA);
-      sc[64 + lane] = 0u;
-      tile(tb, sB, qB, soB);
-      if (ta >= tend) break;
+    int32_t tA = a0 + (int32_t)(s << kSpanLog), tB;
+    int32_t eA = (int32_t)min((int64_t)tA + kSpan, (int64_t)b1), eB;
+    int64_t r = sfirst[s];
+    int64_t rn = sfirst[min(s + nwav, ns - 1)];
+    int32_t iw = idx_window(A, r, lane);
+    {
+      uint32_t cs[4] = {0x4E4E4E4Eu, 0x4E4E4E4Eu, 0x4E4E4E4Eu, 0x4E4E4E4Eu}, cq[2] = {0u, 0u};
+      if (s != 0) {   // spans after the first start >= 16 KB past b0
+        const v4u a = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)tA - 16u, 0, 0);
+        const v2u q = __builtin_amdgcn_raw_buffer_load_b64(rq, (uint32_t)tA - 8u, 0, 0);
+        cs[0] = a[0]; cs[1] = a[1]; cs[2] = a[2]; cs[3] = a[3];
+        cq[0] = q[0]; cq[1] = q[1];
+      }
+      enter(cs, cq, ctx_starts(r, iw, tA), tA);
+    }
+    uint32_t sA[kNdw], qA[kNdw], sB[kNdw], qB[kNdw], soA, soB;
+    scatter_starts(A, sc, r, iw, tA, tA + kTile, lane, tA + kTile >= eA, rn);
+    soA = sc[lane];
+    load32(rs, (uint32_t)(tA + kLaneBytes * lane), sA);
+    load32(rq, (uint32_t)(tA + kLaneBytes * lane), qA);
+    // count tile x while fetching tile y (straight-line: the loads are
+    // unconditional, so the compiler counts the loads in flight exactly and
+    // a tile waits only for its own bytes); false past the wave's last tile
+    auto half = [&](const int32_t tx, const int32_t ex, uint32_t (&sx)[kNdw], uint32_t (&qx)[kNdw], const uint32_t sox,
+                    uint32_t *scpx, int32_t &ty, int32_t &ey, uint32_t (&sy)[kNdw], uint32_t (&qy)[kNdw],
+                    uint32_t &soy, uint32_t *scpy) {
+      ty = tx + kTile;
+      ey = ex;
+      bool entering = false, fin = false;
+      uint32_t psn = 0;
+      if (ty >= ex) {   // x is its span's last tile: y is the next span's first
+        s += nwav;
+        if (s < ns) {
+          ty = a0 + (int32_t)(s << kSpanLog);
+          ey = (int32_t)min((int64_t)ty + kSpan, (int64_t)b1);
+          entering = true;
+          rn = sfirst[min(s + nwav, ns - 1)];
+          psn = ctx_starts(r, iw, ty);
+        } else {
+          fin = true;
+        }
+      }
+      const v4u a = __builtin_amdgcn_raw_buffer_load_b128(rs, entering ? (uint32_t)ty - 16u : kPast, 0, 0);
+      const v2u q = __builtin_amdgcn_raw_buffer_load_b64(rq, entering ? (uint32_t)ty - 8u : kPast, 0, 0);
+      const uint32_t oy = fin ? kPast : (uint32_t)(ty + kLaneBytes * lane);
+      load32(rs, oy, sy);
+      load32(rq, oy, qy);
+      scpx[lane] = 0u;
+      tile(tx, ex, sx, qx, sox, [&] {
+        scatter_starts(A, scpy, r, iw, ty, fin ? INT32_MIN : ty + kTile, lane, ty + kTile >= ey, rn);
+        soy = scpy[lane];
+      });
+      if (fin) return false;
+      if (entering) {
+        const uint32_t cs[4] = {a[0], a[1], a[2], a[3]}, cq[2] = {q[0], q[1]};
+        enter(cs, cq, psn, ty);
+      }
+      return true;
+    };
+    for (;;) {
+      if (!half(tA, eA, sA, qA, soA, sc, tB, eB, sB, qB, soB, sc + 64)) break;
+      if (!half(tB, eB, sB, qB, soB, sc + 64, tA, eA, sA, qA, soA, sc)) break;
     }
     sc[lane] = 0u;
     sc[64 + lane] = 0u;

@@ -41,6 +41,52 @@ __global__ void __launch_bounds__(kWG) k_flat(const char *a, const char *b, uint
   out[blockIdx.x * kWG + threadIdx.x] = x;
 }
 
+// lane owns 32 contiguous bytes: two 16-byte loads at stride 32 (each wave
+// load touches twice the cache lines of a contiguous one); U tiles in flight
+template <int U>
+__global__ void __launch_bounds__(kWG) k_s32(const char *a, const char *b, uint32_t n, uint32_t *out) {
+  const auto ra = rsrc(a, n), rb = rsrc(b, n);
+  uint32_t x = 0;
+  const uint32_t step = gridDim.x * kWG * 32;
+  for (uint32_t o = (blockIdx.x * kWG + threadIdx.x) * 32; o < n; o += U * step) {
+    v4u p[U][2], q[U][2];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      p[u][0] = __builtin_amdgcn_raw_buffer_load_b128(ra, o + u * step, 0, 0);
+      p[u][1] = __builtin_amdgcn_raw_buffer_load_b128(ra, o + u * step + 16, 0, 0);
+      q[u][0] = __builtin_amdgcn_raw_buffer_load_b128(rb, o + u * step, 0, 0);
+      q[u][1] = __builtin_amdgcn_raw_buffer_load_b128(rb, o + u * step + 16, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      for (int h = 0; h < 2; ++h) x ^= p[u][h].x ^ p[u][h].y ^ p[u][h].z ^ p[u][h].w ^ q[u][h].x ^ q[u][h].y ^ q[u][h].z ^ q[u][h].w;
+  }
+  out[blockIdx.x * kWG + threadIdx.x] = x;
+}
+
+// contiguous 16-byte lanes, two wave loads 1 KB apart (same bytes per lane as k_s32)
+template <int U>
+__global__ void __launch_bounds__(kWG) k_c16(const char *a, const char *b, uint32_t n, uint32_t *out) {
+  const auto ra = rsrc(a, n), rb = rsrc(b, n);
+  uint32_t x = 0;
+  const uint32_t step = gridDim.x * kWG * 32;
+  const int lane = threadIdx.x & 63;
+  for (uint32_t o = (blockIdx.x * kWG + (threadIdx.x & ~63)) * 32 + 16 * lane; o < n; o += U * step) {
+    v4u p[U][2], q[U][2];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      p[u][0] = __builtin_amdgcn_raw_buffer_load_b128(ra, o + u * step, 0, 0);
+      p[u][1] = __builtin_amdgcn_raw_buffer_load_b128(ra, o + u * step + 1024, 0, 0);
+      q[u][0] = __builtin_amdgcn_raw_buffer_load_b128(rb, o + u * step, 0, 0);
+      q[u][1] = __builtin_amdgcn_raw_buffer_load_b128(rb, o + u * step + 1024, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      for (int h = 0; h < 2; ++h) x ^= p[u][h].x ^ p[u][h].y ^ p[u][h].z ^ p[u][h].w ^ q[u][h].x ^ q[u][h].y ^ q[u][h].z ^ q[u][h].w;
+  }
+  out[blockIdx.x * kWG + threadIdx.x] = x;
+}
+
 // R reads per wave step, S lanes per read, W bytes per lane
 template <int R, int S, int W>
 __global__ void __launch_bounds__(kWG) k_reads(const char *a, const char *b, uint32_t n, const int32_t *idx,
@@ -91,7 +137,7 @@ int main() {
   hipEventCreate(&e0);
   hipEventCreate(&e1);
   auto run = [&](const char *name, auto launch) {
-    for (int occ : {4, 8, 16, 32}) {
+    for (int occ : {4, 8, 16}) {
       const int grid = cus * occ;
       launch(grid);
       hipDeviceSynchronize();
@@ -107,6 +153,10 @@ int main() {
   };
   run("x4", [&](int g) { k_flat<16><<<g, kWG>>>(a, b, n, out, 1); });
   run("x2", [&](int g) { k_flat<8><<<g, kWG>>>(a, b, n, out, 1); });
+  run("s32u1", [&](int g) { k_s32<1><<<g, kWG>>>(a, b, n, out); });
+  run("s32u2", [&](int g) { k_s32<2><<<g, kWG>>>(a, b, n, out); });
+  run("c16u1", [&](int g) { k_c16<1><<<g, kWG>>>(a, b, n, out); });
+  run("c16u2", [&](int g) { k_c16<2><<<g, kWG>>>(a, b, n, out); });
   run("tri", [&](int g) { k_reads<3, 21, 8><<<g, kWG>>>(a, b, n, idx, nreads, out); });
   run("hex", [&](int g) { k_reads<6, 10, 16><<<g, kWG>>>(a, b, n, idx, nreads, out); });
   return 0;
