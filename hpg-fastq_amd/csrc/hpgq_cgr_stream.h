@@ -69,6 +69,9 @@ constexpr int kTile = 64 * kLaneBytes;       // bytes per wave tile (2 KB)
 #endif
 constexpr int kSpanLog = HPGQ_CGR_SPAN_LOG;
 constexpr int kSpan = 1 << kSpanLog;         // bytes per span (16 KB, 8 tiles)
+#ifndef HPGQ_CGR_CHAINS
+#define HPGQ_CGR_CHAINS 1   // independent add chains per lane and tile (2: measured no faster)
+#endif
 constexpr int kMaxK = 7;                     // 4^7 u64 cells = 128 KB of LDS
 constexpr int64_t kMaxSpans = ((int64_t)1 << 31) / kSpan + 2;
 constexpr int kSlots = 256;                  // fills in flight between two syncs
@@ -302,6 +305,9 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
   const int64_t ns = nspans(a0, b1);
   const int64_t gw = (int64_t)blockIdx.x * kWaves + wid, nwav = (int64_t)gridDim.x * kWaves;
   bool risky = false;
+#if HPGQ_CGR_ABL == 6
+  uint32_t sink = 0;
+#endif
 
   // one descriptor pair per call: offsets past b1 + slack read zeros without
   // memory traffic (the context loads of tiles that enter no span, the
@@ -431,8 +437,7 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
         acc += __builtin_amdgcn_ubfe(j < kLaneBytes - 4 ? nq6 : nq7, 8 * (j & 3), 8);
       mid();
       // one ds_add_u64 per byte: count | quality sum << 32 (spare cell: no word)
-#pragma unroll
-      for (int j = 0; j < kLaneBytes; ++j) {
+      auto step = [&](const int j, uint32_t &w, uint32_t &acc) {
         w = ((w << 2) | __builtin_amdgcn_perm(0u, c.xy[j >> 2], 0x0C0C0C00u | (j & 3))) & M;
         const int jo = j - K;   // the byte leaving the quality window
         const uint32_t qold = jo >= 0 ? __builtin_amdgcn_ubfe(qw[jo >> 2], 8 * (jo & 3), 8)
@@ -449,11 +454,33 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
         asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(addr) : "v"(e), "v"(w), "s"(SPARE));
 #endif
         const unsigned long long inc = ((unsigned long long)acc << 32) | 1ull;
+#if HPGQ_CGR_ABL == 6   // timing probe only: the adds replaced by one VALU op
+        sink += addr ^ (uint32_t)(inc >> 32);
+#else
 #if HPGQ_CGR_ABL == 3   // timing probe only: no table adds
         if (__builtin_expect(addr == 0xFFFFFFFFu, 0))
 #endif
         atomicAdd(reinterpret_cast<unsigned long long *>(reinterpret_cast<char *>(tab) + addr), inc);
+#endif
+      };
+#if HPGQ_CGR_CHAINS == 2
+      // two independent chains (bytes [0,16) and [16,32)) interleaved: the
+      // second's window and quality sum start from bytes 9..15 of this lane
+      constexpr int kH = kLaneBytes / 2;
+      uint32_t w2 = 0, acc2 = 0;
+#pragma unroll
+      for (int j = kH - (K - 1); j < kH; ++j) w2 = ((w2 << 2) | __builtin_amdgcn_perm(0u, c.xy[j >> 2], 0x0C0C0C00u | (j & 3))) & M;
+#pragma unroll
+      for (int j = kH - K; j < kH; ++j) acc2 += __builtin_amdgcn_ubfe(qw[j >> 2], 8 * (j & 3), 8);
+#pragma unroll
+      for (int j = 0; j < kH; ++j) {
+        step(j, w, acc);
+        step(j + kH, w2, acc2);
       }
+#else
+#pragma unroll
+      for (int j = 0; j < kLaneBytes; ++j) step(j, w, acc);
+#endif
       // carry the last lane to the next tile's lane 0
       pxy6 = __builtin_amdgcn_readlane(c.xy[kNdw - 2], 63);
       pxy7 = __builtin_amdgcn_readlane(c.xy[kNdw - 1], 63);
@@ -528,6 +555,9 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
     sc[lane] = 0u;
     sc[64 + lane] = 0u;
   }
+#if HPGQ_CGR_ABL == 6
+  if (sink == 0x12345678u) risky = true;
+#endif
   if (__ballot(risky) && lane == 0) atomicOr(A.gate, GATE_EXACT);
   __syncthreads();
   for (int i = threadIdx.x; i < cells; i += kWG) {
