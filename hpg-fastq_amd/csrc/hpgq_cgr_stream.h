@@ -79,10 +79,10 @@ constexpr int kSlots = 256;                  // fills in flight between two sync
 constexpr uint32_t GATE_EXACT = 1;   // the exact kernels must run
 
 // byte & 7 -> per-byte LUTs (v_perm_b32, codes A=1 C=3 T=4 N=6 G=7)
-constexpr uint32_t kXYLo = 0x00000800u;   // code << 3, code = x | y << 1: A 1, C 0
-constexpr uint32_t kXYHi = 0x10000018u;   //                               T 3, G 2
-constexpr uint32_t kVLo = 0xFF00FF00u;    // 0xFF for A/C/G/T, 0 for N
-constexpr uint32_t kVHi = 0xFF0000FFu;
+constexpr uint32_t kCdLo = 0x00000100u;   // code = x | y << 1: A 1, C 0
+constexpr uint32_t kCdHi = 0x02000003u;   //                    T 3, G 2
+constexpr uint32_t kV1Lo = 0x01000100u;   // 1 for A/C/G/T, 0 for N
+constexpr uint32_t kV1Hi = 0x01000001u;
 constexpr uint32_t kZLo = 0x03000200u;    // bit0: a Z move on x (C/G), bit1: on y (A/C)
 constexpr uint32_t kZHi = 0x01000000u;
 
@@ -130,29 +130,34 @@ __device__ __forceinline__ uint32_t dpp_shr1(uint32_t old, uint32_t v) {   // la
 
 // a lane's bytes of seq: LUT lookups, exactness and per-lane summaries
 struct Cls {
-  uint32_t xy[kNdw];   // per byte: (x | y << 1) << 3
+  uint32_t cd[kNdw];   // per byte: its code x | y << 1
+  uint32_t p0, p1;     // the 32 codes packed, byte j at bits 2j of the 64-bit p1:p0
   uint32_t v;          // bit j: byte j is A/C/G/T
   uint32_t zlo, zhi;   // OR of per-byte Z bits (bit0 x, bit1 y) over the first / last 16 bytes
   uint32_t bad;        // nonzero: a byte that is not exactly A/C/G/T/N
 };
 
 __device__ __forceinline__ Cls classify(const uint32_t s[kNdw]) {
+  static_assert(kNdw == 8, "the packed code stream assumes 32 bytes per lane");
   Cls c;
-  uint32_t bad = 0, zl = 0, zh = 0, vp[kNdw / 2];
-#pragma unroll
-  for (int d = 0; d < kNdw / 2; ++d) vp[d] = 0u;
+  uint32_t bad = 0, zl = 0, zh = 0, vp[kNdw / 2], g[kNdw];
 #pragma unroll
   for (int d = 0; d < kNdw; ++d) {
     const uint32_t code = s[d] & 0x07070707u;
-    bad |= s[d] ^ __builtin_amdgcn_perm(hpgq::cgr::kExHi, hpgq::cgr::kExLo, code);
-    c.xy[d] = __builtin_amdgcn_perm(kXYHi, kXYLo, code);
+    // bad |= s ^ expected (v_bitop3: one op, no compare per dword)
+    bad = __builtin_amdgcn_bitop3_b32(bad, s[d], __builtin_amdgcn_perm(hpgq::cgr::kExHi, hpgq::cgr::kExLo, code), 0xF6);
+    c.cd[d] = __builtin_amdgcn_perm(kCdHi, kCdLo, code);
+    g[d] = __builtin_amdgcn_udot4(c.cd[d], 0x40100401u, 0u, false);   // 4 codes -> 8 bits
     const uint32_t z = __builtin_amdgcn_perm(kZHi, kZLo, code);
     if (d < 4) zl |= z;
     if (d >= kNdw - 4) zh |= z;
-    // gather the V bit of byte j to bit j: byte weights 1,2,4,8 (<< 4 for odd dwords), v_sad_u8 sums
-    const uint32_t vb = __builtin_amdgcn_perm(kVHi, kVLo, code) & ((d & 1) ? 0x80402010u : 0x08040201u);
-    vp[d >> 1] = __builtin_amdgcn_sad_u8(vb, 0u, vp[d >> 1]);
+    // the V bit of byte j to bit j: byte weights 1,2,4,8 (<< 4 for odd dwords) by v_dot4
+    const uint32_t v1 = __builtin_amdgcn_perm(kV1Hi, kV1Lo, code);
+    vp[d >> 1] = (d & 1) ? __builtin_amdgcn_udot4(v1, 0x80402010u, vp[d >> 1], false)
+                         : __builtin_amdgcn_udot4(v1, 0x08040201u, 0u, false);
   }
+  c.p0 = g[0] | (g[1] << 8) | (g[2] << 16) | (g[3] << 24);
+  c.p1 = g[4] | (g[5] << 8) | (g[6] << 16) | (g[7] << 24);
   c.v = 0;
 #pragma unroll
   for (int d = 0; d < kNdw / 2; ++d) c.v |= vp[d] << (8 * d);
@@ -173,7 +178,7 @@ __device__ __forceinline__ RunSum run_sum(const Cls &c) {
 #pragma unroll
   for (int j = 0; j < kLaneBytes; ++j) {
     if (!((c.v >> j) & 1u)) continue;
-    const uint32_t d = (c.xy[j >> 2] >> (8 * (j & 3) + 3 + AX)) & 1u;
+    const uint32_t d = (c.cd[j >> 2] >> (8 * (j & 3) + AX)) & 1u;
     if (d) {
       ++r.cnt;
       ++r.sfx;
@@ -330,7 +335,7 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
   // span entry and taken over when the span's last tile is scattered.
   if (gw < ns) {
     int64_t s = gw;
-    uint32_t pxy6, pxy7, pq6, pq7, pv, pS;   // the previous lane's last two dwords, V and starts
+    uint32_t pp1, pq6, pq7, pv, pS;   // the previous lane's packed codes 16..31, last quality dwords, V and starts
     // the run open at the tile start per axis: exact when eknown, else at
     // most 15 (the last 16 bytes hold a Z on both axes) and walked back for
     // only when a tile needs the exact scan
@@ -343,8 +348,7 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
 #pragma unroll
       for (int d = 0; d < kNdw; ++d) sw[d] = d < kNdw - 4 ? 0x4E4E4E4Eu : cs[d - (kNdw - 4)];
       const Cls c = classify(sw);
-      pxy6 = __builtin_amdgcn_readfirstlane(c.xy[kNdw - 2]);
-      pxy7 = __builtin_amdgcn_readfirstlane(c.xy[kNdw - 1]);
+      pp1 = __builtin_amdgcn_readfirstlane(c.p1);
       pq6 = __builtin_amdgcn_readfirstlane(cq[0]);
       pq7 = __builtin_amdgcn_readfirstlane(cq[1]);
       pv = __builtin_amdgcn_readfirstlane(c.v);
@@ -406,7 +410,7 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
         eknown = false;
       }
       // neighbours (lane 0: the previous tile's last lane / the span context)
-      const uint32_t nxy6 = dpp_shr1(pxy6, c.xy[kNdw - 2]), nxy7 = dpp_shr1(pxy7, c.xy[kNdw - 1]);
+      const uint32_t np1 = dpp_shr1(pp1, c.p1);   // the code stream below byte 0
       const uint32_t nq6 = dpp_shr1(pq6, qw[kNdw - 2]), nq7 = dpp_shr1(pq7, qw[kNdw - 1]);
       const uint32_t nv = dpp_shr1(pv, c.v), nS = dpp_shr1(pS, so);
       // emission: bytes [i-K+1, i] all A/C/G/T and no read start in (i-K+1, i]
@@ -427,31 +431,35 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
         }
         E = (uint32_t)((K == 1 ? V : R & (V << (K - 1))) >> 32);
       }
-      // the code window and the quality sum at the previous lane's last byte
-      uint32_t w = 0, acc = 0;
-#pragma unroll
-      for (int j = kLaneBytes - (K - 1); j < kLaneBytes; ++j)
-        w = ((w << 2) | __builtin_amdgcn_perm(0u, j < kLaneBytes - 4 ? nxy6 : nxy7, 0x0C0C0C00u | (j & 3))) & M;
+      // the quality sum at the previous lane's last byte
+      uint32_t acc = 0;
 #pragma unroll
       for (int j = kLaneBytes - K; j < kLaneBytes; ++j)
         acc += __builtin_amdgcn_ubfe(j < kLaneBytes - 4 ? nq6 : nq7, 8 * (j & 3), 8);
       mid();
       // one ds_add_u64 per byte: count | quality sum << 32 (spare cell: no word)
-      auto step = [&](const int j, uint32_t &w, uint32_t &acc) {
-        w = ((w << 2) | __builtin_amdgcn_perm(0u, c.xy[j >> 2], 0x0C0C0C00u | (j & 3))) & M;
+      // the word ending at byte j: codes of bytes j-K+1..j (oldest at bits 0-1)
+      // from the 96-bit stream np1:p0:p1 (byte i at bit 2(i + 16)), cut out by
+      // one v_alignbit at the cell's byte offset (x 8), then masked
+      auto step = [&](const int j, uint32_t &acc) {
+        const int sh = 2 * j + 29 - 2 * (K - 1);   // stream bit of byte j-K+1, less 3
+        const uint32_t win = sh < 32 ? __builtin_amdgcn_alignbit(c.p0, np1, sh)
+                           : sh < 64 ? __builtin_amdgcn_alignbit(c.p1, c.p0, sh - 32)
+                                     : c.p1 >> (sh - 64);
+        const uint32_t w = win & M;   // M: the cell byte-address mask
         const int jo = j - K;   // the byte leaving the quality window
         const uint32_t qold = jo >= 0 ? __builtin_amdgcn_ubfe(qw[jo >> 2], 8 * (jo & 3), 8)
                                       : __builtin_amdgcn_ubfe(jo + kLaneBytes < kLaneBytes - 4 ? nq6 : nq7, 8 * (jo & 3), 8);
         acc = acc + __builtin_amdgcn_ubfe(qw[j >> 2], 8 * (j & 3), 8) - qold;
-        // addr = E bit j ? w : SPARE (v_bfe_i32 + v_bfi_b32; left to itself the
+        // addr = E bit j ? w : SPARE (v_bfe_i32 + v_bitop3; left to itself the
         // compiler spends three instructions on it)
         uint32_t e, addr;
 #if HPGQ_CGR_ABL == 5   // timing probe only: no emission select
         addr = w;
         (void)e;
 #else
-        asm("v_bfe_i32 %0, %1, %2, 1" : "=v"(e) : "v"(E), "i"(j));
-        asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(addr) : "v"(e), "v"(w), "s"(SPARE));
+        e = (uint32_t)__builtin_amdgcn_sbfe((int)E, j, 1);
+        addr = __builtin_amdgcn_bitop3_b32(e, w, SPARE, 0xCA);   // e ? w : SPARE
 #endif
         const unsigned long long inc = ((unsigned long long)acc << 32) | 1ull;
 #if HPGQ_CGR_ABL == 6   // timing probe only: the adds replaced by one VALU op
@@ -464,26 +472,23 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
 #endif
       };
 #if HPGQ_CGR_CHAINS == 2
-      // two independent chains (bytes [0,16) and [16,32)) interleaved: the
-      // second's window and quality sum start from bytes 9..15 of this lane
+      // two independent quality chains (bytes [0,16) and [16,32)) interleaved:
+      // the second's sum starts from bytes 9..15 of this lane
       constexpr int kH = kLaneBytes / 2;
-      uint32_t w2 = 0, acc2 = 0;
-#pragma unroll
-      for (int j = kH - (K - 1); j < kH; ++j) w2 = ((w2 << 2) | __builtin_amdgcn_perm(0u, c.xy[j >> 2], 0x0C0C0C00u | (j & 3))) & M;
+      uint32_t acc2 = 0;
 #pragma unroll
       for (int j = kH - K; j < kH; ++j) acc2 += __builtin_amdgcn_ubfe(qw[j >> 2], 8 * (j & 3), 8);
 #pragma unroll
       for (int j = 0; j < kH; ++j) {
-        step(j, w, acc);
-        step(j + kH, w2, acc2);
+        step(j, acc);
+        step(j + kH, acc2);
       }
 #else
 #pragma unroll
-      for (int j = 0; j < kLaneBytes; ++j) step(j, w, acc);
+      for (int j = 0; j < kLaneBytes; ++j) step(j, acc);
 #endif
       // carry the last lane to the next tile's lane 0
-      pxy6 = __builtin_amdgcn_readlane(c.xy[kNdw - 2], 63);
-      pxy7 = __builtin_amdgcn_readlane(c.xy[kNdw - 1], 63);
+      pp1 = __builtin_amdgcn_readlane(c.p1, 63);
       pq6 = __builtin_amdgcn_readlane(qw[kNdw - 2], 63);
       pq7 = __builtin_amdgcn_readlane(qw[kNdw - 1], 63);
       pv = __builtin_amdgcn_readlane(c.v, 63);
@@ -589,13 +594,13 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
     if (!v) continue;
     A.scratch[i] = 0ull;
     if (exact) continue;
-    // code bits 2a / 2a+1 = x / y of the base `a` steps back; the newest is
-    // the MSB of co_x / co_y
+    // code bits 2b / 2b+1 = x / y of the base K-1-b steps back (the oldest at
+    // b = 0); the newest is the MSB of co_x / co_y, so bit b of co_x is x of b
     uint32_t cx = 0, cy = 0;
 #pragma unroll
-    for (int a = 0; a < K; ++a) {
-      cx |= ((uint32_t)(i >> (2 * a)) & 1u) << (K - 1 - a);
-      cy |= ((uint32_t)(i >> (2 * a + 1)) & 1u) << (K - 1 - a);
+    for (int b = 0; b < K; ++b) {
+      cx |= ((uint32_t)(i >> (2 * b)) & 1u) << b;
+      cy |= ((uint32_t)(i >> (2 * b + 1)) & 1u) << b;
     }
     const uint32_t cn = (uint32_t)v, q = (uint32_t)(v >> 32);
     const uint32_t cell = (cx << K) | cy;
