@@ -393,10 +393,10 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
       // flags: unsupported bytes
       if (__ballot(c.bad != 0u || (qor & 0x80808080u) != 0u)) risky = true;
       // runs: a 16-byte chunk without a Z on an axis, or a long run entering the tile
-      const uint32_t zand = c.zlo & c.zhi;
-      const bool zfree = !(zand & 0x01010101u) || !(zand & 0x02020202u) ||
-                         !(c.zlo & 0x01010101u) || !(c.zlo & 0x02020202u) ||
-                         !(c.zhi & 0x01010101u) || !(c.zhi & 0x02020202u);
+      // (zlo: x/y Z bits per byte offset over bytes 0..15, zhi over 16..31;
+      // gathered to 4 bits: the chunk-and-axis pairs that hold a Z)
+      const uint32_t zu = c.zlo | (c.zhi << 2);
+      const bool zfree = ((zu | (zu >> 8) | (zu >> 16) | (zu >> 24)) & 0xFu) != 0xFu;
       if (__builtin_expect(__ballot(zfree) != 0ull || einx > 16 || einy > 16, 0)) {
         if (!eknown) {
           einx = run_before<0>(A, b0, t, kRun);
@@ -433,9 +433,11 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
       }
       // the quality sum at the previous lane's last byte
       uint32_t acc = 0;
-#pragma unroll
-      for (int j = kLaneBytes - K; j < kLaneBytes; ++j)
-        acc += __builtin_amdgcn_ubfe(j < kLaneBytes - 4 ? nq6 : nq7, 8 * (j & 3), 8);
+      // (v_sad_u8 sums the previous lane's last K quality bytes, 4 per op)
+      if (K > 4)
+        acc = __builtin_amdgcn_sad_u8(nq7, 0u, __builtin_amdgcn_sad_u8(nq6 & (0xFFFFFFFFu << (8 * (8 - K))), 0u, 0u));
+      else
+        acc = __builtin_amdgcn_sad_u8(nq7 & (0xFFFFFFFFu << (8 * (4 - K))), 0u, 0u);
       mid();
       // one ds_add_u64 per byte: count | quality sum << 32 (spare cell: no word)
       // the word ending at byte j: codes of bytes j-K+1..j (oldest at bits 0-1)
