@@ -80,11 +80,10 @@ constexpr uint32_t GATE_EXACT = 1;   // the exact kernels must run
 
 // byte & 7 -> per-byte LUTs (v_perm_b32, codes A=1 C=3 T=4 N=6 G=7)
 constexpr uint32_t kCdLo = 0x00000100u;   // code = x | y << 1: A 1, C 0
-constexpr uint32_t kCdHi = 0x02000003u;   //                    T 3, G 2
+constexpr uint32_t kCdHi = 0x02030003u;   //                    T 3, G 2, N 3 (N emits no word;
+                                          // as 3 it has no Z bit in ~code below)
 constexpr uint32_t kV1Lo = 0x01000100u;   // 1 for A/C/G/T, 0 for N
 constexpr uint32_t kV1Hi = 0x01000001u;
-constexpr uint32_t kZLo = 0x03000200u;    // bit0: a Z move on x (C/G), bit1: on y (A/C)
-constexpr uint32_t kZHi = 0x01000000u;
 
 struct SArgs {
   const char *seq, *qual;
@@ -148,9 +147,9 @@ __device__ __forceinline__ Cls classify(const uint32_t s[kNdw]) {
     bad = __builtin_amdgcn_bitop3_b32(bad, s[d], __builtin_amdgcn_perm(hpgq::cgr::kExHi, hpgq::cgr::kExLo, code), 0xF6);
     c.cd[d] = __builtin_amdgcn_perm(kCdHi, kCdLo, code);
     g[d] = __builtin_amdgcn_udot4(c.cd[d], 0x40100401u, 0u, false);   // 4 codes -> 8 bits
-    const uint32_t z = __builtin_amdgcn_perm(kZHi, kZLo, code);
-    if (d < 4) zl |= z;
-    if (d >= kNdw - 4) zh |= z;
+    // Z bits: a Z move on x is x = 0 (C/G), on y is y = 0 (A/C): ~code & 3
+    if (d < 4) zl = __builtin_amdgcn_bitop3_b32(zl, c.cd[d], 0x03030303u, 0xF2);   // zl | (~cd & 3s)
+    if (d >= kNdw - 4) zh = __builtin_amdgcn_bitop3_b32(zh, c.cd[d], 0x03030303u, 0xF2);
     // the V bit of byte j to bit j: byte weights 1,2,4,8 (<< 4 for odd dwords) by v_dot4
     const uint32_t v1 = __builtin_amdgcn_perm(kV1Hi, kV1Lo, code);
     vp[d >> 1] = (d & 1) ? __builtin_amdgcn_udot4(v1, 0x80402010u, vp[d >> 1], false)
