@@ -123,6 +123,10 @@ __global__ void __launch_bounds__(256) span_first_kernel(SArgs A) {
   for (int64_t s = s0; s <= s1 && s < ns; ++s) A.span_first[s] = (int32_t)r;
 }
 
+__device__ __forceinline__ uint32_t dpp_ror1(uint32_t v) {   // lane l <- lane l-1, lane 0 <- lane 63
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x13C, 0xF, 0xF, false);
+}
+
 __device__ __forceinline__ uint32_t dpp_shr1(uint32_t old, uint32_t v) {   // lane l <- lane l-1
   return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x138, 0xF, 0xF, false);
 }
@@ -334,7 +338,9 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
   // span entry and taken over when the span's last tile is scattered.
   if (gw < ns) {
     int64_t s = gw;
-    uint32_t pp1, pq6, pq7, pv, pS;   // the previous lane's packed codes 16..31, last quality dwords, V and starts
+    // lane 0 of each: the previous tile's last lane (packed codes 16..31, last
+    // quality dwords, V and starts), the "old" operand of wave_shr:1
+    uint32_t pp1, pq6, pq7, pv, pS;
     // the run open at the tile start per axis: exact when eknown, else at
     // most 15 (the last 16 bytes hold a Z on both axes) and walked back for
     // only when a tile needs the exact scan
@@ -415,20 +421,14 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
       // emission: bytes [i-K+1, i] all A/C/G/T and no read start in (i-K+1, i]
       uint32_t E;
       {
-        // 64-bit frame: the previous lane's bytes just below bit 32, this lane's from bit 32
-        const uint64_t V = ((uint64_t)c.v << 32) | ((uint64_t)nv << (32 - kLaneBytes));
-        const uint64_t W = V & ~(((uint64_t)so << 32) | ((uint64_t)nS << (32 - kLaneBytes)));
-        uint64_t R = W;
-        int have = 1;
+        // 64-bit frames, high word = this lane's bytes, low word = the
+        // previous lane's: V (A/C/G/T) and W = V without read starts.  E bit j
+        // = AND over a < K-1 of (W << a) and (V << (K-1)), high words only:
+        // hi(X << a) = v_alignbit(Xh, Xl, 32 - a)
+        const uint32_t wh = c.v & ~so, wl = nv & ~nS;
+        E = K == 1 ? c.v : wh & __builtin_amdgcn_alignbit(c.v, nv, 32 - (K - 1));
 #pragma unroll
-        for (int step = 0; step < 4; ++step) {
-          if (have < K - 1) {
-            const int sh = have < K - 1 - have ? have : K - 1 - have;
-            R &= R << sh;
-            have += sh;
-          }
-        }
-        E = (uint32_t)((K == 1 ? V : R & (V << (K - 1))) >> 32);
+        for (int a = 1; a < K - 1; ++a) E &= __builtin_amdgcn_alignbit(wh, wl, 32 - a);
       }
       // the quality sum at the previous lane's last byte
       uint32_t acc = 0;
@@ -489,11 +489,13 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
       for (int j = 0; j < kLaneBytes; ++j) step(j, acc);
 #endif
       // carry the last lane to the next tile's lane 0
-      pp1 = __builtin_amdgcn_readlane(c.p1, 63);
-      pq6 = __builtin_amdgcn_readlane(qw[kNdw - 2], 63);
-      pq7 = __builtin_amdgcn_readlane(qw[kNdw - 1], 63);
-      pv = __builtin_amdgcn_readlane(c.v, 63);
-      pS = __builtin_amdgcn_readlane(so, 63);
+      // (rotated by one lane: lane 0 holds lane 63's, the "old" operand of
+      // the next tile's wave_shr:1)
+      pp1 = dpp_ror1(c.p1);
+      pq6 = dpp_ror1(qw[kNdw - 2]);
+      pq7 = dpp_ror1(qw[kNdw - 1]);
+      pv = dpp_ror1(c.v);
+      pS = dpp_ror1(so);
     };
     int32_t tA = a0 + (int32_t)(s << kSpanLog), tB;
     int32_t eA = (int32_t)min((int64_t)tA + kSpan, (int64_t)b1), eB;
