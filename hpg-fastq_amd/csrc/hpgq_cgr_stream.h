@@ -293,14 +293,16 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
   static_assert(K >= 1 && K <= kMaxK, "LDS table");
   constexpr int cells = 1 << (2 * K);
   constexpr uint32_t M = (uint32_t)(cells - 1) << 3;   // cell byte address mask
-  constexpr uint32_t SPARE = (uint32_t)cells << 3;      // the spare cell
+  constexpr uint32_t SPARE = (uint32_t)cells << 3;      // the spare cells (one per lane: bytes
+                                                        // that end no word do not collide)
   constexpr uint32_t kRun = 48 - K;
-  __shared__ unsigned long long tab[cells + 1];
+  __shared__ unsigned long long tab[cells + 64];
   __shared__ uint32_t scb[kWaves * 3 * 64];   // per wave: two start bitmaps (this tile, next tile) + context
   __shared__ uint32_t last;
-  for (int i = threadIdx.x; i < cells + 1; i += kWG) tab[i] = 0ull;
+  for (int i = threadIdx.x; i < cells + 64; i += kWG) tab[i] = 0ull;
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: spans, tiles and buffer descriptors stay scalar
+  const uint32_t spare = SPARE + 8u * (uint32_t)lane;
   uint32_t *sc = scb + 192 * wid;
   sc[lane] = 0u;
   sc[64 + lane] = 0u;
@@ -452,7 +454,7 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
         const uint32_t qold = jo >= 0 ? __builtin_amdgcn_ubfe(qw[jo >> 2], 8 * (jo & 3), 8)
                                       : __builtin_amdgcn_ubfe(jo + kLaneBytes < kLaneBytes - 4 ? nq6 : nq7, 8 * (jo & 3), 8);
         acc = acc + __builtin_amdgcn_ubfe(qw[j >> 2], 8 * (j & 3), 8) - qold;
-        // addr = E bit j ? w : SPARE (v_bfe_i32 + v_bitop3; left to itself the
+        // addr = E bit j ? w : spare (v_bfe_i32 + v_bitop3; left to itself the
         // compiler spends three instructions on it)
         uint32_t e, addr;
 #if HPGQ_CGR_ABL == 5   // timing probe only: no emission select
@@ -460,7 +462,7 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
         (void)e;
 #else
         e = (uint32_t)__builtin_amdgcn_sbfe((int)E, j, 1);
-        addr = __builtin_amdgcn_bitop3_b32(e, w, SPARE, 0xCA);   // e ? w : SPARE
+        addr = __builtin_amdgcn_bitop3_b32(e, w, spare, 0xCA);   // e ? w : spare
 #endif
         const unsigned long long inc = ((unsigned long long)acc << 32) | 1ull;
 #if HPGQ_CGR_ABL == 6   // timing probe only: the adds replaced by one VALU op
