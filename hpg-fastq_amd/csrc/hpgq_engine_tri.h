@@ -391,13 +391,26 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
   // block prologue: lane j describes read (pair) r0 + j in read table `tb`;
   // lanes >= nr get length 0, so whatever gathers them contributes nothing.
   // Returns this lane's lengths (the epilogue needs them).
-  auto load_block = [&](int64_t blk, int tb, uint32_t (&len)[NM], uint32_t &tw, uint32_t &nraw) {
+  // a block's read offsets (lane j: read r0 + j), fetched one block ahead of
+  // its prologue so the prologue does not wait for them
+  auto fetch_idx = [&](int64_t blk, int32_t (&ia)[NM], int32_t (&ie)[NM]) {
     const int64_t r0 = blk * kBlock;
     const int nr = (int)min((int64_t)kBlock, A.num_reads - r0);
     const int l = min(lane, nr - 1);
 #pragma unroll
     for (int m = 0; m < NM; ++m) {
-      int a = A.idx[m][r0 + l], e = A.idx[m][r0 + l + 1];
+      ia[m] = A.idx[m][r0 + l];
+      ie[m] = A.idx[m][r0 + l + 1];
+    }
+  };
+  auto load_block = [&](int64_t blk, int tb, uint32_t (&len)[NM], uint32_t &tw, uint32_t &nraw,
+                        const int32_t (&ia)[NM], const int32_t (&ie)[NM]) {
+    const int64_t r0 = blk * kBlock;
+    const int nr = (int)min((int64_t)kBlock, A.num_reads - r0);
+    const int l = min(lane, nr - 1);
+#pragma unroll
+    for (int m = 0; m < NM; ++m) {
+      int a = ia[m], e = ie[m];
       nraw = lane < nr ? (uint32_t)(e - a) : 0u;
       if (EDIT) {   // trim here, then describe the trimmed window
         tw = lane < nr ? trim_word(*A.cold, rq[m], bq[m] + a, e - a) : 0u;
@@ -533,8 +546,11 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
   uint32_t tw = 0, twn = 0, nraw = 0, nrawn = 0;   // EDIT: trim word, untrimmed length
   int tb = 0;   // read table of the current block
   int64_t blk = gw;
+  int32_t ia[NM], ie[NM];   // offsets of the block after the next one to be described
   if (blk < nblocks) {
-    load_block(blk, tb, len, tw, nraw);
+    fetch_idx(blk, ia, ie);
+    load_block(blk, tb, len, tw, nraw, ia, ie);
+    fetch_idx(blk + nw < nblocks ? blk + nw : blk, ia, ie);
     const int nr0 = (int)min((int64_t)kBlock, A.num_reads - blk * kBlock);
     load_group(0, tb, (nr0 + kSegs - 1) / kSegs, 0, 0);
   }
@@ -551,7 +567,10 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
     // the next block's prologue (offsets and, for edit, the trims, which read
     // the quality ends): at the start of this block's last group pair, so the
     // lines the trims touch are still in L2 when the next block streams them
-    if (!HPGQ_TRI_LATE_PROLOGUE) load_block(nblk, tb ^ 1, lenn, twn, nrawn);
+    if (!HPGQ_TRI_LATE_PROLOGUE) {
+      load_block(nblk, tb ^ 1, lenn, twn, nrawn, ia, ie);
+      fetch_idx(nblk + nw < nblocks ? nblk + nw : nblk, ia, ie);
+    }
     if (stats && since_flush > kByteEvery - kBlock / kSegs) {   // keep every byte <= 255
 #pragma unroll
       for (int m = 0; m < NM; ++m) acc[m].flush(pos_acc(m), lmax, p0);
@@ -580,7 +599,10 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
         else load_group(0, tb ^ 1, nnt, 0, slot);
       };
       for (int g = 0; g < ngroups; g += 2) {
-        if (HPGQ_TRI_LATE_PROLOGUE && m == NM - 1 && g + 2 >= ngroups) load_block(nblk, tb ^ 1, lenn, twn, nrawn);
+        if (HPGQ_TRI_LATE_PROLOGUE && m == NM - 1 && g + 2 >= ngroups) {
+          load_block(nblk, tb ^ 1, lenn, twn, nrawn, ia, ie);
+          fetch_idx(nblk + nw < nblocks ? nblk + nw : nblk, ia, ie);
+        }
         load_group(m, tb, nt, g + 1, 1);
         process_group(g, 0);
         if (g + 2 < ngroups) load_group(m, tb, nt, g + 2, 0);
