@@ -35,21 +35,24 @@
 // never violate this; a batch that does (poly-A/T/G runs, lowercase, IUPAC)
 // sets the gate and the exact kernels redo the whole call.
 //
-// Layout: the bytes [idx[0], idx[n]) are cut into spans of kSpan bytes; a
-// wave takes a span as tiles of 2 KB, a lane 32 contiguous bytes of seq and
-// of quality per tile (16-byte loads, the next tile's in flight while this
-// one is counted).  The K-1 bytes of context come from the neighbouring lane
-// by DPP (lane 0: the last lane of the previous tile, or a broadcast load at
-// the span start).  Read starts inside a tile are scattered into a per-wave
-// LDS bitmap from the read offsets the wave walks with a cursor.  Words go to
-// the workgroup's LDS table (u64 per cell: count | quality sum << 32, one
-// ds_add_u64 per byte; a byte that ends no word adds to a spare cell),
-// flushed to a global u64 scratch table; the last workgroup to finish moves
-// it into the reference layout (or discards it when the gate is set).  A run
-// of >= kRun (>= 41) D-moves covers a whole aligned 16-byte chunk with no Z
-// on that axis; a tile whose chunks all hold a Z on both axes can only hold
-// runs of <= 30, so only tiles with a Z-free chunk (or entered with a long
-// open run) are scanned exactly, lane by lane.
+// Layout: the bytes [idx[0], idx[n]) are cut into spans of kSpan bytes; wave
+// g takes spans g, g + W, ... (W waves in the grid) as one stream of 2 KB
+// tiles, a lane 32 contiguous bytes of seq and of quality per tile (16-byte
+// loads; the next tile -- across span boundaries too, with its span's
+// context and cursor -- in flight while this one is counted).  The K-1
+// bytes of context come from the neighbouring lane by DPP (lane 0: the last
+// lane of the previous tile, or a broadcast load at a span start).  The
+// lane's bytes become a packed 2-bit code stream (v_dot4), so a word's cell
+// is one v_alignbit and a mask.  Read starts inside a tile are scattered into
+// a per-wave LDS bitmap from the read offsets the wave walks with a cursor.
+// Words go to the workgroup's LDS table (u64 per cell: count | quality sum
+// << 32, one ds_add_u64 per byte; a byte that ends no word adds to its lane's
+// spare cell), flushed to a global u64 scratch table; the last workgroup to
+// finish moves it into the reference layout (or discards it when the gate is
+// set).  A run of >= kRun (>= 41) D-moves covers a whole aligned 16-byte
+// chunk with no Z on that axis; a tile whose chunks all hold a Z on both axes
+// can only hold runs of <= 30, so only tiles with a Z-free chunk (or entered
+// with a long open run) are scanned exactly, lane by lane.
 #pragma once
 
 namespace hpgq {
