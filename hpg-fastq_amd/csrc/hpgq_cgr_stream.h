@@ -64,7 +64,7 @@ constexpr int kWG = kWaves * 64;
 #ifndef HPGQ_CGR_LANE_BYTES
 #define HPGQ_CGR_LANE_BYTES 32
 #endif
-constexpr int kLaneBytes = HPGQ_CGR_LANE_BYTES;   // 16 or 32
+constexpr int kLaneBytes = HPGQ_CGR_LANE_BYTES;   // 32 (the packed code stream assumes it)
 constexpr int kNdw = kLaneBytes / 4;
 constexpr int kTile = 64 * kLaneBytes;       // bytes per wave tile (2 KB)
 #ifndef HPGQ_CGR_SPAN_LOG
