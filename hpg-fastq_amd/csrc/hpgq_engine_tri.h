@@ -451,12 +451,17 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
   TriPending<NW> grp[2][kU];
   // issue group g (kU steps) of mate m; steps past the block end gather
   // lane 63 (length 0), so they add nothing
+#ifndef HPGQ_TRI_PRIO
+#define HPGQ_TRI_PRIO 0   // timing probe: raised wave priority while a group's loads issue
+#endif
   auto load_group = [&](int m, int tb, int nt, int g, int slot) {
+    if (HPGQ_TRI_PRIO) __builtin_amdgcn_s_setprio(HPGQ_TRI_PRIO);
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       const int t = g * kU + u;
       gather(m, tb, t < nt ? min(kSegs * t + seg, 63) : 63, grp[slot][u]);
     }
+    if (HPGQ_TRI_PRIO) __builtin_amdgcn_s_setprio(0);
   };
 
   // one triple: per-lane partial (raw quality | G+C << 18); adds (SUB = false)
