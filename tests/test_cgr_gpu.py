@@ -107,6 +107,24 @@ def test_cgr_large_batch_k7(path):
     assert log == [0 if path == H.CGR_PATH_AUTO else 1]
 
 
+@pytest.mark.parametrize("k", [4, 7])
+def test_cgr_stream_many_spans_per_wave(k):
+    """150 MB in one call: more 16 KB spans than the grid has waves, so every
+    wave walks a tile stream across span boundaries (next span's context,
+    cursor and first tile fetched while the last tile is counted).  Property
+    check against the exact GPU kernels (validated against the oracle above)
+    at a size the CPU oracle would take minutes on."""
+    reads = O.synth(600_000, seed=11, L=250)
+    log = []
+    ts, tq, wc, _ = gpu_cgr(k, [reads], exact_log=log)
+    assert log == [0]   # the stream pass ran
+    es, eq, ew, rep = gpu_cgr(k, [reads], path=H.CGR_PATH_EXACT)
+    assert rep == 0
+    assert wc == ew and wc > 0
+    np.testing.assert_array_equal(ts, es)
+    np.testing.assert_array_equal(tq, eq)
+
+
 def _run_batch(rng, k, run_len, n=900, split=False):
     """Random reads with D-move runs of run_len on x (A/T), y (G/T) or both
     (T), N sprinkled inside the runs (N does not move f), some runs split

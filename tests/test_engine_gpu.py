@@ -315,3 +315,23 @@ def test_rccl_allreduce_single_rank():
         got = e.counters()
     _, _, want = O.run(p, reads)
     np.testing.assert_array_equal(got, want)
+
+
+# ---- many blocks per wave: the persistent grid's block pipeline ------------
+# (next block's prologue and offsets fetched ahead; the small cases above give
+# each wave at most one block)
+@pytest.mark.parametrize("case", ["c2", "c4", "c3"])
+def test_many_blocks_per_wave(case, geo_choice):
+    n = 1_200_000 if case != "c3" else 600_000   # > 4096 waves x 48 reads x 3
+    if case == "c4":
+        p = H.edit_params(lmax=150, stats=True, left_length=10, left_quality_range="20,",
+                          right_length=30, right_quality_range="20,")
+    else:
+        p = H.stats_params(lmax=150, read_quality_range="20,", read_length_range="50,")
+    if case == "c3":
+        p.paired = 1
+        r1 = O.synth(n, seed=21, L=150, trunc_pct=5, mate=0)
+        r2 = O.synth(n, seed=21, L=150, trunc_pct=5, mate=1)
+        assert_same(p, r1, r2)
+    else:
+        assert_same(p, O.synth(n, seed=20, L=150, trunc_pct=5, n_per_1024=2))
