@@ -29,6 +29,7 @@ struct hpgq_ctx {
   bool tri = false;               // segmented FAST kernel (lmax <= 160)
   bool hex = false;               // ... in its 16-byte-lane geometry (lmax <= 156)
   bool tri_edit = false;          // ... trimming in its block prologue (single-end edit)
+  bool tri_x = false;             // ... with the N / out-of-range read filters
   int grid = 0;
   uint64_t *d_slab = nullptr;     // [grid][nm * clen] per-workgroup partials
   hpgq::ColdParams *d_cold = nullptr;
@@ -152,7 +153,15 @@ static const void *tri_for(int mw, bool un, int nm, bool edit) {
 }
 
 // tri: the segmented kernel (hpgq_engine_tri.h), hex selects its 16-byte-lane geometry
-static const void *kernel_for(int nm, int nch, bool gen, bool tri, bool hex, bool edit, char *name, size_t cap) {
+static const void *kernel_for(int nm, int nch, bool gen, bool tri, bool hex, bool edit, bool tx, char *name,
+                              size_t cap) {
+  if (tri && tx) {   // spill-free occupancy per variant, as below
+    using hpgq::engine_tri_x_kernel;
+    const int mw = hex ? (nm == 2 ? 3 : 4) : (nm == 2 ? 3 : 5);
+    std::snprintf(name, cap, "hpgq::engine_tri_x_kernel<%d, %d, %d>", mw, nm, hex ? 4 : 2);
+    if (hex) return nm == 2 ? (const void *)engine_tri_x_kernel<3, 2, 4> : (const void *)engine_tri_x_kernel<4, 1, 4>;
+    return nm == 2 ? (const void *)engine_tri_x_kernel<3, 2, 2> : (const void *)engine_tri_x_kernel<5, 1, 2>;
+  }
   if (tri) {
     const char *w = std::getenv("HPGQ_TRI_WAVES");      // occupancy experiment knob
     const char *u = std::getenv("HPGQ_TRI_UNALIGNED");  // load-scheme experiment knob (tri only)
@@ -286,11 +295,13 @@ int hpgq_open(hpgq_ctx_t **out, int device, const hpgq_params_t *p) {
   {
     const char *force = std::getenv("HPGQ_KERNEL");   // "single" forces the one-read kernel
     const int fl = engine_flags(*p);
-    const bool filter_extras = fl & (hpgq::F_NEED_N | hpgq::F_NEED_OOR | hpgq::F_NEED_LR);
+    const bool lr = fl & hpgq::F_NEED_LR;                          // window filters: engine_kernel
+    const bool nx = fl & (hpgq::F_NEED_N | hpgq::F_NEED_OOR);     // N / out-of-range: engine_tri_x_kernel
     const bool edit = fl & hpgq::F_EDIT;
-    c->tri = !filter_extras && (!edit || c->nm == 1) && p->lmax <= hpgq::kTriPos &&
+    c->tri = !lr && !(nx && edit) && (!edit || c->nm == 1) && p->lmax <= hpgq::kTriPos &&
              !(force && std::strcmp(force, "single") == 0);
     c->tri_edit = c->tri && edit;
+    c->tri_x = c->tri && nx;
     const char *geo = std::getenv("HPGQ_TRI_GEO");   // "tri" forces the 8-byte-lane geometry
     c->hex = c->tri && p->lmax <= hpgq::kHexPos &&
              !(geo && std::strcmp(geo, "tri") == 0);
@@ -304,7 +315,7 @@ int hpgq_open(hpgq_ctx_t **out, int device, const hpgq_params_t *p) {
     // and mate two read tables (2 x 1 KB) + segment ends (256 B)
     const size_t mate_words = (size_t)6 * p->lmax + (((size_t)hlen + 1) & ~(size_t)1) + 2 * HPGQ_NUM_SCALARS;
     const size_t tri_lds = (size_t)c->nm * mate_words * 4 + 16 + 17 * 16 +   // + the byte-mask table
-                           (size_t)hpgq::kWaves * c->nm * (2 * 256 + 64) * 4;
+                           (size_t)hpgq::kWaves * c->nm * (2 * 256 + (c->tri_x ? 128 : 64)) * 4;
     if (tri_lds > c->lds_bytes) c->lds_bytes = tri_lds;
   }
   HPGQ_HIP_TRY(hipSetDevice(device));
@@ -315,7 +326,8 @@ int hpgq_open(hpgq_ctx_t **out, int device, const hpgq_params_t *p) {
   HPGQ_HIP_TRY(hipMemsetAsync(c->d_err, 0, sizeof(int32_t), c->stream));
   int cus = 0;
   HPGQ_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-  const void *kfn = kernel_for(c->nm, c->nch, c->gen, c->tri, c->hex, c->tri_edit, c->kname, sizeof(c->kname));
+  const void *kfn = kernel_for(c->nm, c->nch, c->gen, c->tri, c->hex, c->tri_edit, c->tri_x, c->kname,
+                               sizeof(c->kname));
   c->kfn = kfn;
   if (c->lds_bytes > 64 * 1024)
     HPGQ_HIP_TRY(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize,

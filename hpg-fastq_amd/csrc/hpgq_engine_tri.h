@@ -310,9 +310,13 @@ struct MateTag {
 // EDIT (NM = 1): the block prologue trims each read (trim_word, written to
 // A.trim when the caller wants it) and describes it by its window [ts, n - te)
 // (offset + ts, length n - ts - te): stats and filter see the trimmed read.
-template <int MINW, bool UNAL, int NM, bool EDIT, int NW>
-__global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
+// NX: the filter also counts N bases and out-of-range qualities per read
+// (max_N, max_out_of_quality; src/filter_fastq.c): a second per-step scan
+// of (N | out-of-range << 16), its segment ends in a second LDS list
+template <int MINW, bool UNAL, int NM, bool EDIT, int NW, bool NX>
+__device__ __forceinline__ void tri_body(const EngineArgs &A) {
   static_assert(!EDIT || NM == 1, "edit on the three-read kernel is single-end");
+  static_assert(!(NX && EDIT), "the N / out-of-range filter variant does not edit");
   using G = Geo<NW>;
   constexpr int kSegs = G::kSegs, kSegW = G::kSegW, kBlock = G::kBlock, kU = G::kU;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -343,11 +347,13 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
   auto sc = [&](int m) {
     return reinterpret_cast<unsigned long long *>(base + m * mate_words + 6 * lmax + hist_words);
   };
-  constexpr int kWaveWords = NM * (2 * 256 + 64);
+  constexpr int kMateWaveWords = 2 * 256 + (NX ? 128 : 64);
+  constexpr int kWaveWords = NM * kMateWaveWords;
   const int tab_words = (NM * mate_words + 3) & ~3;   // 16 B aligned (host: + 16 B)
   uint32_t *wtab = base + tab_words + wave * kWaveWords;
-  auto tab = [&](int m, int tb) { return wtab + m * (2 * 256 + 64) + tb * 256; };
-  auto wends = [&](int m) { return wtab + m * (2 * 256 + 64) + 2 * 256; };
+  auto tab = [&](int m, int tb) { return wtab + m * kMateWaveWords + tb * 256; };
+  auto wends = [&](int m) { return wtab + m * kMateWaveWords + 2 * 256; };
+  auto wends2 = [&](int m) { return wtab + m * kMateWaveWords + 2 * 256 + 64; };   // NX only
   // byte masks by valid-byte count c = clamp(n - p0, 0, 4 NW): mtab[c][w]
   // (one LDS read per step instead of a clamp and a 64-bit shift per word)
   uint32_t *mtab = base + tab_words + kWaves * kWaveWords;   // 16 B aligned
@@ -466,7 +472,7 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
 
   // one triple: per-lane partial (raw quality | G+C << 18); adds (SUB = false)
   // or removes (SUB = true) the lane's positions from mate m's counters
-  auto account = [&](auto mtag, const TriPending<NW> &pd, bool count, auto sub_tag) -> uint32_t {
+  auto account = [&](auto mtag, const TriPending<NW> &pd, bool count, auto sub_tag, uint32_t &x2) -> uint32_t {
     constexpr int m = decltype(mtag)::value;
     constexpr bool SUB = decltype(sub_tag)::value;
     uint32_t sw[NW], qw[NW];
@@ -544,6 +550,27 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
       gc += (uint32_t)__builtin_popcount(cg[w]);
       qs = __builtin_amdgcn_sad_u8(qm[w], 0u, qs);
     }
+    if (NX && !SUB) {   // N | out-of-range << 16 over the lane's valid bytes (as engine_kernel)
+      const ColdParams &C = *A.cold;
+      uint32_t nn = 0, oo = 0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        const uint32_t m80 = mk[w] & 0x80808080u;
+        if (A.flags & F_NEED_N) nn += (uint32_t)__builtin_popcount(zero_bytes(sw[w] ^ 0x4E4E4E4Eu) & m80);
+        if (A.flags & F_NEED_OOR) {
+          uint32_t b;
+          if (A.flags & F_OOR_ALL) {
+            b = 0x80808080u;
+          } else {
+            b = 0;
+            if (!(A.flags & F_OOR_LO_NONE)) b |= ~ge_bytes(qw[w], C.oor_lo4) & 0x80808080u;
+            if (!(A.flags & F_OOR_HI_NONE)) b |= ge_bytes(qw[w], C.oor_hi4);
+          }
+          oo += (uint32_t)__builtin_popcount(b & m80);
+        }
+      }
+      x2 = nn | (oo << 16);
+    }
     return qs + (gc << 18);
   };
 
@@ -592,10 +619,15 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
         for (int u = 0; u < kU; ++u) {
           const int t = g * kU + u;
           // every read is added; failed ones are taken out in the block epilogue
-          const uint32_t x = account(MateTag<m>{}, grp[slot][u], stats, AddTag{});
+          uint32_t x2 = 0;
+          const uint32_t x = account(MateTag<m>{}, grp[slot][u], stats, AddTag{}, x2);
           const uint32_t P = wave_scan(x);
           // segment ends (the last lane of each segment) -> wends[kSegs t + seg], no wait needed
           if (ls == kSegW - 1 && seg < kSegs && t < nt) wends(m)[kSegs * t + seg] = P;
+          if (NX) {
+            const uint32_t P2 = wave_scan(x2);
+            if (ls == kSegW - 1 && seg < kSegs && t < nt) wends2(m)[kSegs * t + seg] = P2;
+          }
         }
       };
       // after this mate's last group: the next mate's first group, or the next block's
@@ -639,6 +671,14 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
       const int sraw = (int)(r1[m] & 0x3FFFFu);
       if (filter)
         pass = pass && n >= A.min_len && n <= A.max_len && lo_r * n <= sraw && sraw <= hi_r * n;
+      if (NX && filter) {
+        const uint32_t e2 = valid ? wends2(m)[lane] : 0u;
+        const uint32_t p2 = __builtin_amdgcn_mov_dpp(e2, 0x138, 0xF, 0xF, true);   // lane j-1
+        const uint32_t r2 = e2 - (((not_seg_first >> lane) & 1u) ? p2 : 0u);
+        const ColdParams &C = *A.cold;
+        if ((A.flags & F_NEED_N) && (int)(r2 & 0xFFFFu) > C.max_n) pass = false;
+        if ((A.flags & F_NEED_OOR) && (int)(r2 >> 16) > C.max_oor) pass = false;
+      }
     }
     if (valid && A.mask) A.mask[r0 + lane] = (uint8_t)pass;
     const uint64_t failed = __ballot(valid && !pass);
@@ -691,14 +731,15 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
         nsub = max(nsub, n);
         if (c == seg) mycnt = n;
       }
+      uint32_t sub_x2 = 0;   // (unused: failed reads leave the counters only)
       for (int k = 0; k < nsub; ++k) {
         const int src = seg < kSegs && k < mycnt ? (int)flist[min(k * kSegs + seg, 63)] : 63;
         TriPending<NW> pd;
         gather(0, tb, src, pd);
-        (void)account(MateTag<0>{}, pd, true, SubTag{});
+        (void)account(MateTag<0>{}, pd, true, SubTag{}, sub_x2);
         if (NM == 2) {
           gather(NM - 1, tb, src, pd);
-          (void)account(MateTag<NM - 1>{}, pd, true, SubTag{});
+          (void)account(MateTag<NM - 1>{}, pd, true, SubTag{}, sub_x2);
         }
       }
     }
@@ -753,6 +794,18 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
     for (int i = tid; i < hlen; i += kWG) rm[HPGQ_NUM_SCALARS + i] += h[i];
     for (int i = tid; i < 6 * lmax; i += kWG) rm[off_pos + i] += pa[i];
   }
+}
+
+
+template <int MINW, bool UNAL, int NM, bool EDIT, int NW>
+__global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
+  tri_body<MINW, UNAL, NM, EDIT, NW, false>(A);
+}
+
+// the segmented kernel with the N / out-of-range read filters (no edit)
+template <int MINW, int NM, int NW>
+__global__ void __launch_bounds__(kWG, MINW) engine_tri_x_kernel(EngineArgs A) {
+  tri_body<MINW, false, NM, false, NW, true>(A);
 }
 
 }  // namespace hpgq

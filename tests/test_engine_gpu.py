@@ -335,3 +335,15 @@ def test_many_blocks_per_wave(case, geo_choice):
         assert_same(p, r1, r2)
     else:
         assert_same(p, O.synth(n, seed=20, L=150, trunc_pct=5, n_per_1024=2))
+
+
+@pytest.mark.parametrize("name", ["max_n", "oor_only"])
+def test_n_oor_filters_route_to_segmented_kernel(name, geo_choice):
+    """max_N / max_out_of_quality run on the segmented kernel's filter variant
+    (a second per-step scan of N | out-of-range), bit-identical to the oracle,
+    at a size that gives every wave several blocks."""
+    p = H.stats_params(lmax=150, **STATS_CASES[name])
+    with H.Engine(p) as e:
+        assert "engine_tri_x_kernel" in e.kernel_name
+        assert ("4>" in e.kernel_name) == (geo_choice == "auto")
+    assert_same(p, O.synth(600_000, seed=23, L=150, trunc_pct=5, n_per_1024=12))

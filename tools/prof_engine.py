@@ -1,7 +1,7 @@
 """Profiling driver: the C2 engine kernel on one resident 10M-read batch.
 
 Run under rocprofv3 (kernel trace or --pmc passes); no timing of its own.
-  python tools/prof_engine.py [--reads N] [--iters K] [--mode c2|stats|edit|edit0|editL|editR|pe|cgr]
+  python tools/prof_engine.py [--reads N] [--iters K] [--mode c2|stats|edit|edit0|editL|editR|maxn|pe|cgr]
 """
 import argparse
 import ctypes as C
@@ -52,6 +52,9 @@ elif args.mode == "stats":
 elif args.mode == "edit":
     p = H.edit_params(lmax=L, stats=True, left_length=10, left_quality_range="20,",
                       right_length=30, right_quality_range="20,")
+elif args.mode == "maxn":   # C2 plus max_N / max_out_of_quality (the N / out-of-range filter variant)
+    p = H.stats_params(lmax=L, read_quality_range="20,", read_length_range="50,", max_N=2,
+                       max_out_of_quality=20)
 elif args.mode in ("edit0", "editL", "editR"):   # timing probes: the edit kernel, fewer trims
     p = H.edit_params(lmax=L, stats=True, left_length=10 if args.mode == "editL" else 0,
                       left_quality_range="20,", right_length=30 if args.mode == "editR" else 0,
