@@ -138,11 +138,19 @@ def cpu_baseline(args, params):
         el = time.perf_counter() - t0
         if el >= args.cpu_seconds:
             break
+    # one pass on one thread beside the threaded figure
+    nthreads, threads = threads, 1
+    t1 = time.perf_counter()
+    assert run() == 0
+    el1 = time.perf_counter() - t1
+    threads = nthreads
     return {"value": round(done / el / 1e6, 3), "unit": CONFIGS[args.config]["unit"],
             "cores": threads, "kind": "port",
+            "value_1thread": round(n / el1 / 1e6, 3),
             "sample": f"{n} synthetic {L} bp {'pairs' if mates == 2 else 'reads'} (seed "
                       f"{args.seed}, same generator and options), {done // n} passes in "
-                      f"{el:.1f} s; {what} -O3 OpenMP, {threads} threads of {ncores} visible"}
+                      f"{el:.1f} s; {what} -O3 OpenMP, {threads} threads of {ncores} visible; "
+                      f"value_1thread: one pass on 1 thread ({el1:.1f} s)"}
 
 
 # ---- resident synthetic shard ----------------------------------------------
