@@ -72,6 +72,9 @@ constexpr int kTile = 64 * kLaneBytes;       // bytes per wave tile (2 KB)
 #endif
 constexpr int kSpanLog = HPGQ_CGR_SPAN_LOG;
 constexpr int kSpan = 1 << kSpanLog;         // bytes per span (16 KB, 8 tiles)
+#ifndef HPGQ_CGR_XCHG
+#define HPGQ_CGR_XCHG 0   // 1: read and clear by one exchange (measured ~1% slower)
+#endif
 #ifndef HPGQ_CGR_CHAINS
 #define HPGQ_CGR_CHAINS 1   // independent add chains per lane and tile (2: measured no faster)
 #endif
@@ -124,6 +127,18 @@ __global__ void __launch_bounds__(256) span_first_kernel(SArgs A) {
   const int64_t s0 = lo < 0 ? 0 : (lo >> kSpanLog) + 1;
   const int64_t s1 = r == A.num_reads ? ns - 1 : (hi >> kSpanLog);   // past the last start: the end sentinel
   for (int64_t s = s0; s <= s1 && s < ns; ++s) A.span_first[s] = (int32_t)r;
+}
+
+// a lane's word of a start bitmap, cleared for its next use in the same LDS op
+// (ds_wrxchg_rtn_b32: one LDS instruction instead of a read and a write)
+__device__ __forceinline__ uint32_t take_bits(uint32_t *p) {
+#if HPGQ_CGR_XCHG
+  return atomicExch(p, 0u);
+#else
+  const uint32_t v = *p;
+  *p = 0u;
+  return v;
+#endif
 }
 
 __device__ __forceinline__ uint32_t dpp_ror1(uint32_t v) {   // lane l <- lane l-1, lane 0 <- lane 63
@@ -519,7 +534,7 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
     }
     uint32_t sA[kNdw], qA[kNdw], sB[kNdw], qB[kNdw], soA, soB;
     scatter_starts(A, sc, r, iw, tA, tA + kTile, lane, tA + kTile >= eA, rn);
-    soA = sc[lane];
+    soA = take_bits(&sc[lane]);
     load32(rs, (uint32_t)(tA + kLaneBytes * lane), sA);
     load32(rq, (uint32_t)(tA + kLaneBytes * lane), qA);
     // count tile x while fetching tile y (straight-line: the loads are
@@ -549,10 +564,10 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
       const uint32_t oy = fin ? kPast : (uint32_t)(ty + kLaneBytes * lane);
       load32(rs, oy, sy);
       load32(rq, oy, qy);
-      scpx[lane] = 0u;
+      (void)scpx;   // (cleared when read: take_bits)
       tile(tx, ex, sx, qx, sox, [&] {
         scatter_starts(A, scpy, r, iw, ty, fin ? INT32_MIN : ty + kTile, lane, ty + kTile >= ey, rn);
-        soy = scpy[lane];
+        soy = take_bits(&scpy[lane]);
       });
       if (fin) return false;
       if (entering) {
