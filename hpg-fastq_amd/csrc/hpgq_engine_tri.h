@@ -331,6 +331,13 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   const int p0 = owner ? 4 * NW * ls : (1 << 26);   // first position of this lane (8*p0 fits int32)
   const uint32_t lane8 = 4u * NW * (uint32_t)ls;   // byte offset of this lane's window
   const bool stats = A.flags & F_STATS, filter = A.flags & F_FILTER;
+  // NX: the filter's extra limits, read once (not from *A.cold inside the loop,
+  // where each scalar reload would wait for the outstanding LDS operations too)
+  const uint32_t x_lo4 = NX ? (uint32_t)uni((int)A.cold->oor_lo4) : 0u;
+  const uint32_t x_hi4 = NX ? (uint32_t)uni((int)A.cold->oor_hi4) : 0u;
+  const int x_maxn = NX ? uni(A.cold->max_n) : 0, x_maxo = NX ? uni(A.cold->max_oor) : 0;
+  const bool x_n = NX && (A.flags & F_NEED_N), x_o = NX && (A.flags & F_NEED_OOR);
+  const bool x_all = A.flags & F_OOR_ALL, x_lonone = A.flags & F_OOR_LO_NONE, x_hinone = A.flags & F_OOR_HI_NONE;
   // raw-sum bounds: pass iff min_len <= n <= max_len and lo_r*n <= S <= hi_r*n
   const int lo_r = A.min_q + A.phred, hi_r = A.max_q + A.phred;
 
@@ -551,20 +558,19 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       qs = __builtin_amdgcn_sad_u8(qm[w], 0u, qs);
     }
     if (NX && !SUB) {   // N | out-of-range << 16 over the lane's valid bytes (as engine_kernel)
-      const ColdParams &C = *A.cold;
       uint32_t nn = 0, oo = 0;
 #pragma unroll
       for (int w = 0; w < NW; ++w) {
         const uint32_t m80 = mk[w] & 0x80808080u;
-        if (A.flags & F_NEED_N) nn += (uint32_t)__builtin_popcount(zero_bytes(sw[w] ^ 0x4E4E4E4Eu) & m80);
-        if (A.flags & F_NEED_OOR) {
+        if (x_n) nn += (uint32_t)__builtin_popcount(zero_bytes(sw[w] ^ 0x4E4E4E4Eu) & m80);
+        if (x_o) {
           uint32_t b;
-          if (A.flags & F_OOR_ALL) {
+          if (x_all) {
             b = 0x80808080u;
           } else {
             b = 0;
-            if (!(A.flags & F_OOR_LO_NONE)) b |= ~ge_bytes(qw[w], C.oor_lo4) & 0x80808080u;
-            if (!(A.flags & F_OOR_HI_NONE)) b |= ge_bytes(qw[w], C.oor_hi4);
+            if (!x_lonone) b |= ~ge_bytes(qw[w], x_lo4) & 0x80808080u;
+            if (!x_hinone) b |= ge_bytes(qw[w], x_hi4);
           }
           oo += (uint32_t)__builtin_popcount(b & m80);
         }
@@ -675,9 +681,8 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
         const uint32_t e2 = valid ? wends2(m)[lane] : 0u;
         const uint32_t p2 = __builtin_amdgcn_mov_dpp(e2, 0x138, 0xF, 0xF, true);   // lane j-1
         const uint32_t r2 = e2 - (((not_seg_first >> lane) & 1u) ? p2 : 0u);
-        const ColdParams &C = *A.cold;
-        if ((A.flags & F_NEED_N) && (int)(r2 & 0xFFFFu) > C.max_n) pass = false;
-        if ((A.flags & F_NEED_OOR) && (int)(r2 >> 16) > C.max_oor) pass = false;
+        if (x_n && (int)(r2 & 0xFFFFu) > x_maxn) pass = false;
+        if (x_o && (int)(r2 >> 16) > x_maxo) pass = false;
       }
     }
     if (valid && A.mask) A.mask[r0 + lane] = (uint8_t)pass;
