@@ -338,6 +338,12 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   const int x_maxn = NX ? uni(A.cold->max_n) : 0, x_maxo = NX ? uni(A.cold->max_oor) : 0;
   const bool x_n = NX && (A.flags & F_NEED_N), x_o = NX && (A.flags & F_NEED_OOR);
   const bool x_all = A.flags & F_OOR_ALL, x_lonone = A.flags & F_OOR_LO_NONE, x_hinone = A.flags & F_OOR_HI_NONE;
+#ifndef HPGQ_TRI_COLD_COPY
+#define HPGQ_TRI_COLD_COPY 1
+#endif
+  // EDIT: the trim bounds, read once (see NX above)
+  ColdParams cold{};
+  if (EDIT && HPGQ_TRI_COLD_COPY) cold = *A.cold;
   // raw-sum bounds: pass iff min_len <= n <= max_len and lo_r*n <= S <= hi_r*n
   const int lo_r = A.min_q + A.phred, hi_r = A.max_q + A.phred;
 
@@ -426,7 +432,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       int a = ia[m], e = ie[m];
       nraw = lane < nr ? (uint32_t)(e - a) : 0u;
       if (EDIT) {   // trim here, then describe the trimmed window
-        tw = lane < nr ? trim_word(*A.cold, rq[m], bq[m] + a, e - a) : 0u;
+        tw = lane < nr ? trim_word(HPGQ_TRI_COLD_COPY ? cold : *A.cold, rq[m], bq[m] + a, e - a) : 0u;
         if (A.trim && lane < nr) A.trim[r0 + l] = tw;
         a += (int)(tw & 0xFFFFu);
         e -= (int)(tw >> 16);
