@@ -53,6 +53,19 @@ CONFIGS = {
     "c5": dict(metric="Mreads/s (250 bp) chaos game k=7 tables",
                unit="Mreads/s", reads=25_000_000, batch=5_000_000, L=250, seed=5,
                workload="C5: chaos game k=7 feature tables (200 M x 250 bp over 8 GPUs)"),
+    # routing / geometry cases, not BASELINE configs
+    "c2_1024": dict(metric="Mreads/s (150 bp) stats+filter, lmax 1024 (drop-in default)",
+                    unit="Mreads/s", reads=100_000_000, batch=10_000_000, L=150, seed=2, lmax=1024,
+                    workload="C2 flags with the CLI's default --lmax 1024 (routing by read length)"),
+    "c2_250": dict(metric="Mreads/s (250 bp) stats+filter",
+                   unit="Mreads/s", reads=50_000_000, batch=5_000_000, L=250, seed=6,
+                   workload="C2 flags on 250 bp reads (--lmax 250: wide geometry)"),
+    "c2_250_1024": dict(metric="Mreads/s (250 bp) stats+filter, lmax 1024",
+                        unit="Mreads/s", reads=50_000_000, batch=5_000_000, L=250, seed=6, lmax=1024,
+                        workload="C2 flags on 250 bp reads with --lmax 1024 (hex defers to wide)"),
+    "c2_lr": dict(metric="Mreads/s (150 bp) stats+filter with a 5' window filter",
+                  unit="Mreads/s", reads=100_000_000, batch=10_000_000, L=150, seed=2,
+                  workload="C2 flags + --left-length 10 --left-quality-range 20,"),
 }
 
 
@@ -75,18 +88,48 @@ def parse():
 
 
 def params_for(cfg, L):
+    lmax = CONFIGS[cfg].get("lmax", L)
     if cfg == "c4":
-        return H.edit_params(lmax=L, stats=True, left_length=10, left_quality_range="20,",
+        return H.edit_params(lmax=lmax, stats=True, left_length=10, left_quality_range="20,",
                              right_length=30, right_quality_range="20,")
-    p = H.stats_params(lmax=L, read_quality_range="20,", read_length_range="50,")
+    extra = dict(left_length=10, left_quality_range="20,") if cfg == "c2_lr" else {}
+    p = H.stats_params(lmax=lmax, read_quality_range="20,", read_length_range="50,", **extra)
     if cfg == "c3":
         p.paired = 1
     return p
 
 
 # ---- CPU baseline: the oracle (C + OpenMP) on a bounded sample --------------
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def native_oracle():
+    """The oracle rebuilt HERE with -O3 -march=native: the tree's
+    liboracle.so is built portable (-march=x86-64-v2) in the build container,
+    whose CPU is not the GPU box's.  Falls back to the portable build."""
+    import subprocess
+    import tempfile
+    src = os.path.join(ROOT, "oracle", "hpgq_oracle.c")
+    out = os.path.join(tempfile.gettempdir(), f"hpgq_oracle_native_{os.getpid()}.so")
+    cmd = ["gcc", "-O3", "-march=native", "-std=c99", "-fopenmp", "-fPIC", "-ffp-contract=off",
+           "-shared", "-o", out, src]
+    try:
+        subprocess.run(cmd, check=True, capture_output=True, timeout=120)
+        return out, "gcc -O3 -march=native -fopenmp (built on this host)"
+    except (OSError, subprocess.SubprocessError):
+        return os.path.join(ROOT, "oracle", "liboracle.so"), "gcc -O3 -march=x86-64-v2 -fopenmp (portable)"
+
+
 def cpu_baseline(args, params):
-    lib = C.CDLL(os.path.join(ROOT, "oracle", "liboracle.so"))
+    so, build = native_oracle()
+    lib = C.CDLL(so)
     lib.oracle_run.restype = C.c_int
     lib.oracle_run.argtypes = [C.POINTER(H.Params), C.POINTER(H.Batch), C.POINTER(H.Batch),
                                C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
@@ -96,7 +139,10 @@ def cpu_baseline(args, params):
     lib.oracle_cgr_fill_batches.argtypes = [C.c_int, C.c_int, C.POINTER(H.Batch), C.c_int,
                                             C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
     ncores = len(os.sched_getaffinity(0))
-    threads = max(1, min(16, ncores))
+    # the GPU box gives one GPU's job a share of the host's cores and says so in
+    # OMP_NUM_THREADS (16 there); sched_getaffinity shows the whole host
+    share = int(os.environ.get("OMP_NUM_THREADS") or ncores)
+    threads = max(1, min(share, ncores))
     L = args.read_length
     n = 2_000_000 if args.config != "c5" else 400_000
     mates = 2 if args.config == "c3" else 1
@@ -109,6 +155,7 @@ def cpu_baseline(args, params):
         lib.oracle_synth(C.byref(s), 0, n, seq.ctypes.data, qual.ctypes.data, idx.ctypes.data)
         bufs.append((seq, qual, idx))
     bs = [H.Batch(n, sq.ctypes.data, ql.ctypes.data, ix.ctypes.data) for sq, ql, ix in bufs]
+    nt = [threads]
     if args.config == "c5":
         # independent fill calls (one per batch of 20 k reads) spread over the threads
         nb = 20
@@ -120,37 +167,51 @@ def cpu_baseline(args, params):
         ts = np.zeros(128 * 128, np.uint32)
         tq = np.zeros(128 * 128, np.uint32)
         wc = np.zeros(1, np.uint32)
-        run = lambda: lib.oracle_cgr_fill_batches(7, 33, sub, nb, ts.ctypes.data,  # noqa: E731
-                                                  tq.ctypes.data, wc.ctypes.data, threads)
+        run = lambda p=None: lib.oracle_cgr_fill_batches(7, 33, sub, nb, ts.ctypes.data,  # noqa: E731
+                                                         tq.ctypes.data, wc.ctypes.data, nt[0])
         what = f"oracle_cgr_fill_batches (old/chaos_game.c restated), {nb} fill calls"
     else:
         mask = np.zeros(n, np.uint8)
         trim = np.zeros(n * mates, np.uint32)
-        ctr = np.zeros(H.counters_len(params.lmax) * mates, np.uint64)
-        run = lambda: lib.oracle_run(C.byref(params), C.byref(bs[0]),  # noqa: E731
-                                     C.byref(bs[1]) if mates == 2 else None, mask.ctypes.data,
-                                     trim.ctypes.data, ctr.ctypes.data, threads)
+
+        def run(p=params):
+            ctr = np.zeros(H.counters_len(p.lmax) * mates, np.uint64)
+            return lib.oracle_run(C.byref(p), C.byref(bs[0]), C.byref(bs[1]) if mates == 2 else None,
+                                  mask.ctypes.data, trim.ctypes.data, ctr.ctypes.data, nt[0])
         what = "oracle_run (hpgq_oracle.c)"
-    done, t0 = 0, time.perf_counter()
-    while True:
-        assert run() == 0
-        done += n
-        el = time.perf_counter() - t0
-        if el >= args.cpu_seconds:
-            break
+
+    def timed(p=None, budget=args.cpu_seconds):
+        done, t0 = 0, time.perf_counter()
+        while True:
+            assert (run(p) if p is not None else run()) == 0
+            done += n
+            el = time.perf_counter() - t0
+            if el >= budget:
+                return done, el
+    done, el = timed()
+    out = {"value": round(done / el / 1e6, 3), "unit": CONFIGS[args.config]["unit"],
+           "cores": threads, "kind": "port", "cpu": cpu_model(), "cores_visible": ncores,
+           "build": build}
     # one pass on one thread beside the threaded figure
-    nthreads, threads = threads, 1
+    nt[0] = 1
     t1 = time.perf_counter()
     assert run() == 0
     el1 = time.perf_counter() - t1
-    threads = nthreads
-    return {"value": round(done / el / 1e6, 3), "unit": CONFIGS[args.config]["unit"],
-            "cores": threads, "kind": "port",
-            "value_1thread": round(n / el1 / 1e6, 3),
-            "sample": f"{n} synthetic {L} bp {'pairs' if mates == 2 else 'reads'} (seed "
-                      f"{args.seed}, same generator and options), {done // n} passes in "
-                      f"{el:.1f} s; {what} -O3 OpenMP, {threads} threads of {ncores} visible; "
-                      f"value_1thread: one pass on 1 thread ({el1:.1f} s)"}
+    out["value_1thread"] = round(n / el1 / 1e6, 3)
+    nt[0] = threads
+    c1 = ""
+    if args.config == "c2":
+        # BASELINE.json configs[0] (C1): `stats` (no filter) on 1 M x 150 SE reads, CPU
+        p1 = H.stats_params(lmax=150)
+        d1, e1 = timed(p1, budget=max(2.0, args.cpu_seconds / 3))
+        out["c1_stats_mreads_s"] = round(d1 / e1 / 1e6, 3)
+        c1 = (f"; c1_stats_mreads_s: C1 `stats` without filter, same reads, {d1 // n} passes "
+              f"in {e1:.1f} s")
+    out["sample"] = (f"{n} synthetic {L} bp {'pairs' if mates == 2 else 'reads'} (seed "
+                     f"{args.seed}, same generator and options), {done // n} passes in "
+                     f"{el:.1f} s; {what}, {threads} OpenMP threads (this GPU's CPU share; "
+                     f"{ncores} visible); value_1thread: one pass on 1 thread ({el1:.1f} s){c1}")
+    return out
 
 
 # ---- resident synthetic shard ----------------------------------------------

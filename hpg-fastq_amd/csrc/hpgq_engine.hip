@@ -1,5 +1,7 @@
-// hpgq_engine.hip — libhpgq: engine context, launches and the C-ABI.
-// The kernel itself lives in hpgq_engine_kernel.h (design notes there).
+// hpgq_engine.hip — libhpgq: engine context, the kernel chain and the C-ABI.
+// The kernels live in hpgq_engine_kernel.h (catch-all, routing) and
+// hpgq_engine_tri.h (segmented), instantiated per geometry in
+// hpgq_engine_geo.hip.
 
 #include "hpgq_engine_kernel.h"
 #include "hpgq_engine_tri.h"
@@ -8,10 +10,29 @@
 // C-ABI
 // ===========================================================================
 
+#include <climits>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <rccl/rccl.h>
+
+namespace {
+
+// one kernel of the chain
+struct Stage {
+  const void *fn = nullptr;
+  size_t lds = 0;
+  int grid = 0;
+  int block = 0;           // reads per unit (direct stages)
+  int defer_len = INT_MAX;
+  bool follow = false;
+  char name[80] = {0};
+};
+
+// flags words behind the counters (one memset clears both)
+enum { FL_PEND1 = 0, FL_PEND2 = 2, FL_ERR = 4, FL_WORDS = 8 };
+
+}  // namespace
 
 struct hpgq_ctx {
   int device = 0;
@@ -19,21 +40,20 @@ struct hpgq_ctx {
   hpgq_params_t p{};
   int nm = 1;
   size_t clen = 0;
-  uint64_t *d_counters = nullptr;
-  int32_t *d_err = nullptr;
-  size_t lds_bytes = 0;
-  char kname[64] = {0};   // the engine kernel instance hpgq_open chose
-  const void *kfn = nullptr;
-  int nch = 1;
-  bool gen = false;               // generic (edit / N / OOR / left-right) kernel variant
-  bool tri = false;               // segmented FAST kernel (lmax <= 160)
-  bool hex = false;               // ... in its 16-byte-lane geometry (lmax <= 156)
-  bool tri_edit = false;          // ... trimming in its block prologue (single-end edit)
-  bool tri_x = false;             // ... with the N / out-of-range read filters
-  int grid = 0;
-  uint64_t *d_slab = nullptr;     // [grid][nm * clen] per-workgroup partials
+  // d_state: [nm * clen] u64 counters | FL_WORDS u32 (deferred-read counts by
+  // call parity, error flag)
+  uint64_t *d_state = nullptr;
+  uint32_t *d_flags = nullptr;
+  uint64_t *d_global = nullptr;   // hpgq_allreduce output
+  bool reduced = false;           // d_global is current (no run / reset since)
   hpgq::ColdParams *d_cold = nullptr;
-  bool dirty = false;             // slab holds partials not yet folded into d_counters
+  // the chain: s1 takes the batch; s2 (wide segmented) and s3 (catch-all) take
+  // what the stage before deferred
+  Stage s1, s2, s3;
+  bool has2 = false, has3 = false;
+  int parity = 0;
+  uint64_t *d_bits1 = nullptr, *d_bits2 = nullptr;   // deferred reads per s1 unit
+  size_t bits_cap = 0;
   // host-path device staging
   char *d_buf = nullptr;
   size_t d_buf_cap = 0;
@@ -65,9 +85,10 @@ static int engine_flags(const hpgq_params_t &p) {
   if (p.filter_on) f |= hpgq::F_FILTER;
   if (p.edit_on) f |= hpgq::F_EDIT;
   if (p.stats_on) f |= hpgq::F_STATS;
-  // reads never exceed lmax (else the call fails), so a bound >= lmax cannot bite
-  if (p.filter_on && p.max_N < p.lmax) f |= hpgq::F_NEED_N;
-  if (p.filter_on && p.max_out_of_quality < p.lmax) f |= hpgq::F_NEED_OOR;
+  // reads of any length are filtered, so any bound can bite (the segmented
+  // kernels only count N / out-of-range when it can bite on their reads: nx_bites)
+  if (p.filter_on && p.max_N < INT_MAX) f |= hpgq::F_NEED_N;
+  if (p.filter_on && p.max_out_of_quality < INT_MAX) f |= hpgq::F_NEED_OOR;
   if (p.filter_on && (p.left_length > 0 || p.right_length > 0)) f |= hpgq::F_NEED_LR;
   // out of range  <=>  raw < phred + min_q  or  raw > phred + max_q
   uint32_t lo4, hi4;
@@ -120,65 +141,128 @@ static void cold_params(const hpgq_params_t &p, hpgq::ColdParams &C) {
 template <int NM, bool GEN>
 static const void *kernel_nch(int nch) {
   switch (nch) {
-    case 1: return (const void *)hpgq::engine_kernel<NM, 1, GEN>;
-    case 2: return (const void *)hpgq::engine_kernel<NM, 2, GEN>;
-    default: return (const void *)hpgq::engine_kernel<NM, 5, GEN>;
+    case 1: return (const void *)hpgq::engine_kernel<NM, 1, GEN, false>;
+    case 2: return (const void *)hpgq::engine_kernel<NM, 2, GEN, false>;
+    default: return (const void *)hpgq::engine_kernel<NM, 5, GEN, false>;
   }
 }
 
-template <int NW>
-static const void *tri_for(int mw, bool un, int nm, bool edit) {
-  using hpgq::engine_tri_kernel;
-  if (edit) return mw <= 4 ? (const void *)engine_tri_kernel<4, false, 1, true, NW>
-                           : (const void *)engine_tri_kernel<5, false, 1, true, NW>;
-  if constexpr (NW == 4) {
-    if (un && !edit) return (const void *)engine_tri_kernel<4, true, 1, false, 4>;
-    if (nm == 2) return (const void *)engine_tri_kernel<3, false, 2, false, 4>;   // 3 waves/SIMD: two mates' accumulators
-  }
-  if constexpr (NW == 2) {
-    if (nm == 2) {   // paired-end (tri geometry: two mates' accumulators do not fit hex's registers)
-      if (mw <= 4) return (const void *)engine_tri_kernel<4, false, 2, false, 2>;
-      if (mw == 5) return (const void *)engine_tri_kernel<5, false, 2, false, 2>;
-      return (const void *)engine_tri_kernel<6, false, 2, false, 2>;
-    }
-    if (un) {
-      if (mw <= 4) return (const void *)engine_tri_kernel<4, true, 1, false, 2>;
-      if (mw == 5) return (const void *)engine_tri_kernel<5, true, 1, false, 2>;
-      return (const void *)engine_tri_kernel<6, true, 1, false, 2>;
-    }
-  }
-  if (mw <= 4) return (const void *)engine_tri_kernel<4, false, 1, false, NW>;
-  if (mw == 5) return (const void *)engine_tri_kernel<5, false, 1, false, NW>;
-  return (const void *)engine_tri_kernel<6, false, 1, false, NW>;
+// the catch-all kernel: chunk count from lmax (the pipelined loads must hold
+// every read the counters can hold; longer reads take its chunk loop)
+static void catch_all(Stage &s, int nm, int lmax, bool gen, bool follow) {
+  int nch = (lmax + hpgq::kChunk - 1) / hpgq::kChunk;
+  if (nch > 2 || follow) nch = 5;   // instantiated chunk counts: 1, 2, 5
+  if (follow)   // the follow-up instance: every option, five chunks (reads <= 1260 pipelined)
+    s.fn = nm == 2 ? (const void *)hpgq::engine_kernel<2, 5, true, true>
+                   : (const void *)hpgq::engine_kernel<1, 5, true, true>;
+  else
+    s.fn = nm == 2 ? (gen ? kernel_nch<2, true>(nch) : kernel_nch<2, false>(nch))
+                   : (gen ? kernel_nch<1, true>(nch) : kernel_nch<1, false>(nch));
+  s.follow = follow;
+  s.block = 64;
+  std::snprintf(s.name, sizeof(s.name), "hpgq::engine_kernel<%d, %d, %s>%s", nm, nch, gen ? "true" : "false",
+                follow ? " (follow-up)" : "");
 }
 
-// tri: the segmented kernel (hpgq_engine_tri.h), hex selects its 16-byte-lane geometry
-static const void *kernel_for(int nm, int nch, bool gen, bool tri, bool hex, bool edit, bool tx, char *name,
-                              size_t cap) {
-  if (tri && tx) {   // spill-free occupancy per variant, as below
-    using hpgq::engine_tri_x_kernel;
-    const int mw = hex ? (nm == 2 ? 3 : 4) : (nm == 2 ? 3 : 5);
-    std::snprintf(name, cap, "hpgq::engine_tri_x_kernel<%d, %d, %d>", mw, nm, hex ? 4 : 2);
-    if (hex) return nm == 2 ? (const void *)engine_tri_x_kernel<3, 2, 4> : (const void *)engine_tri_x_kernel<4, 1, 4>;
-    return nm == 2 ? (const void *)engine_tri_x_kernel<3, 2, 2> : (const void *)engine_tri_x_kernel<5, 1, 2>;
+static size_t seg_lds(const hpgq_params_t &p, int nm, bool nx) {
+  const size_t hlen = (size_t)p.lmax + 1 + HPGQ_MEANQ_BINS + HPGQ_GC_BINS;
+  const size_t mate_words = (size_t)6 * p.lmax + ((hlen + 1) & ~(size_t)1) + 2 * HPGQ_NUM_SCALARS;
+  // per mate [6][lmax] + hist + scalars, 16 B alignment, the byte-mask table,
+  // per wave and mate two read tables (2 x 1 KB) + segment ends (+ NX ends),
+  // per wave a compaction scratch and a deferral word
+  return (size_t)nm * mate_words * 4 + 16 + 17 * 16 +
+         (size_t)hpgq::kWaves * ((size_t)nm * (2 * 256 + (nx ? 128 : 64)) + 64 + 4) * 4;
+}
+
+static size_t catch_all_lds(const hpgq_params_t &p, int nm) {
+  const size_t hlen = (size_t)p.lmax + 1 + HPGQ_MEANQ_BINS + HPGQ_GC_BINS;
+  const size_t hist_words = ((size_t)nm * hlen + 1) & ~(size_t)1;
+  return ((size_t)nm * 6 * p.lmax + hist_words) * 4 + (size_t)nm * HPGQ_NUM_SCALARS * 8 +
+         sizeof(hpgq::ColdParams) + (size_t)hpgq::kWaves * 64 * 4;
+}
+
+static int seg_block(int geo) {
+  return geo == hpgq::GEO_TRI ? hpgq::Geo<hpgq::GEO_TRI>::kBlock
+                              : (geo == hpgq::GEO_HEX ? hpgq::Geo<hpgq::GEO_HEX>::kBlock
+                                                      : hpgq::Geo<hpgq::GEO_WIDE>::kBlock);
+}
+
+static int seg_pos(int geo) {
+  return geo == hpgq::GEO_TRI ? hpgq::Geo<hpgq::GEO_TRI>::kPos
+                              : (geo == hpgq::GEO_HEX ? hpgq::Geo<hpgq::GEO_HEX>::kPos
+                                                      : hpgq::Geo<hpgq::GEO_WIDE>::kPos);
+}
+
+static bool seg_stage(Stage &s, int geo, int nm, bool edit, bool nx, bool follow) {
+  hpgq::SegChoice ch{};
+  if (geo == hpgq::GEO_TRI) ch = hpgq::seg_kernel_tri(nm, edit, nx, follow, s.name, sizeof(s.name));
+  else if (geo == hpgq::GEO_HEX) ch = hpgq::seg_kernel_hex(nm, edit, nx, follow, s.name, sizeof(s.name));
+  else ch = hpgq::seg_kernel_wide(nm, edit, nx, follow, s.name, sizeof(s.name));
+  s.fn = ch.fn;
+  s.follow = follow;
+  s.block = seg_block(geo);
+  return ch.fn != nullptr;
+}
+
+static int finish_stage(hpgq_ctx *c, Stage &s, size_t lds, int cus) {
+  s.lds = lds;
+  if (s.lds > 64 * 1024)
+    HPGQ_HIP_TRY(hipFuncSetAttribute(s.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)s.lds));
+  int per_cu = 0;
+  HPGQ_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, s.fn, hpgq::kWG, s.lds));
+  if (per_cu < 1) per_cu = 1;
+  s.grid = cus * per_cu;   // persistent: every workgroup resident, grid-stride over units
+  return HPGQ_OK;
+}
+
+// Route by the reads' ACTUAL lengths: the first stage is the
+// segmented kernel whenever the options allow one; it defers the reads it
+// cannot hold, the wide geometry takes those up to 252 bases and the
+// catch-all takes the rest.  lmax only sizes the counters, so a ctx opened
+// with the CLI's lmax 1024 runs 150 bp reads on the hex geometry.
+static int plan_chain(hpgq_ctx *c, int cus) {
+  const hpgq_params_t &p = c->p;
+  const int fl = engine_flags(p);
+  const bool stats = fl & hpgq::F_STATS;
+  const bool lr = fl & hpgq::F_NEED_LR;
+  // N / out-of-range limits can only bite on a segmented kernel's reads (<= 252
+  // bases) when they are below 252; else the plain variant runs
+  const int posw = hpgq::Geo<hpgq::GEO_WIDE>::kPos;
+  const bool nx = p.filter_on && (p.max_N < posw || p.max_out_of_quality < posw);
+  const bool edit = fl & hpgq::F_EDIT;
+  const char *force = std::getenv("HPGQ_KERNEL");   // "single": the catch-all alone (tests)
+  const bool seg = !lr && !(nx && edit) && !(edit && c->nm == 2) && !(force && std::strcmp(force, "single") == 0);
+  if (!seg) {
+    catch_all(c->s1, c->nm, p.lmax, needs_generic(fl), false);
+    return finish_stage(c, c->s1, catch_all_lds(p, c->nm), cus);
   }
-  if (tri) {
-    const char *w = std::getenv("HPGQ_TRI_WAVES");      // occupancy experiment knob
-    const char *u = std::getenv("HPGQ_TRI_UNALIGNED");  // load-scheme experiment knob (tri only)
-    const int nw = hex ? 4 : 2;
-    int mw = w ? std::atoi(w) : (hex ? 4 : (nm == 2 ? 4 : 5));   // spill-free occupancy per variant
-    mw = mw <= 4 ? 4 : (mw == 5 ? 5 : 6);
-    if (hex) mw = nm == 2 ? 3 : 4;   // 116-123 VGPRs (SE)
-    if (edit && mw > 5) mw = 5;
-    const bool un = !edit && nm == 1 && u && std::atoi(u) != 0;
-    std::snprintf(name, cap, "hpgq::engine_tri_kernel<%d, %s, %d, %s, %d>", mw, un ? "true" : "false", edit ? 1 : nm,
-                  edit ? "true" : "false", nw);
-    return hex ? tri_for<4>(mw, un, nm, edit) : tri_for<2>(mw, un, nm, edit);
+  // first geometry: hex for short reads; wide when the counters say reads are
+  // 157..252 long; HPGQ_TRI_GEO=tri|hex|wide forces one (tests, A/B)
+  int geo = (stats && p.lmax > hpgq::Geo<hpgq::GEO_HEX>::kPos && p.lmax <= hpgq::Geo<hpgq::GEO_WIDE>::kPos)
+                ? hpgq::GEO_WIDE
+                : hpgq::GEO_HEX;
+  if (const char *g = std::getenv("HPGQ_TRI_GEO")) {
+    if (!std::strcmp(g, "tri")) geo = hpgq::GEO_TRI;
+    else if (!std::strcmp(g, "hex")) geo = hpgq::GEO_HEX;
+    else if (!std::strcmp(g, "wide")) geo = hpgq::GEO_WIDE;
   }
-  std::snprintf(name, cap, "hpgq::engine_kernel<%d, %d, %s>", nm, nch == 1 ? 1 : (nch == 2 ? 2 : 5),
-                gen ? "true" : "false");
-  if (nm == 2) return gen ? kernel_nch<2, true>(nch) : kernel_nch<2, false>(nch);
-  return gen ? kernel_nch<1, true>(nch) : kernel_nch<1, false>(nch);
+  if (!seg_stage(c->s1, geo, c->nm, edit, nx, false)) return HPGQ_E_INVALID;
+  const int pos1 = seg_pos(geo);
+  // a merged read longer than lmax leaves the segmented kernels (the
+  // catch-all counts it as a long read)
+  c->s1.defer_len = stats ? std::min(pos1, p.lmax) : pos1;
+  int rc = finish_stage(c, c->s1, seg_lds(p, c->nm, nx), cus);
+  if (rc) return rc;
+  c->has2 = geo != hpgq::GEO_WIDE && c->s1.defer_len < posw && !(stats && p.lmax <= pos1);
+  if (c->has2) {
+    if (!seg_stage(c->s2, hpgq::GEO_WIDE, c->nm, edit, nx, true)) return HPGQ_E_INVALID;
+    c->s2.defer_len = stats ? std::min(posw, p.lmax) : posw;
+    rc = finish_stage(c, c->s2, seg_lds(p, c->nm, nx), cus);
+    if (rc) return rc;
+  }
+  c->has3 = true;
+  catch_all(c->s3, c->nm, p.lmax, true, true);
+  return finish_stage(c, c->s3, catch_all_lds(p, c->nm), cus);
 }
 
 extern "C" {
@@ -224,9 +308,17 @@ const char *hpgq_strerror(int code) {
   }
 }
 
-const char *hpgq_version(void) { return "hpgq 0.1 (gfx950)"; }
+const char *hpgq_version(void) { return "hpgq 0.2 (gfx950)"; }
 
-const char *hpgq_kernel_name(const hpgq_ctx_t *ctx) { return ctx ? ctx->kname : ""; }
+const char *hpgq_kernel_name(const hpgq_ctx_t *ctx) { return ctx ? ctx->s1.name : ""; }
+
+const char *hpgq_kernel_chain(const hpgq_ctx_t *ctx) {
+  static thread_local char buf[300];
+  if (!ctx) return "";
+  std::snprintf(buf, sizeof(buf), "%s%s%s%s%s", ctx->s1.name, ctx->has2 ? " -> " : "", ctx->has2 ? ctx->s2.name : "",
+                ctx->has3 ? " -> " : "", ctx->has3 ? ctx->s3.name : "");
+  return buf;
+}
 
 int hpgq_host_alloc(void **ptr, size_t bytes) {
   if (!ptr) return HPGQ_E_INVALID;
@@ -272,6 +364,8 @@ static int validate_params(const hpgq_params_t *p) {
   return HPGQ_OK;
 }
 
+static size_t state_bytes(const hpgq_ctx *c) { return c->clen * c->nm * sizeof(uint64_t) + FL_WORDS * 4; }
+
 int hpgq_open(hpgq_ctx_t **out, int device, const hpgq_params_t *p) {
   if (!out) return HPGQ_E_INVALID;
   *out = nullptr;
@@ -289,56 +383,19 @@ int hpgq_open(hpgq_ctx_t **out, int device, const hpgq_params_t *p) {
   c->p = *p;
   c->nm = p->paired ? 2 : 1;
   c->clen = hpgq_counters_len(p->lmax);
-  c->nch = (p->lmax + hpgq::kChunk - 1) / hpgq::kChunk;
-  if (c->nch > 2) c->nch = 5;   // instantiated chunk counts: 1, 2, 5
-  c->gen = needs_generic(engine_flags(*p));
-  {
-    const char *force = std::getenv("HPGQ_KERNEL");   // "single" forces the one-read kernel
-    const int fl = engine_flags(*p);
-    const bool lr = fl & hpgq::F_NEED_LR;                          // window filters: engine_kernel
-    const bool nx = fl & (hpgq::F_NEED_N | hpgq::F_NEED_OOR);     // N / out-of-range: engine_tri_x_kernel
-    const bool edit = fl & hpgq::F_EDIT;
-    c->tri = !lr && !(nx && edit) && (!edit || c->nm == 1) && p->lmax <= hpgq::kTriPos &&
-             !(force && std::strcmp(force, "single") == 0);
-    c->tri_edit = c->tri && edit;
-    c->tri_x = c->tri && nx;
-    const char *geo = std::getenv("HPGQ_TRI_GEO");   // "tri" forces the 8-byte-lane geometry
-    c->hex = c->tri && p->lmax <= hpgq::kHexPos &&
-             !(geo && std::strcmp(geo, "tri") == 0);
-  }
-  {
-    const int hlen = p->lmax + 1 + HPGQ_MEANQ_BINS + HPGQ_GC_BINS;
-    const size_t hist_words = ((size_t)c->nm * hlen + 1) & ~(size_t)1;
-    c->lds_bytes = ((size_t)c->nm * 6 * p->lmax + hist_words) * 4 +
-                   (size_t)c->nm * HPGQ_NUM_SCALARS * 8 + sizeof(hpgq::ColdParams);
-    // the three-read kernel: per mate [6][lmax] + hist + scalars, and per wave
-    // and mate two read tables (2 x 1 KB) + segment ends (256 B)
-    const size_t mate_words = (size_t)6 * p->lmax + (((size_t)hlen + 1) & ~(size_t)1) + 2 * HPGQ_NUM_SCALARS;
-    const size_t tri_lds = (size_t)c->nm * mate_words * 4 + 16 + 17 * 16 +   // + the byte-mask table
-                           (size_t)hpgq::kWaves * c->nm * (2 * 256 + (c->tri_x ? 128 : 64)) * 4;
-    if (tri_lds > c->lds_bytes) c->lds_bytes = tri_lds;
-  }
   HPGQ_HIP_TRY(hipSetDevice(device));
   HPGQ_HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-  HPGQ_HIP_TRY(hipMalloc(&c->d_counters, c->clen * c->nm * sizeof(uint64_t)));
-  HPGQ_HIP_TRY(hipMalloc(&c->d_err, sizeof(int32_t)));
-  HPGQ_HIP_TRY(hipMemsetAsync(c->d_counters, 0, c->clen * c->nm * sizeof(uint64_t), c->stream));
-  HPGQ_HIP_TRY(hipMemsetAsync(c->d_err, 0, sizeof(int32_t), c->stream));
+  HPGQ_HIP_TRY(hipMalloc(&c->d_state, state_bytes(c)));
+  c->d_flags = reinterpret_cast<uint32_t *>(c->d_state + c->clen * c->nm);
+  HPGQ_HIP_TRY(hipMalloc(&c->d_global, c->clen * c->nm * sizeof(uint64_t)));
+  HPGQ_HIP_TRY(hipMemsetAsync(c->d_state, 0, state_bytes(c), c->stream));
   int cus = 0;
   HPGQ_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-  const void *kfn = kernel_for(c->nm, c->nch, c->gen, c->tri, c->hex, c->tri_edit, c->tri_x, c->kname,
-                               sizeof(c->kname));
-  c->kfn = kfn;
-  if (c->lds_bytes > 64 * 1024)
-    HPGQ_HIP_TRY(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     (int)c->lds_bytes));
-  int per_cu = 0;
-  HPGQ_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kfn, hpgq::kWG, c->lds_bytes));
-  if (per_cu < 1) per_cu = 1;
-  c->grid = cus * per_cu;   // persistent: every workgroup resident, grid-stride over reads
-  HPGQ_HIP_TRY(hipMalloc(&c->d_slab, (size_t)c->grid * c->nm * c->clen * sizeof(uint64_t)));
-  HPGQ_HIP_TRY(hipMemsetAsync(c->d_slab, 0, (size_t)c->grid * c->nm * c->clen * sizeof(uint64_t),
-                              c->stream));
+  rc = plan_chain(c, cus);
+  if (rc) {
+    hpgq_close(c);
+    return rc;
+  }
   {
     hpgq::ColdParams cp{};
     cold_params(c->p, cp);
@@ -355,10 +412,11 @@ void hpgq_close(hpgq_ctx_t *c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->comm) ncclCommDestroy(c->comm);
-  (void)hipFree(c->d_counters);
-  (void)hipFree(c->d_err);
-  (void)hipFree(c->d_slab);
+  (void)hipFree(c->d_state);
+  (void)hipFree(c->d_global);
   (void)hipFree(c->d_cold);
+  (void)hipFree(c->d_bits1);
+  (void)hipFree(c->d_bits2);
   (void)hipFree(c->d_buf);
   (void)hipFree(c->d_mask);
   (void)hipFree(c->d_trim);
@@ -366,30 +424,94 @@ void hpgq_close(hpgq_ctx_t *c) {
   delete c;
 }
 
-static int launch(hpgq_ctx *c, hpgq::EngineArgs &A) {
-  if (A.num_reads <= 0) return HPGQ_OK;
-  A.slab = c->d_slab;
-  A.err = c->d_err;
-  const int64_t per_block = c->tri ? (c->hex ? hpgq::kHexBlock : hpgq::kTriBlock) : 64;
-  const int64_t nblocks = (A.num_reads + per_block - 1) / per_block;
-  const int64_t need = (nblocks + hpgq::kWaves - 1) / hpgq::kWaves;
-  const int grid = (int)std::min<int64_t>(need, c->grid);
-  void *args[] = {&A};
-  HPGQ_HIP_TRY(hipLaunchKernel(c->kfn, dim3(grid), dim3(hpgq::kWG), args,
-                               c->lds_bytes, c->stream));
-  c->dirty = true;
+// per-unit deferral masks for a batch of n reads
+static int ensure_bits(hpgq_ctx *c, int64_t n) {
+  const size_t units = (size_t)((n + c->s1.block - 1) / c->s1.block) + 1;
+  if (units <= c->bits_cap) return HPGQ_OK;
+  HPGQ_HIP_TRY(hipStreamSynchronize(c->stream));
+  (void)hipFree(c->d_bits1);
+  (void)hipFree(c->d_bits2);
+  c->d_bits1 = c->d_bits2 = nullptr;
+  c->bits_cap = 0;
+  const size_t cap = units + units / 4 + 64;
+  if (hipMalloc(&c->d_bits1, cap * 8) != hipSuccess) return HPGQ_E_NOMEM;
+  if (hipMalloc(&c->d_bits2, cap * 8) != hipSuccess) return HPGQ_E_NOMEM;
+  c->bits_cap = cap;
   return HPGQ_OK;
 }
 
-// fold the per-workgroup slab rows into d_counters (async on the ctx stream)
-static int fold(hpgq_ctx *c) {
-  if (!c->dirty) return HPGQ_OK;
-  const int len = (int)(c->clen * c->nm);
-  hipLaunchKernelGGL(hpgq::slab_reduce_kernel, dim3((len + 255) / 256), dim3(256), 0, c->stream,
-                     c->d_slab, c->grid, len, c->d_counters);
-  HPGQ_HIP_TRY(hipGetLastError());
-  c->dirty = false;
+static int launch_stage(hpgq_ctx *c, const Stage &s, hpgq::EngineArgs &A) {
+  const int64_t units = s.follow ? A.nunits : (A.num_reads + s.block - 1) / s.block;
+  const int64_t need = (units + hpgq::kWaves - 1) / hpgq::kWaves;
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(need, s.grid));
+  void *args[] = {&A};
+  HPGQ_HIP_TRY(hipLaunchKernel(s.fn, dim3(grid), dim3(hpgq::kWG), args, s.lds, c->stream));
   return HPGQ_OK;
+}
+
+// the chain over one batch (A: batch, outputs and options filled in)
+static int launch(hpgq_ctx *c, hpgq::EngineArgs &A) {
+  if (A.num_reads <= 0) return HPGQ_OK;
+  if (A.num_reads > INT32_MAX) return HPGQ_E_INVALID;   // read ids are 32-bit in the follow-up stages
+  A.counters = c->d_state;
+  A.err = reinterpret_cast<int32_t *>(c->d_flags + FL_ERR);
+  c->reduced = false;
+  if (!c->has3) {   // the catch-all alone
+    A.unit_bits = A.unit_and = nullptr;
+    A.pending = A.pending_clear = nullptr;
+    A.defer_bits = nullptr;
+    A.defer_count = nullptr;
+    A.defer_len = INT_MAX;
+    return launch_stage(c, c->s1, A);
+  }
+  int rc = ensure_bits(c, A.num_reads);
+  if (rc) return rc;
+  const int s = c->parity, o = s ^ 1;
+  c->parity = o;
+  uint32_t *f = c->d_flags;
+  // stage 1: every read; deferrals -> bits1, count -> PEND1[s]
+  hpgq::EngineArgs A1 = A;
+  A1.unit_bits = A1.unit_and = nullptr;
+  A1.pending = A1.pending_clear = nullptr;
+  A1.defer_bits = c->d_bits1;
+  A1.defer_count = f + FL_PEND1 + s;
+  A1.defer_len = c->s1.defer_len;
+  rc = launch_stage(c, c->s1, A1);
+  if (rc) return rc;
+  const int64_t nunits = (A.num_reads + c->s1.block - 1) / c->s1.block;
+  const uint64_t *last_bits = c->d_bits1;
+  const uint32_t *last_count = f + FL_PEND1 + s;
+  uint32_t *last_clear = f + FL_PEND1 + o;
+  const uint64_t *and_bits = nullptr;
+  if (c->has2) {   // stage 2: the deferred reads up to 252 bases; longer -> bits2, PEND2[s]
+    hpgq::EngineArgs A2 = A;
+    A2.unit_bits = c->d_bits1;
+    A2.unit_and = nullptr;
+    A2.nunits = nunits;
+    A2.unit_reads = c->s1.block;
+    A2.pending = last_count;
+    A2.pending_clear = last_clear;
+    A2.defer_bits = c->d_bits2;
+    A2.defer_count = f + FL_PEND2 + s;
+    A2.defer_len = c->s2.defer_len;
+    rc = launch_stage(c, c->s2, A2);
+    if (rc) return rc;
+    and_bits = c->d_bits1;   // bits2 words are only written for units with bits1 set
+    last_bits = c->d_bits2;
+    last_count = f + FL_PEND2 + s;
+    last_clear = f + FL_PEND2 + o;
+  }
+  hpgq::EngineArgs A3 = A;   // stage 3: the catch-all, whatever is left
+  A3.unit_bits = last_bits;
+  A3.unit_and = and_bits;
+  A3.nunits = nunits;
+  A3.unit_reads = c->s1.block;
+  A3.pending = last_count;
+  A3.pending_clear = last_clear;
+  A3.defer_bits = nullptr;
+  A3.defer_count = nullptr;
+  A3.defer_len = INT_MAX;
+  return launch_stage(c, c->s3, A3);
 }
 
 int hpgq_run_device(hpgq_ctx_t *c, const hpgq_batch_t *b, const hpgq_batch_t *b2,
@@ -445,8 +567,8 @@ int hpgq_run_host(hpgq_ctx_t *c, const hpgq_batch_t *b, const hpgq_batch_t *b2,
   for (int m = 0; m < c->nm; ++m) {
     const int32_t *ix = bs[m]->data_indices;
     bytes[m] = (size_t)(ix[n] - ix[0]);
-    off[m][0] = total; total += (bytes[m] + 255) & ~(size_t)255;   // seq
-    off[m][1] = total; total += (bytes[m] + 255) & ~(size_t)255;   // quality
+    off[m][0] = total; total += (bytes[m] + HPGQ_DEVICE_SLACK + 255) & ~(size_t)255;   // seq
+    off[m][1] = total; total += (bytes[m] + HPGQ_DEVICE_SLACK + 255) & ~(size_t)255;   // quality
     off[m][2] = total; total += ((size_t)(n + 1) * 4 + 255) & ~(size_t)255;
   }
   int rc = ensure_dev(c, total, (size_t)n);
@@ -482,45 +604,37 @@ int hpgq_sync(hpgq_ctx_t *c) {
   HPGQ_HIP_TRY(hipSetDevice(c->device));
   HPGQ_HIP_TRY(hipStreamSynchronize(c->stream));
   int32_t err = 0;
-  HPGQ_HIP_TRY(hipMemcpy(&err, c->d_err, sizeof(err), hipMemcpyDeviceToHost));
+  HPGQ_HIP_TRY(hipMemcpy(&err, c->d_flags + FL_ERR, sizeof(err), hipMemcpyDeviceToHost));
   return err ? HPGQ_E_READ_TOO_LONG : HPGQ_OK;
 }
 
 int hpgq_reset(hpgq_ctx_t *c) {
   if (!c) return HPGQ_E_INVALID;
   HPGQ_HIP_TRY(hipSetDevice(c->device));
-  HPGQ_HIP_TRY(hipMemsetAsync(c->d_counters, 0, c->clen * c->nm * sizeof(uint64_t), c->stream));
-  HPGQ_HIP_TRY(hipMemsetAsync(c->d_slab, 0, (size_t)c->grid * c->nm * c->clen * sizeof(uint64_t),
-                              c->stream));
-  HPGQ_HIP_TRY(hipMemsetAsync(c->d_err, 0, sizeof(int32_t), c->stream));
-  c->dirty = false;
+  HPGQ_HIP_TRY(hipMemsetAsync(c->d_state, 0, state_bytes(c), c->stream));
+  c->reduced = false;
   return HPGQ_OK;
 }
 
-int hpgq_fold(hpgq_ctx_t *c) {
-  if (!c) return HPGQ_E_INVALID;
-  HPGQ_HIP_TRY(hipSetDevice(c->device));
-  return fold(c);
-}
+// the kernels add into the counters themselves: nothing to fold (kept for the ABI)
+int hpgq_fold(hpgq_ctx_t *c) { return c ? HPGQ_OK : HPGQ_E_INVALID; }
 
 size_t hpgq_counters_size(const hpgq_ctx_t *c) { return c ? c->clen * c->nm : 0; }
 
 int hpgq_read_counters(hpgq_ctx_t *c, uint64_t *out, size_t n) {
   if (!c || !out || n < c->clen * c->nm) return HPGQ_E_INVALID;
   HPGQ_HIP_TRY(hipSetDevice(c->device));
-  int rc = fold(c);
-  if (rc) return rc;
-  HPGQ_HIP_TRY(hipMemcpyAsync(out, c->d_counters, c->clen * c->nm * sizeof(uint64_t),
+  HPGQ_HIP_TRY(hipMemcpyAsync(out, c->reduced ? c->d_global : c->d_state, c->clen * c->nm * sizeof(uint64_t),
                               hipMemcpyDeviceToHost, c->stream));
   HPGQ_HIP_TRY(hipStreamSynchronize(c->stream));
   return HPGQ_OK;
 }
 
-uint64_t *hpgq_counters_device(hpgq_ctx_t *c) { return c ? c->d_counters : nullptr; }
+uint64_t *hpgq_counters_device(hpgq_ctx_t *c) { return c ? c->d_state : nullptr; }
 void *hpgq_stream(hpgq_ctx_t *c) { return c ? (void *)c->stream : nullptr; }
 
 // ---------------------------------------------------------------------------
-// RCCL (one process per GPU): one in-place sum of the packed counters
+// RCCL (one process per GPU): one sum of the packed counters
 // ---------------------------------------------------------------------------
 
 static_assert(sizeof(ncclUniqueId) <= HPGQ_COMM_ID_BYTES, "nccl id size");
@@ -546,17 +660,20 @@ int hpgq_comm_init(hpgq_ctx_t *c, int nranks, int rank, const char id[HPGQ_COMM_
   return HPGQ_OK;
 }
 
+// out of place: the ctx's own counters keep accumulating, so repeated calls
+// (or batches after one) never count another rank's reads twice
 int hpgq_allreduce(hpgq_ctx_t *c) {
   if (!c) return HPGQ_E_INVALID;
   if (!c->comm) return HPGQ_E_STATE;
   HPGQ_HIP_TRY(hipSetDevice(c->device));
-  int rc = fold(c);
-  if (rc) return rc;
-  if (ncclAllReduce(c->d_counters, c->d_counters, c->clen * c->nm, ncclUint64, ncclSum, c->comm,
-                    c->stream) != ncclSuccess)
+  if (ncclAllReduce(c->d_state, c->d_global, c->clen * c->nm, ncclUint64, ncclSum, c->comm, c->stream) !=
+      ncclSuccess)
     return HPGQ_E_RCCL;
+  c->reduced = true;
   return HPGQ_OK;
 }
+
+uint64_t *hpgq_global_counters_device(hpgq_ctx_t *c) { return c ? c->d_global : nullptr; }
 
 // ---------------------------------------------------------------------------
 // derived summary (stats_counters_t view)

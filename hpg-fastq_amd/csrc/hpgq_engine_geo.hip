@@ -1,0 +1,59 @@
+// hpgq_engine_geo.hip — instances of the segmented kernel for ONE geometry
+// (built once per geometry with -DHPGQ_GEO=0|1|2, so the three compile in
+// parallel).  Occupancy per variant (MINW, waves per SIMD) is the highest at
+// which the variant's registers fit without spills: single-end 4 (tri 5),
+// paired-end 3 (two mates' accumulators), see DESIGN.md §4.1.
+#include <cstdio>
+
+#include "hpgq_engine_tri.h"
+
+#ifndef HPGQ_GEO
+#error "build with -DHPGQ_GEO=0 (tri), 1 (hex) or 2 (wide)"
+#endif
+
+namespace hpgq {
+
+namespace {
+
+constexpr int G = HPGQ_GEO;
+constexpr int kSeW = G == GEO_TRI ? 5 : 4;   // single-end
+constexpr int kPeW = 3;                      // paired-end
+constexpr const char *kGeoName = G == GEO_TRI ? "tri" : (G == GEO_HEX ? "hex" : "wide");
+
+template <bool F>
+SegChoice pick(int nm, bool edit, bool nx, char *name, size_t cap) {
+  constexpr int kSe = kSeW;
+  const void *fn = nullptr;
+  int w = nm == 2 ? kPeW : kSe;
+  if (nx) {
+    if (edit) return SegChoice{nullptr, 0};
+    fn = nm == 2 ? (const void *)engine_tri_x_kernel<kPeW, 2, G, F> : (const void *)engine_tri_x_kernel<kSe, 1, G, F>;
+    std::snprintf(name, cap, "hpgq::engine_tri_x_kernel<%d, %d, %s%s>", w, nm, kGeoName, F ? ", follow" : "");
+  } else {
+    if (edit && nm == 2) return SegChoice{nullptr, 0};
+    if (nm == 2) fn = (const void *)engine_tri_kernel<kPeW, 2, false, G, F>;
+    else if (edit) fn = (const void *)engine_tri_kernel<kSe, 1, true, G, F>;
+    else fn = (const void *)engine_tri_kernel<kSe, 1, false, G, F>;
+    std::snprintf(name, cap, "hpgq::engine_tri_kernel<%d, %d, %s, %s%s>", w, nm, edit ? "edit" : "filter", kGeoName,
+                  F ? ", follow" : "");
+  }
+  return SegChoice{fn, w};
+}
+
+}  // namespace
+
+#if HPGQ_GEO == 0
+SegChoice seg_kernel_tri(int nm, bool edit, bool nx, bool follow, char *name, size_t cap) {
+  return follow ? SegChoice{nullptr, 0} : pick<false>(nm, edit, nx, name, cap);
+}
+#elif HPGQ_GEO == 1
+SegChoice seg_kernel_hex(int nm, bool edit, bool nx, bool follow, char *name, size_t cap) {
+  return follow ? SegChoice{nullptr, 0} : pick<false>(nm, edit, nx, name, cap);
+}
+#else
+SegChoice seg_kernel_wide(int nm, bool edit, bool nx, bool follow, char *name, size_t cap) {
+  return follow ? pick<true>(nm, edit, nx, name, cap) : pick<false>(nm, edit, nx, name, cap);
+}
+#endif
+
+}  // namespace hpgq

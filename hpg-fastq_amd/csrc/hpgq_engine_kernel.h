@@ -1,4 +1,5 @@
-// hpgq_engine_kernel.h — the fused edit -> filter -> stats kernel (gfx950).
+// hpgq_engine_kernel.h — the fused edit -> filter -> stats kernels (gfx950):
+// shared arguments, read routing and the catch-all one-wave-per-read kernel.
 //
 // Replaces, for one SoA batch resident in HBM:
 //   fastq_edit          src/edit_fastq.c:154            (5'/3' trim)
@@ -6,35 +7,35 @@
 //   fastq_reads_stats   src/stats_fastq.c:230,244
 //   the consumer merge  src/stats_fastq.c:257-417       (per-read + per-base counters)
 //
-// Mapping: ONE WAVE PER READ, streaming straight from HBM (no LDS staging).
-//   * reads are taken 64 at a time (a "block"); the block prologue loads the
-//     64 read offsets coalesced (lane j <-> read j) and precomputes, per lane,
-//     the aligned byte offset and alignment of read j in both buffers.
+// Read routing.  A batch runs through a short chain of
+// kernels on the ctx stream.  The first (the segmented kernel of
+// hpgq_engine_tri.h) takes every read whose length fits its geometry and
+// DEFERS the others: per unit (one of its read blocks) it stores a 64-bit mask
+// of the deferred reads and counts them.  The next kernel in the chain walks
+// those masks instead of the batch (a "follow-up" stage); it exits at once when
+// the count is zero, which is the usual case.  The last stage is engine_kernel
+// below, which takes any read of any length, so every read is processed by
+// exactly one stage and the counters of all stages add up.
+//
+// engine_kernel mapping: ONE WAVE PER READ, streaming straight from HBM.
+//   * reads are taken per unit (64 reads, or the deferred reads of an earlier
+//     stage's unit, compacted); the unit prologue loads the read offsets (lane
+//     j <-> read j) and precomputes the aligned byte offsets and alignments.
 //   * per read, v_readlane puts those in SGPRs; lane l then loads ONE dword per
-//     buffer with a buffer_load (SRD bounds check instead of per-lane clamps;
-//     offset = SGPR read offset + lane*4) and takes its right neighbour's
-//     dword by DPP wave_shl:1; v_alignbyte realigns the window so lane l < 63
-//     holds positions 4l..4l+3 (+252c for chunk c).  Lane 63 only donates its
-//     word.
-//   * per-read sums (raw quality via v_sad_u8, G/C, N, out-of-range counts by
-//     SWAR zero-byte / byte-compare tests) are packed into one or two u32 and
+//     buffer and 252-position chunk with a buffer_load (SRD bounds check, offset
+//     = SGPR read offset + lane*4) and takes its right neighbour's dword by DPP
+//     wave_shl:1; v_alignbyte realigns so lane l < 63 holds positions 4l..4l+3.
+//   * per-read sums (raw quality via v_sad_u8, G/C, N, out-of-range counts) are
 //     reduced with DPP row_shr + row_bcast; the pass/fail decision is then
-//     wave-uniform 32-bit scalar arithmetic.
+//     wave-uniform scalar arithmetic.
 //   * per-position base counters: v_perm_b32 maps each base byte to a field
 //     shift; 5 six-bit fields (A,C,G,T,N) per position in one u32, quality
-//     sums as 16-bit pairs; every 63 reads flushed into per-workgroup LDS u32
-//     arrays (ds_add), no global atomics on the per-base path.
-//   * per-read results go to lane j of three VGPRs (v_writelane); the block
-//     epilogue does the histogram-key divisions, the LDS histogram atomics and
-//     the coalesced mask / trim stores vectorised over lanes.
-//   * loads are register-pipelined: group g+1 (kU reads) is in flight while
-//     group g is processed, across block boundaries; every group issue has a
-//     fixed load count so the compiler counts vmcnt statically.
-//   * at kernel end each workgroup adds its LDS partials into its own row of a
-//     u64 slab (plain RMW); a reduce kernel folds the rows when counters are read.
-// FAST instances (template GEN = false) handle the common filter (length and
-// mean-quality bounds) with stats; GEN = true adds N / out-of-range /
-// left/right windows / edit, selected at run time.
+//     sums as 16-bit pairs; every 63 reads flushed into per-workgroup LDS.
+//   * reads longer than the NCH chunks the pipeline holds take a chunk loop
+//     (long_trim / long_eval): filter and edit for any length; such a read is
+//     always longer than lmax, so stats count it as a long read (error).
+//   * the workgroup epilogue adds its LDS partials into the ctx counters with
+//     one no-return u64 global atomic per nonzero entry (no slab, no fold).
 // All arithmetic is integer; results are bit-identical to the oracle.
 #pragma once
 #include "hpgq_common.h"
@@ -50,7 +51,7 @@ constexpr int kChunk = 252;       // positions per chunk (63 lanes x 4)
 constexpr int F_FILTER = 1, F_EDIT = 2, F_STATS = 4, F_NEED_N = 8, F_NEED_OOR = 16, F_NEED_LR = 32,
               F_OOR_LO_NONE = 64, F_OOR_HI_NONE = 128, F_OOR_ALL = 256;
 
-// parameters only the rarer (GEN) paths read; copied into LDS at kernel start
+// parameters only the rarer paths read
 struct ColdParams {
   int left_len, min_left, max_left;
   int right_len, min_right, max_right;
@@ -67,13 +68,28 @@ struct EngineArgs {
   const int32_t *idx[2];
   uint8_t *mask;
   uint32_t *trim;
-  uint64_t *slab;        // [gridDim.x][nm * clen]
+  uint64_t *counters;    // [nm][clen], accumulated with global atomics
   int32_t *err;
   const ColdParams *cold;
-  int64_t num_reads;
+  int64_t num_reads;     // of the batch (data end, paired trim offset)
   int lmax, clen, phred, flags;
   // pass iff min_len <= wn <= max_len and min_q*wn <= S - phred*wn <= max_q*wn
   int min_len, max_len, min_q, max_q;   // min_q/max_q clamped so that *1260 fits int32
+  // ---- read routing (see the header comment) ----
+  // follow-up stage: unit u holds the reads u*unit_reads + b for the set bits b
+  // of unit_bits[u] & unit_and[u] (unit_and may be null); nullptr: this kernel
+  // takes the whole batch in units of its own block size
+  const uint64_t *unit_bits;
+  const uint64_t *unit_and;
+  int64_t nunits;
+  int unit_reads;
+  const uint32_t *pending;    // follow-up: reads deferred to this stage (0: exit at once)
+  uint32_t *pending_clear;    // follow-up: the same counter of the next call, zeroed here
+  // deferral out (segmented kernels): reads longer than defer_len go to the next
+  // stage: bits per unit (every unit this kernel visits stores its word) + count
+  uint64_t *defer_bits;
+  uint32_t *defer_count;
+  int defer_len;
 };
 
 // ---------------------------------------------------------------------------
@@ -115,6 +131,13 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
   return __builtin_amdgcn_readlane(v, 63);
 }
 
+// wave sum of per-lane u64 values (each < 2^58), in 16-bit slices
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t v) {
+  const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+  return (uint64_t)wave_sum(lo & 0xFFFFu) + ((uint64_t)wave_sum(lo >> 16) << 16) +
+         ((uint64_t)wave_sum(hi) << 32);
+}
+
 __device__ __forceinline__ int wave_min(int v) {
   const int big = 0x7FFFFFFF;
   v = min(v, __builtin_amdgcn_update_dpp(big, v, 0x111, 0xF, 0xF, false));
@@ -144,13 +167,88 @@ __device__ __forceinline__ uint32_t next_lane(uint32_t v) {
 
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
 
-// v[lane j] = val (val, j wave-uniform).  v_writelane takes the lane from M0:
-// two SGPR operands would break the constant-bus limit.
-__device__ __forceinline__ uint32_t put_lane(uint32_t v, uint32_t val, int j) {
-  asm volatile("s_mov_b32 m0, %2\n\ts_nop 0\n\tv_writelane_b32 %0, %1, m0"
-               : "+v"(v) : "s"(val), "s"(j) : "m0");
-  return v;
+__device__ __forceinline__ uint64_t uni64(uint64_t x) {
+  return (uint64_t)(uint32_t)uni((int)(uint32_t)x) | ((uint64_t)(uint32_t)uni((int)(uint32_t)(x >> 32)) << 32);
 }
+
+__device__ __forceinline__ uint64_t lanes_below(int lane) { return (1ull << lane) - 1ull; }
+
+// v[lane j] = val (j wave-uniform): a compare + select, no inline asm (the old
+// v_writelane form needed M0, which an asm clobber list cannot reserve)
+__device__ __forceinline__ uint32_t put_lane(uint32_t v, uint32_t val, int j) {
+  return (int)(threadIdx.x & 63) == j ? val : v;
+}
+
+// ---------------------------------------------------------------------------
+// units: the blocks of reads a wave takes in turn
+// ---------------------------------------------------------------------------
+
+// One unit: reads base + pos for the positions pos of `bits`, base = u *
+// (reads per unit); direct units have contiguous bits 0..nr-1 (bits unused).
+// u < 0: no unit (the pipeline's dummy).  32-bit: batches hold < 2^31 reads.
+struct Unit {
+  int u;
+  int nr;
+  uint64_t bits;
+};
+
+// Unit source of one wave: units u = gw, gw + nw, ... of BLOCK reads each.
+// Follow-up (FOLLOW): the same sequence over the earlier stage's units,
+// skipping those without deferred reads; each candidate's mask is one scalar
+// load (lgkmcnt: it never waits behind the wave's vector loads in flight; a
+// ballot over a vector-loaded window of masks cost the segmented kernel ~40
+// VGPRs and its occupancy).
+template <bool FOLLOW, int BLOCK>
+struct UnitIter {
+  int nw, nunits, num_reads, next_u;
+  const uint64_t *bits1, *bits2;
+  uint64_t held;   // positions a unit can hold (follow: the earlier stage's block)
+
+  __device__ __forceinline__ void init(const EngineArgs &A, int gw, int nw_) {
+    nw = nw_;
+    num_reads = (int)A.num_reads;
+    nunits = FOLLOW ? (int)A.nunits : (num_reads + BLOCK - 1) / BLOCK;
+    next_u = gw;
+    bits1 = A.unit_bits;
+    bits2 = A.unit_and;
+    held = FOLLOW && A.unit_reads < 64 ? (1ull << A.unit_reads) - 1ull : ~0ull;
+  }
+  __device__ __forceinline__ Unit next() {
+    for (;;) {
+      const int u = next_u;
+      if (u >= nunits) return Unit{-1, 0, 0};
+      next_u = u + nw;
+      if (!FOLLOW) return Unit{u, min(BLOCK, num_reads - u * BLOCK), 0ull};
+      uint64_t v = bits1[u] & held;
+      if (bits2) v &= bits2[u];
+      if (v) return Unit{u, __builtin_popcountll(v), v};
+    }
+  }
+};
+
+// read id of lane j (< U.nr) of unit U (first read `base`); scratch: 64 u32 of
+// per-wave LDS
+template <bool FOLLOW>
+__device__ __forceinline__ int unit_read(const Unit &U, int base, uint32_t *scratch) {
+  const int lane = threadIdx.x & 63;
+  if (!FOLLOW) return base + lane;
+  // compaction: the lane of each set bit writes its position to slot rank
+  if ((U.bits >> lane) & 1ull) scratch[__builtin_popcountll(U.bits & lanes_below(lane))] = (uint32_t)lane;
+  __builtin_amdgcn_wave_barrier();
+  const int pos = lane < U.nr ? (int)scratch[lane] : 0;
+  __builtin_amdgcn_wave_barrier();
+  return base + pos;
+}
+
+// a follow-up stage with nothing deferred to it exits at once (grid-uniform)
+__device__ __forceinline__ bool follow_up_idle(const EngineArgs &A) {
+  if (A.pending_clear && blockIdx.x == 0 && threadIdx.x == 0) *A.pending_clear = 0u;
+  return A.unit_bits != nullptr && uni((int)*A.pending) == 0;
+}
+
+// ---------------------------------------------------------------------------
+// base fields
+// ---------------------------------------------------------------------------
 
 // field shift per base code; code = byte & 7 is one-to-one on A,C,G,T,N:
 //   pad(0x08)->0 'A'->1 'C'->3 'T'->4 'N'->6 'G'->7, codes 2 and 5 unused
@@ -188,24 +286,29 @@ struct Pending {            // issued loads for one read of one mate
   uint32_t s[NCH], q[NCH];
 };
 
-// wave-uniform read descriptor, unpacked from the block prologue's lane j
+// wave-uniform read descriptor, unpacked from the unit prologue's lane j
 struct ReadRef {
   uint32_t os, oq;   // aligned byte offsets (dword) into the SRDs
   int als, alq;      // byte alignment of the read start
-  int n;             // length
+  int n;             // length (full 32 bits)
 };
 
-// loads: lane l, chunk c reads the dword at os + 4*(63c + l); reads past the
-// data end return 0 (SRD bound), past the read end they are garbage we mask
+// loads: lane l, chunk c reads the dword at os + 4*(63c + l) + c0; reads past
+// the data end return 0, past the read end they are garbage we mask.  The
+// whole offset goes in the VGPR operand: the SRD range check covers the vector
+// offset only (not soffset), and it is what keeps every load inside
+// [base, base + data end) -- the base of a batch with absolute offsets lies
+// before its allocation, so an unchecked offset below data_indices[0] would
+// read unmapped memory.
 template <int NCH>
 __device__ __forceinline__ void issue(const MateBuf &b, const ReadRef &r, uint32_t lane4,
-                                      Pending<NCH> &p) {
+                                      Pending<NCH> &p, int c0 = 0) {
   // readfirstlane: the offsets are uniform, say so (else hipcc may waterfall)
   const uint32_t os = (uint32_t)uni((int)r.os), oq = (uint32_t)uni((int)r.oq);
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
-    p.s[c] = __builtin_amdgcn_raw_buffer_load_b32(b.rs, lane4 + 252 * c, os, 0);
-    p.q[c] = __builtin_amdgcn_raw_buffer_load_b32(b.rq, lane4 + 252 * c, oq, 0);
+    p.s[c] = __builtin_amdgcn_raw_buffer_load_b32(b.rs, os + lane4 + kChunk * c + c0, 0, 0);
+    p.q[c] = __builtin_amdgcn_raw_buffer_load_b32(b.rq, oq + lane4 + kChunk * c + c0, 0, 0);
   }
 }
 
@@ -218,6 +321,18 @@ __device__ __forceinline__ void finish(const ReadRef &r, const Pending<NCH> &p,
     sw[c] = __builtin_amdgcn_alignbyte(next_lane(p.s[c]), p.s[c], (uint32_t)r.als);
     qw[c] = __builtin_amdgcn_alignbyte(next_lane(p.q[c]), p.q[c], (uint32_t)r.alq);
   }
+}
+
+// the read's window starting `ts` bases in
+__device__ __forceinline__ ReadRef shift_ref(const ReadRef &rr, int ts) {
+  ReadRef r2 = rr;
+  const uint32_t xs = rr.os + (uint32_t)(rr.als + ts), xq = rr.oq + (uint32_t)(rr.alq + ts);
+  r2.os = xs & ~3u;
+  r2.oq = xq & ~3u;
+  r2.als = (int)(xs & 3u);
+  r2.alq = (int)(xq & 3u);
+  r2.n = rr.n - ts;
+  return r2;
 }
 
 template <int NCH>
@@ -278,10 +393,16 @@ struct PosAcc {
 
 // per-read outcome (wave-uniform)
 struct ReadOut {
-  uint32_t r1;   // raw quality sum | GC << 18
+  uint32_t r1;   // raw quality sum | GC << 18 (reads <= NCH chunks)
   int wn, ts, te;
   bool pass;
 };
+
+// mean-quality window test min*k <= S - phred*k <= max*k in 64-bit arithmetic
+__device__ __forceinline__ bool mean_in(int64_t sraw, int64_t k, int phred, int lo, int hi) {
+  const int64_t s = sraw - (int64_t)phred * k;
+  return (int64_t)lo * k <= s && s <= (int64_t)hi * k;
+}
 
 template <bool GEN, int NCH>
 __device__ __forceinline__ ReadOut evaluate(const EngineArgs &A, const ColdParams &C,
@@ -338,14 +459,8 @@ __device__ __forceinline__ ReadOut evaluate(const EngineArgs &A, const ColdParam
         if ((A.flags & F_NEED_OOR) && (int)(r2 >> 16) > C.max_oor) pass = false;
       }
       if (A.flags & F_NEED_LR) {
-        if (kl > 0) {
-          const int64_t s = (int64_t)wave_sum(pl) - (int64_t)A.phred * kl;
-          if (!((int64_t)C.min_left * kl <= s && s <= (int64_t)C.max_left * kl)) pass = false;
-        }
-        if (kr > 0) {
-          const int64_t s = (int64_t)wave_sum(pr) - (int64_t)A.phred * kr;
-          if (!((int64_t)C.min_right * kr <= s && s <= (int64_t)C.max_right * kr)) pass = false;
-        }
+        if (kl > 0 && !mean_in(wave_sum(pl), kl, A.phred, C.min_left, C.max_left)) pass = false;
+        if (kr > 0 && !mean_in(wave_sum(pr), kr, A.phred, C.min_right, C.max_right)) pass = false;
       }
     }
   }
@@ -388,27 +503,136 @@ __device__ __forceinline__ void trim_read(const ColdParams &C, const uint32_t (&
   }
 }
 
-template <int NM, int NCH, bool GEN>
+// ---- reads longer than the pipeline's NCH chunks: one chunk at a time -------
+
+// one 252-position chunk [c0, c0 + 252) of read r (words of positions c0 + 4 lane ..)
+__device__ __forceinline__ void chunk_words(const MateBuf &b, const ReadRef &r, uint32_t lane4, int c0,
+                                            uint32_t &sw, uint32_t &qw) {
+  Pending<1> p;
+  issue<1>(b, r, lane4, p, c0);
+  sw = __builtin_amdgcn_alignbyte(next_lane(p.s[0]), p.s[0], (uint32_t)r.als);
+  qw = __builtin_amdgcn_alignbyte(next_lane(p.q[0]), p.q[0], (uint32_t)r.alq);
+}
+
+// edit (A6) trims of a read of any length (same rule as trim_read)
+__device__ __forceinline__ void long_trim(const ColdParams &C, const MateBuf &b, const ReadRef &r,
+                                       uint32_t lane4, int lane_p0, int &ts, int &te) {
+  const int n = r.n;
+  ts = 0;
+  te = 0;
+  uint32_t sw, qw;
+  if (C.e_left_len > 0) {
+    const int lim = min(C.e_left_len, n);
+    ts = lim;
+    for (int c0 = 0; c0 < lim; c0 += kChunk) {
+      chunk_words(b, r, lane4, c0, sw, qw);
+      const int p0 = c0 + lane_p0;
+      const uint32_t ok = in_range(qw, C.el_lo4, C.el_hi4, C.el_lo_none, C.el_hi_none, C.el_none_in) &
+                          byte_mask(lim - p0);
+      const int first = wave_min(ok ? p0 + (__builtin_ctz(ok) >> 3) : 0x7FFFFFFF);
+      if (first < lim) {
+        ts = first;
+        break;
+      }
+    }
+  }
+  if (C.e_right_len > 0) {
+    const int lim = min(C.e_right_len, n - ts);
+    const int lo = n - lim;
+    te = lim;
+    for (int c0 = ((n - 1) / kChunk) * kChunk; lim > 0 && c0 >= 0 && c0 + kChunk > lo; c0 -= kChunk) {
+      chunk_words(b, r, lane4, c0, sw, qw);
+      const int p0 = c0 + lane_p0;
+      const uint32_t ok = in_range(qw, C.er_lo4, C.er_hi4, C.er_lo_none, C.er_hi_none, C.er_none_in) &
+                          byte_mask(n - p0) & ~byte_mask(lo - p0);
+      const int last = wave_max(ok ? p0 + ((31 - __builtin_clz(ok)) >> 3) : -1);
+      if (last >= 0) {
+        te = n - 1 - last;
+        break;
+      }
+    }
+  }
+}
+
+// filter (A5) of the window r (its n = the window length) of any length
+__device__ __forceinline__ bool long_eval(const EngineArgs &A, const ColdParams &C, const MateBuf &b,
+                                       const ReadRef &r, uint32_t lane4, int lane_p0) {
+  if (!(A.flags & F_FILTER)) return true;
+  const int wn = r.n;
+  if (wn < A.min_len || wn > A.max_len) return false;
+  const bool lr = A.flags & F_NEED_LR;
+  const int kl = lr ? min(C.left_len, wn) : 0, kr = lr ? min(C.right_len, wn) : 0;
+  uint64_t sq = 0, sl = 0, sr = 0, nn = 0, oo = 0;
+  for (int c0 = 0; c0 < wn; c0 += kChunk) {
+    uint32_t sw, qw;
+    chunk_words(b, r, lane4, c0, sw, qw);
+    const int p0 = c0 + lane_p0;
+    const uint32_t m = byte_mask(wn - p0), m80 = m & 0x80808080u, q = qw & m;
+    sq += __builtin_amdgcn_sad_u8(q, 0u, 0u);
+    if (A.flags & F_NEED_N) nn += __builtin_popcount(zero_bytes(sw ^ 0x4E4E4E4Eu) & m80);
+    if (A.flags & F_NEED_OOR) {
+      uint32_t bad;
+      if (A.flags & F_OOR_ALL) {
+        bad = 0x80808080u;
+      } else {
+        bad = 0;
+        if (!(A.flags & F_OOR_LO_NONE)) bad |= ~ge_bytes(qw, C.oor_lo4) & 0x80808080u;
+        if (!(A.flags & F_OOR_HI_NONE)) bad |= ge_bytes(qw, C.oor_hi4);
+      }
+      oo += __builtin_popcount(bad & m80);
+    }
+    if (kl > 0) sl += __builtin_amdgcn_sad_u8(q & byte_mask(kl - p0), 0u, 0u);
+    if (kr > 0) sr += __builtin_amdgcn_sad_u8(q & ~byte_mask(wn - kr - p0), 0u, 0u);
+  }
+  bool pass = mean_in((int64_t)wave_sum64(sq), wn, A.phred, A.min_q, A.max_q);
+  if ((A.flags & F_NEED_N) && (int64_t)wave_sum64(nn) > C.max_n) pass = false;
+  if ((A.flags & F_NEED_OOR) && (int64_t)wave_sum64(oo) > C.max_oor) pass = false;
+  if (kl > 0 && !mean_in((int64_t)wave_sum64(sl), kl, A.phred, C.min_left, C.max_left)) pass = false;
+  if (kr > 0 && !mean_in((int64_t)wave_sum64(sr), kr, A.phred, C.min_right, C.max_right)) pass = false;
+  return pass;
+}
+
+// add one workgroup's partial counter set into the global counters: one
+// no-return u64 atomic per nonzero entry (set layout: include/hpgq.h)
+__device__ __forceinline__ void add_partials(uint64_t *dst, const unsigned long long *sc,
+                                             const uint32_t *hist, int hlen, const uint32_t *pos,
+                                             int lmax, int tid, int nthreads) {
+  for (int i = tid; i < HPGQ_NUM_SCALARS; i += nthreads)
+    if (sc[i]) atomicAdd(reinterpret_cast<unsigned long long *>(dst + i), sc[i]);
+  for (int i = tid; i < hlen; i += nthreads)
+    if (hist[i]) atomicAdd(reinterpret_cast<unsigned long long *>(dst + HPGQ_NUM_SCALARS + i),
+                           (unsigned long long)hist[i]);
+  uint64_t *dp = dst + HPGQ_NUM_SCALARS + hlen;
+  for (int i = tid; i < 6 * lmax; i += nthreads)
+    if (pos[i]) atomicAdd(reinterpret_cast<unsigned long long *>(dp + i), (unsigned long long)pos[i]);
+}
+
+template <int NM, int NCH, bool GEN, bool FOLLOW>
 __global__ void __launch_bounds__(kWG) engine_kernel(EngineArgs A) {
+  if (FOLLOW && follow_up_idle(A)) return;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = uni(tid >> 6);
   const int lmax = A.lmax;
   const int hlen = lmax + 1 + HPGQ_MEANQ_BINS + HPGQ_GC_BINS;
+  constexpr int kCap = kChunk * NCH;   // positions the pipelined loads hold
   // lane l < 63 owns positions 4l.. of every chunk; lane 63 none
   const int lane_p0 = lane < 63 ? 4 * lane : 0x40000000;
   const uint32_t lane4 = 4u * (uint32_t)lane;
+  const int ublock = FOLLOW ? A.unit_reads : 64;   // reads per unit
 
-  // LDS: pos_acc [NM][6][lmax] u32 | hist [NM][hlen] u32 | sc [NM][8] u64 | cold
+  // LDS: pos_acc [NM][6][lmax] u32 | hist [NM][hlen] u32 | sc [NM][8] u64 | cold |
+  //      per wave: compaction scratch [64] u32
   uint32_t *pos_acc = reinterpret_cast<uint32_t *>(lds);
   uint32_t *hist = pos_acc + NM * 6 * lmax;
   const int hist_words = (NM * hlen + 1) & ~1;
   unsigned long long *sc = reinterpret_cast<unsigned long long *>(hist + hist_words);
   ColdParams *cold = reinterpret_cast<ColdParams *>(sc + NM * HPGQ_NUM_SCALARS);
+  uint32_t *scratch = reinterpret_cast<uint32_t *>(cold + 1) + wave * 64;
   for (int i = tid; i < NM * 6 * lmax + hist_words; i += kWG) pos_acc[i] = 0;
   for (int i = tid; i < NM * HPGQ_NUM_SCALARS; i += kWG) sc[i] = 0;
-  if (GEN && tid < (int)(sizeof(ColdParams) / 4))
+  if (tid < (int)(sizeof(ColdParams) / 4))
     reinterpret_cast<uint32_t *>(cold)[tid] = reinterpret_cast<const uint32_t *>(A.cold)[tid];
   __syncthreads();
 
@@ -422,77 +646,78 @@ __global__ void __launch_bounds__(kWG) engine_kernel(EngineArgs A) {
   for (int m = 0; m < NM; ++m) acc[m].zero();
   int since_flush = 0;
   uint64_t fx16[NM];
-  uint32_t cnt[NM][7];   // input, passed, failed, edited, stats, long, any-long (wave-uniform)
+  uint32_t cnt[NM][6];   // input, passed, failed, edited, stats, long (wave-uniform)
 #pragma unroll
   for (int m = 0; m < NM; ++m) {
     fx16[m] = 0;
 #pragma unroll
-    for (int k = 0; k < 7; ++k) cnt[m][k] = 0;
+    for (int k = 0; k < 6; ++k) cnt[m][k] = 0;
   }
 
   // reads per pipeline group (two groups of registers in flight)
   constexpr int kU = ((NM == 1 ? 8 : 4) / NCH) > 0 ? ((NM == 1 ? 8 : 4) / NCH) : 1;
-  const int64_t nblocks = (A.num_reads + 63) / 64;
-  const int64_t gw = (int64_t)blockIdx.x * kWaves + wave;
-  const int64_t nw = (int64_t)gridDim.x * kWaves;
+  UnitIter<FOLLOW, 64> it;
+  it.init(A, (int)blockIdx.x * kWaves + wave, (int)gridDim.x * kWaves);
 
-  // block prologue: lane j describes read r0 + j of mate m
-  //   off_s/off_q: aligned byte offsets; info: n | als << 16 | alq << 20
-  auto load_block = [&](int64_t blk, uint32_t (&off_s)[NM], uint32_t (&off_q)[NM],
-                        uint32_t (&info)[NM]) {
-    const int64_t r0 = blk * 64;
-    const int nr = (int)min((int64_t)64, A.num_reads - r0);
-    const int l = min(lane, nr - 1);
+  // unit prologue: lane j describes read j of unit U for mate m
+  //   off_s/off_q: aligned byte offsets; al: als | alq << 2; len: length; rid: read id
+  auto load_block = [&](const Unit &U, uint32_t (&off_s)[NM], uint32_t (&off_q)[NM],
+                        uint32_t (&al)[NM], int32_t (&len)[NM], int &rid) __attribute__((always_inline)) {
+    rid = U.nr > 0 ? unit_read<FOLLOW>(U, U.u * ublock, scratch) : 0;
+    const bool on = lane < U.nr;
 #pragma unroll
     for (int m = 0; m < NM; ++m) {
-      const int a = A.idx[m][r0 + l], e = A.idx[m][r0 + l + 1];
-      const uint32_t xs = (uint32_t)(mb[m].bs + a), xq = (uint32_t)(mb[m].bq + a);
+      const int a = on ? A.idx[m][rid] : 0, e = on ? A.idx[m][rid + 1] : 0;
+      // absent reads (the pipeline's dummy unit): offsets past the SRD range
+      const uint32_t xs = on ? (uint32_t)(mb[m].bs + a) : 0x80000000u;
+      const uint32_t xq = on ? (uint32_t)(mb[m].bq + a) : 0x80000000u;
       off_s[m] = xs & ~3u;
       off_q[m] = xq & ~3u;
-      info[m] = (uint32_t)(e - a) | ((xs & 3u) << 16) | ((xq & 3u) << 20);
+      al[m] = (xs & 3u) | ((xq & 3u) << 2);
+      len[m] = e - a;
     }
   };
-  auto ref_of = [&](const uint32_t (&off_s)[NM], const uint32_t (&off_q)[NM],
-                    const uint32_t (&info)[NM], int m, int j) {
+  auto ref_of = [&](const uint32_t (&off_s)[NM], const uint32_t (&off_q)[NM], const uint32_t (&al)[NM],
+                    const int32_t (&len)[NM], int m, int j) __attribute__((always_inline)) {
     ReadRef r;
     r.os = __builtin_amdgcn_readlane(off_s[m], j);
     r.oq = __builtin_amdgcn_readlane(off_q[m], j);
-    const uint32_t inf = __builtin_amdgcn_readlane(info[m], j);
-    r.n = (int)(inf & 0xFFFFu);
-    r.als = (int)((inf >> 16) & 3u);
-    r.alq = (int)((inf >> 20) & 3u);
+    const uint32_t a = __builtin_amdgcn_readlane(al[m], j);
+    r.n = __builtin_amdgcn_readlane(len[m], j);
+    r.als = (int)(a & 3u);
+    r.alq = (int)((a >> 2) & 3u);
     return r;
   };
 
   Pending<NCH> grp[2][kU][NM];
-  auto load_group = [&](const uint32_t (&os)[NM], const uint32_t (&oq)[NM],
-                        const uint32_t (&inf)[NM], int nr, int g, int slot) {
+  auto load_group = [&](const uint32_t (&os)[NM], const uint32_t (&oq)[NM], const uint32_t (&al)[NM],
+                        const int32_t (&len)[NM], int nr, int g, int slot) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
-      const int j = min(g * kU + u, nr - 1);   // past the block end: reload the last read
+      const int j = max(min(g * kU + u, nr - 1), 0);   // past the unit end: reload the last read
 #pragma unroll
-      for (int m = 0; m < NM; ++m) issue<NCH>(mb[m], ref_of(os, oq, inf, m, j), lane4, grp[slot][u][m]);
+      for (int m = 0; m < NM; ++m) issue<NCH>(mb[m], ref_of(os, oq, al, len, m, j), lane4, grp[slot][u][m]);
     }
   };
 
-  uint32_t os[NM], oq[NM], inf[NM], osn[NM], oqn[NM], infn[NM];
-  int64_t blk = gw;
-  if (blk < nblocks) {
-    load_block(blk, os, oq, inf);
-    load_group(os, oq, inf, (int)min((int64_t)64, A.num_reads - blk * 64), 0, 0);
+  uint32_t os[NM], oq[NM], al[NM], osn[NM], oqn[NM], aln[NM];
+  int32_t ln[NM], lnn[NM];
+  int rid = 0, ridn = 0;
+  Unit cur = it.next();
+  if (cur.u >= 0) {
+    load_block(cur, os, oq, al, ln, rid);
+    load_group(os, oq, al, ln, cur.nr, 0, 0);
   }
-  for (; blk < nblocks; blk += nw) {
-    const int64_t r0 = blk * 64;
-    const int nr = (int)min((int64_t)64, A.num_reads - r0);
-    const int64_t nblk = blk + nw < nblocks ? blk + nw : blk;   // next block (or self)
-    const int nnr = (int)min((int64_t)64, A.num_reads - nblk * 64);
-    load_block(nblk, osn, oqn, infn);
-    // per-read results, lane j <-> read r0 + j
+  while (cur.u >= 0) {
+    const int nr = cur.nr;
+    const Unit nxt = it.next();
+    load_block(nxt, osn, oqn, aln, lnn, ridn);
+    // per-read results, lane j <-> read j of the unit
     uint32_t res_r1[NM], res_info[NM], res_trim[NM];
 #pragma unroll
     for (int m = 0; m < NM; ++m) res_r1[m] = res_info[m] = res_trim[m] = 0;
 
-    auto process_group = [&](int g, int slot) {
+    auto process_group = [&](int g, int slot) __attribute__((always_inline)) {
 #pragma unroll
       for (int u = 0; u < kU; ++u) {
         const int j = g * kU + u;
@@ -502,42 +727,47 @@ __global__ void __launch_bounds__(kWG) engine_kernel(EngineArgs A) {
         bool lng[NM];
 #pragma unroll
         for (int m = 0; m < NM; ++m) {
-          const ReadRef rr = ref_of(os, oq, inf, m, j);
+          const ReadRef rr = ref_of(os, oq, al, ln, m, j);
           finish<NCH>(rr, grp[slot][u][m], sw[m], qw[m]);
           int ts = 0, te = 0;
-          if (GEN && (A.flags & F_EDIT) && rr.n <= kChunk * NCH) {
-            trim_read<NCH>(*cold, qw[m], rr.n, lane_p0, ts, te);
-            if (ts > 0) {   // window no longer starts at the read start: realign
-              ReadRef r2 = rr;
-              const uint32_t xs = rr.os + (uint32_t)(rr.als + ts), xq = rr.oq + (uint32_t)(rr.alq + ts);
-              r2.os = xs & ~3u;
-              r2.oq = xq & ~3u;
-              r2.als = (int)(xs & 3u);
-              r2.alq = (int)(xq & 3u);
+          if (GEN && (A.flags & F_EDIT)) {
+            if (rr.n <= kCap) trim_read<NCH>(*cold, qw[m], rr.n, lane_p0, ts, te);
+            else long_trim(*cold, mb[m], rr, lane4, lane_p0, ts, te);
+            if (ts > 0 && rr.n - ts - te <= kCap) {   // window no longer starts at the read start: realign
+              const ReadRef r2 = shift_ref(rr, ts);
               Pending<NCH> p2;
               issue<NCH>(mb[m], r2, lane4, p2);
               finish<NCH>(r2, p2, sw[m], qw[m]);
             }
           }
           const int wn = rr.n - ts - te;
+          if (wn <= kCap) {
 #pragma unroll
-          for (int c = 0; c < NCH; ++c) mk[m][c] = byte_mask(wn - lane_p0 - kChunk * c);
-          out[m] = evaluate<GEN, NCH>(A, *cold, sw[m], qw[m], mk[m], wn, lane_p0);
+            for (int c = 0; c < NCH; ++c) mk[m][c] = byte_mask(wn - lane_p0 - kChunk * c);
+            out[m] = evaluate<GEN, NCH>(A, *cold, sw[m], qw[m], mk[m], wn, lane_p0);
+          } else {   // longer than the pipelined chunks (and than lmax): filter by chunk loop
+            ReadRef rw = shift_ref(rr, ts);
+            rw.n = wn;
+            out[m].r1 = 0;
+            out[m].wn = wn;
+            out[m].pass = long_eval(A, *cold, mb[m], rw, lane4, lane_p0);
+          }
           out[m].ts = ts;
           out[m].te = te;
-          lng[m] = rr.n > lmax;
+          lng[m] = wn > lmax;
         }
         bool pass = out[0].pass;
         if (NM == 2) pass = pass && out[NM - 1].pass;
 #pragma unroll
         for (int m = 0; m < NM; ++m) {
           if ((A.flags & F_STATS) && pass && !lng[m]) acc[m].add(sw[m], qw[m], mk[m]);
-          const uint32_t info = (uint32_t)out[m].wn | ((uint32_t)pass << 16) |
-                                ((uint32_t)lng[m] << 17) |
-                                ((uint32_t)(out[m].ts + out[m].te > 0) << 18);
+          // wn only feeds the histograms of reads <= lmax, so 16 bits suffice
+          const uint32_t info = (uint32_t)min(out[m].wn, 0xFFFF) | ((uint32_t)pass << 16) |
+                                ((uint32_t)lng[m] << 17) | ((uint32_t)(out[m].ts + out[m].te > 0) << 18);
           res_r1[m] = put_lane(res_r1[m], out[m].r1, j);
           res_info[m] = put_lane(res_info[m], info, j);
-          if (GEN) res_trim[m] = put_lane(res_trim[m], (uint32_t)out[m].ts | ((uint32_t)out[m].te << 16), j);
+          if (GEN)
+            res_trim[m] = put_lane(res_trim[m], (uint32_t)out[m].ts | ((uint32_t)out[m].te << 16), j);
         }
         if ((A.flags & F_STATS) && pass && ++since_flush == kFlushEvery) {
 #pragma unroll
@@ -547,22 +777,22 @@ __global__ void __launch_bounds__(kWG) engine_kernel(EngineArgs A) {
       }
     };
 
-    // group g of this block sits in slot g & 1; the group after the last one
-    // is the next block's group 0 (full blocks have an even group count, so it
-    // lands in slot 0, where the next block expects it)
+    // group g of this unit sits in slot g & 1; the group after the last one
+    // is the next unit's group 0 (full units have an even group count, so it
+    // lands in slot 0, where the next unit expects it)
     const int ngroups = (nr + kU - 1) / kU;
     for (int g = 0; g < ngroups; g += 2) {
-      if (g + 1 < ngroups) load_group(os, oq, inf, nr, g + 1, 1);
-      else load_group(osn, oqn, infn, nnr, 0, 1);
+      if (g + 1 < ngroups) load_group(os, oq, al, ln, nr, g + 1, 1);
+      else load_group(osn, oqn, aln, lnn, nxt.nr, 0, 1);
       process_group(g, 0);
       if (g + 1 < ngroups) {
-        if (g + 2 < ngroups) load_group(os, oq, inf, nr, g + 2, 0);
-        else load_group(osn, oqn, infn, nnr, 0, 0);
+        if (g + 2 < ngroups) load_group(os, oq, al, ln, nr, g + 2, 0);
+        else load_group(osn, oqn, aln, lnn, nxt.nr, 0, 0);
         process_group(g + 1, 1);
       }
     }
 
-    // ---- block epilogue, vectorised over lanes (lane j = read r0 + j) ------
+    // ---- unit epilogue, vectorised over lanes (lane j = read j) -------------
     const bool valid = lane < nr;
 #pragma unroll
     for (int m = 0; m < NM; ++m) {
@@ -572,14 +802,13 @@ __global__ void __launch_bounds__(kWG) engine_kernel(EngineArgs A) {
       const bool lg = valid && ((info >> 17) & 1u);
       const bool edited = valid && ((info >> 18) & 1u);
       if (valid) {
-        if (m == 0 && A.mask) A.mask[r0 + lane] = (uint8_t)pass;
-        if (A.trim) A.trim[(int64_t)m * A.num_reads + r0 + lane] = res_trim[m];
+        if (m == 0 && A.mask) A.mask[rid] = (uint8_t)pass;
+        if (A.trim) A.trim[(int64_t)m * A.num_reads + rid] = res_trim[m];
       }
       cnt[m][0] += (uint32_t)nr;
       cnt[m][1] += (uint32_t)__builtin_popcountll(__ballot(pass));
       cnt[m][2] += (uint32_t)__builtin_popcountll(__ballot(valid && !pass));
       cnt[m][3] += (uint32_t)__builtin_popcountll(__ballot(edited));
-      cnt[m][6] += (uint32_t)__builtin_popcountll(__ballot(lg));
       if (A.flags & F_STATS) {
         cnt[m][4] += (uint32_t)__builtin_popcountll(__ballot(pass));
         cnt[m][5] += (uint32_t)__builtin_popcountll(__ballot(pass && lg));
@@ -601,8 +830,11 @@ __global__ void __launch_bounds__(kWG) engine_kernel(EngineArgs A) {
     for (int m = 0; m < NM; ++m) {
       os[m] = osn[m];
       oq[m] = oqn[m];
-      inf[m] = infn[m];
+      al[m] = aln[m];
+      ln[m] = lnn[m];
     }
+    rid = ridn;
+    cur = nxt;
   }
 
   // ---- workgroup epilogue ---------------------------------------------------
@@ -610,10 +842,7 @@ __global__ void __launch_bounds__(kWG) engine_kernel(EngineArgs A) {
   for (int m = 0; m < NM; ++m) acc[m].flush(pos_acc + m * 6 * lmax, lmax, lane_p0);
 #pragma unroll
   for (int m = 0; m < NM; ++m) {
-    // fx16: u64 per lane -> wave sum in 16-bit slices (no overflow)
-    const uint32_t lo = (uint32_t)fx16[m], hi = (uint32_t)(fx16[m] >> 32);
-    const uint64_t tot = (uint64_t)wave_sum(lo & 0xFFFFu) + ((uint64_t)wave_sum(lo >> 16) << 16) +
-                         ((uint64_t)wave_sum(hi) << 32);
+    const uint64_t tot = wave_sum64(fx16[m]);
     if (lane == 0) {
       unsigned long long *scm = sc + m * HPGQ_NUM_SCALARS;
       if (cnt[m][0]) atomicAdd(&scm[HPGQ_S_NUM_INPUT], (unsigned long long)cnt[m][0]);
@@ -623,33 +852,14 @@ __global__ void __launch_bounds__(kWG) engine_kernel(EngineArgs A) {
       if (cnt[m][4]) atomicAdd(&scm[HPGQ_S_NUM_STATS], (unsigned long long)cnt[m][4]);
       if (cnt[m][5]) atomicAdd(&scm[HPGQ_S_LONG_READS], (unsigned long long)cnt[m][5]);
       if (tot) atomicAdd(&scm[HPGQ_S_ACC_MEANQ_FX16], (unsigned long long)tot);
-      if (cnt[m][6] && A.err) atomicOr(A.err, 1);
+      // a merged read the per-position counters cannot hold: the call fails
+      if (cnt[m][5] && A.err) atomicOr(A.err, 1);
     }
   }
   __syncthreads();
-  // add this workgroup's partials into its slab row (no other block touches it)
-  uint64_t *row = A.slab + (size_t)blockIdx.x * NM * A.clen;
-  const int off_pos = HPGQ_NUM_SCALARS + hlen;
-  for (int m = 0; m < NM; ++m) {
-    uint64_t *rm = row + (size_t)m * A.clen;
-    for (int i = tid; i < HPGQ_NUM_SCALARS; i += kWG) rm[i] += sc[m * HPGQ_NUM_SCALARS + i];
-    for (int i = tid; i < hlen; i += kWG) rm[HPGQ_NUM_SCALARS + i] += hist[m * hlen + i];
-    for (int i = tid; i < 6 * lmax; i += kWG) rm[off_pos + i] += pos_acc[m * 6 * lmax + i];
-  }
-}
-
-// fold the slab rows into the counters and clear them:
-//   counters[k] += sum_rows slab[row][k]; slab[row][k] = 0
-__global__ void __launch_bounds__(256) slab_reduce_kernel(uint64_t *slab, int rows, int len,
-                                                          uint64_t *counters) {
-  const int k = blockIdx.x * 256 + threadIdx.x;
-  if (k >= len) return;
-  uint64_t s = 0;
-  for (int r = 0; r < rows; ++r) {
-    s += slab[(size_t)r * len + k];
-    slab[(size_t)r * len + k] = 0;
-  }
-  counters[k] += s;
+  for (int m = 0; m < NM; ++m)
+    add_partials(A.counters + (size_t)m * A.clen, sc + m * HPGQ_NUM_SCALARS, hist + m * hlen, hlen,
+                 pos_acc + m * 6 * lmax, lmax, tid, kWG);
 }
 
 }  // namespace hpgq

@@ -1,74 +1,77 @@
-// hpgq_engine_tri.h — FAST single-end stats/filter kernel, three reads per wave.
+// hpgq_engine_tri.h — the FAST segmented stats/filter/edit kernel: several
+// reads per wave step.
 //
-// Same contract and outputs as engine_kernel<1, *, false> (hpgq_engine_kernel.h)
-// for batches whose reads are at most 160 bases: the per-read fixed cost (the
-// DPP reduction, the pass/fail decision, bookkeeping) is shared by three reads
-// and lane utilisation goes from 38/64 to 57/64 at 150 bp.  The kernel is
-// VALU-issue bound (PMC: ~80% VALU busy at 13.9 Greads/s with the previous
-// per-position field scheme), so everything below counts VALU instructions
-// (15.3 Greads/s with this one at 5 waves/SIMD).
+// Same contract and outputs as engine_kernel (hpgq_engine_kernel.h) for the
+// reads whose length fits the geometry; longer reads are DEFERRED to the next
+// stage of the chain (unit masks + a count, see hpgq_engine_kernel.h), so the
+// kernel can run first on any batch.  The per-read fixed cost (the DPP scan,
+// the pass/fail decision, bookkeeping) is shared by the reads of a step.  The
+// kernel is close to VALU-issue bound, so everything below counts VALU
+// instructions.
 //
-//   * the wave is cut into 3 segments of 21 lanes (lanes 20, 41, 62, 63 own no
-//     positions); segment k works on read 3t + k of the block and lane ls < 20
-//     of a segment owns positions 8ls..8ls+7 (160 per read).
-//   * the block prologue writes one 16-byte record per read (dword-aligned seq
+// Geometries (Geo<G>): a wave step holds kSegs reads, each owning a segment of
+// kSegW lanes; a lane of a segment owns 4*NW consecutive positions.
+//   tri  (G 0): 3 x 21 lanes x  8 B, reads <= 160, 54-read blocks
+//   hex  (G 1): 6 x 10 lanes x 16 B, reads <= 156, 48-read blocks (1 KB per
+//               wave-load: ~10 % more streaming rate than tri,
+//               tools/ubench/stream_rates.hip)
+//   wide (G 2): 4 x 16 lanes x 16 B, reads <= 252, 60-read blocks (250 bp
+//               reads fill 98 % of the lanes)
+//   * the unit prologue writes one 16-byte record per read (dword-aligned seq
 //     and qual offsets, length | alignments) into a per-wave LDS table; each
 //     lane fetches its segment's record with ONE ds_read_b128, issues ONE
-//     buffer_load_dwordx2 per buffer and realigns with DPP wave_shl:1 +
-//     v_alignbyte (UNAL = true loads unaligned windows instead: fewer VALU,
-//     but measured ~15% slower in the address/data path).  The SRDs cover
-//     data_end + 8 bytes (the slack the C-ABI requires of device buffers).
+//     buffer load per buffer and realigns with DPP wave_shl:1 + v_alignbyte
+//     (the last lane of a segment borrows from the next segment, which only
+//     reaches positions >= kPos).  Deferred and absent reads get offsets past
+//     the SRD range, so their loads cost no memory traffic.
 //   * base classification: code = byte & 7 (one-to-one on A,C,G,T,N; masked
 //     bytes -> 0), then three v_perm_b32 LUTs: the expected byte (exact-match
 //     check; lowercase / IUPAC / other bytes take a rare path and count as
 //     "other"), C|G<<4 and A|T<<4 nibble one-hots.  G+C per read = popcount of
 //     the C|G word.  N is not counted: the workgroup epilogue derives it as
 //     count - A - C - G - T - other, count from the length histogram.
-//   * nibble counters (<= 15 triples) are widened into 8-bit per-base counters
-//     (<= 255 triples) and those flushed to LDS u32 arrays (ds_add); quality
+//   * nibble counters (<= 15 steps) are widened into 8-bit per-base counters
+//     (<= 255 steps) and those flushed to LDS u32 arrays (ds_add); quality
 //     sums are 16-bit pairs.
 //   * per-read sums (raw quality | G+C << 18) use ONE inclusive DPP prefix scan
-//     for the three segments; lanes 20, 41, 62 store the segment ends to LDS
-//     (no wait) and the block epilogue takes differences.
+//     for the wave; the last lane of each segment stores its segment end to
+//     LDS (no wait) and the block epilogue takes differences.  (Per wave at
+//     most 64 x 16 x 255 < 2^18 quality units: the fields never carry.)
 //   * every read is accumulated; the epilogue decides pass/fail for the block
 //     vectorised over lanes and takes the failed reads back out.
-// The stats layout, histogram rules and workgroup epilogue are identical, so
-// the two kernels are interchangeable (the tests run both against the oracle).
+// The stats layout, histogram rules and counter epilogue are those of
+// engine_kernel, so all kernels of a chain add into one counter set.
 #pragma once
 #include "hpgq_engine_kernel.h"
 
 namespace hpgq {
 
-constexpr int kTriPos = 160;    // positions per segment (tri: 20 owning lanes x 8)
-constexpr int kHexPos = 156;    // hex: 10 lanes x 16, the last lane's realignment stops at 156
 constexpr int kTriSlack = 8;    // readable bytes past the data end the loads may touch
 
-// Segment geometry by dwords per lane (NW):
-//   NW = 2 ("tri"): 3 segments of 21 lanes, 20 owning 8 positions (8-byte loads);
-//                   lane 20 loads the continuation its neighbour's realignment needs
-//   NW = 4 ("hex"): 6 segments of 10 lanes, each owning 16 positions (16-byte loads:
-//                   1 KB per wave-load, ~10 % more streaming rate than the tri shape,
-//                   tools/ubench/stream_rates.hip); lanes 60-63 idle; reads <= 156
-// kBlock reads (<= 64: lane j <-> read j in the epilogue) in steps of kSegs reads,
-// kU steps per pipeline group, an even number of groups per block.
-template <int NW>
+constexpr int GEO_TRI = 0, GEO_HEX = 1, GEO_WIDE = 2;
+
+// kBlock reads (<= 64: lane j <-> read j in the epilogue) in steps of kSegs
+// reads, kU steps per pipeline group, an even number of groups per block.
+template <int G>
 struct Geo;
 template <>
-struct Geo<2> {
-  static constexpr int kSegs = 3, kSegW = 21, kOwn = 20, kBlock = 54, kU = 3, kPos = kTriPos;
+struct Geo<GEO_TRI> {
+  static constexpr int kNW = 2, kSegs = 3, kSegW = 21, kOwn = 20, kBlock = 54, kU = 3, kPos = 160;
 };
 template <>
-struct Geo<4> {
-  static constexpr int kSegs = 6, kSegW = 10, kOwn = 10, kBlock = 48, kU = 2, kPos = kHexPos;
+struct Geo<GEO_HEX> {
+  static constexpr int kNW = 4, kSegs = 6, kSegW = 10, kOwn = 10, kBlock = 48, kU = 2, kPos = 156;
 };
-constexpr int kTriBlock = Geo<2>::kBlock;
-constexpr int kHexBlock = Geo<4>::kBlock;
+template <>
+struct Geo<GEO_WIDE> {   // 60-read blocks: read-table entry 63 stays empty (the padding steps' source)
+  static constexpr int kNW = 4, kSegs = 4, kSegW = 16, kOwn = 16, kBlock = 60, kU = 2, kPos = 252;
+};
 
-template <int NW>
+template <int G>
 constexpr uint64_t not_seg_first_mask() {   // lanes j with j % kSegs != 0
   uint64_t m = 0;
   for (int j = 0; j < 64; ++j)
-    if (j % Geo<NW>::kSegs) m |= 1ull << j;
+    if (j % Geo<G>::kSegs) m |= 1ull << j;
   return m;
 }
 constexpr int kNibbleEvery = 15;   // 4-bit counters
@@ -87,8 +90,8 @@ typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
 template <int NW>
 struct TriPending {
-  uint32_t s[NW], q[NW];   // the lane's 4*NW bytes of seq / quality (raw dwords if aligned loads)
-  uint32_t n;              // its read's length (| als << 16 | alq << 20 if aligned loads)
+  uint32_t s[NW], q[NW];   // the lane's 4*NW bytes of seq / quality (raw dwords)
+  uint32_t n;              // its read's length | als << 16 | alq << 20
 };
 
 __device__ __forceinline__ uint32_t next_lane0(uint32_t v) {   // lane i <- lane i+1, lane 63 <- 0
@@ -104,15 +107,6 @@ __device__ __forceinline__ uint32_t wave_scan(uint32_t v) {
   v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xA, 0xF, false);
   v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xC, 0xF, false);
   return v;
-}
-
-// masks of the lane's NW words: bytes at positions < n (nv = n - p0)
-template <int NW>
-__device__ __forceinline__ void tri_masks(int nv, uint32_t (&m)[NW]) {
-  const int e = 32 - 8 * nv;   // right shift of 0x00000000FFFFFFFF giving m[0]
-  const uint64_t ones = 0xFFFFFFFFull;
-#pragma unroll
-  for (int w = 0; w < NW; ++w) m[w] = (uint32_t)(ones >> min(max(e + 32 * w, 0), 32));
 }
 
 // 0xFF in every byte of d that is non-zero
@@ -134,7 +128,7 @@ struct TriAcc {
       q02[w] = q13[w] = 0;
     }
   }
-  // nibbles -> bytes (every <= 15 triples and before any subtraction)
+  // nibbles -> bytes (every <= 15 steps and before any subtraction)
   __device__ __forceinline__ void widen() {
 #pragma unroll
     for (int w = 0; w < NW; ++w) {
@@ -147,7 +141,7 @@ struct TriAcc {
   }
   // bytes -> LDS (pos_acc [6][lmax]: qsum, A, C, G, T, N/other); nibbles empty
   __device__ __forceinline__ void flush(uint32_t *pos_acc, int lmax, int p0) {
-    // rare (every <= 255 triples): keep its 40 LDS addresses out of the hot
+    // rare (every <= 255 steps): keep its 40 LDS addresses out of the hot
     // loop's registers (hipcc would hoist them as loop invariants and spill)
     asm volatile("" : "+v"(p0), "+s"(lmax), "+s"(pos_acc));
 #pragma unroll
@@ -172,10 +166,8 @@ struct TriAcc {
 // codes of a masked word; marks bytes that are not exactly A/C/G/T/N
 __device__ __forceinline__ uint32_t tri_codes(uint32_t s, uint32_t m, uint32_t &bad) {
   const uint32_t codes = s & m & 0x07070707u;
-#if HPGQ_TRI_ABL != 1   // (1: timing probe only, no exactness check)
   const uint32_t ex = __builtin_amdgcn_perm(kX7Hi, kX7Lo, codes);
   bad |= (s ^ ex) & m;
-#endif
   return codes;
 }
 
@@ -201,28 +193,30 @@ struct TriTag {
 using AddTag = TriTag<false>;
 using SubTag = TriTag<true>;
 
-// MINW: minimum waves per SIMD the register allocation must allow (occupancy)
-// ---- edit (A6) on the three-read kernel --------------------------------------
+// ---- edit (A6) on the segmented kernel ---------------------------------------
 // The trim of one read: the leading run of out-of-range qualities within the
 // first min(edit_left_length, n) bases and the trailing run within the last
 // min(edit_right_length, n - ts) with the SWAR in_range
 // test, from three 16-byte loads issued together for windows up to 16 / 32
-// bytes (else 8 bytes at a time); quality bytes [off, off + n) of rq.  Returns ts | te << 16,
-// the edit output.  Called by the block prologue (one lane per read), so the
-// lines it touches are still in L2 when the block's triples stream the read.
+// bytes (else 8 bytes at a time); quality bytes [off, off + n) of rq.  Returns
+// ts | te << 16, the edit output.  Called by the unit prologue (one lane per
+// read), so the lines it touches are still in L2 when the steps stream the read.
 __device__ __forceinline__ uint32_t trim_word(const ColdParams &C, __amdgpu_buffer_rsrc_t rq,
                                               int off, int n) {
-  auto ok8 = [&](int pos, bool right) -> uint64_t {   // 0x80 per in-range byte of [pos, pos+8)
-    const v2u w = __builtin_amdgcn_raw_buffer_load_b64(rq, (uint32_t)(off + pos), 0, 0);
+  auto ok_of = [&](uint32_t x, uint32_t y, bool right) __attribute__((always_inline)) -> uint64_t {   // 0x80 per in-range byte
     uint32_t lo, hi;
     if (!right) {
-      lo = in_range(w.x, C.el_lo4, C.el_hi4, C.el_lo_none, C.el_hi_none, C.el_none_in);
-      hi = in_range(w.y, C.el_lo4, C.el_hi4, C.el_lo_none, C.el_hi_none, C.el_none_in);
+      lo = in_range(x, C.el_lo4, C.el_hi4, C.el_lo_none, C.el_hi_none, C.el_none_in);
+      hi = in_range(y, C.el_lo4, C.el_hi4, C.el_lo_none, C.el_hi_none, C.el_none_in);
     } else {
-      lo = in_range(w.x, C.er_lo4, C.er_hi4, C.er_lo_none, C.er_hi_none, C.er_none_in);
-      hi = in_range(w.y, C.er_lo4, C.er_hi4, C.er_lo_none, C.er_hi_none, C.er_none_in);
+      lo = in_range(x, C.er_lo4, C.er_hi4, C.er_lo_none, C.er_hi_none, C.er_none_in);
+      hi = in_range(y, C.er_lo4, C.er_hi4, C.er_lo_none, C.er_hi_none, C.er_none_in);
     }
     return (uint64_t)lo | ((uint64_t)hi << 32);
+  };
+  auto ok8 = [&](int pos, bool right) __attribute__((always_inline)) -> uint64_t {
+    const v2u w = __builtin_amdgcn_raw_buffer_load_b64(rq, (uint32_t)(off + pos), 0, 0);
+    return ok_of(w.x, w.y, right);
   };
   auto low_bytes = [](int k) -> uint64_t { return k >= 8 ? ~0ull : ((1ull << (8 * max(k, 0))) - 1); };
   int ts = 0, te = 0;
@@ -230,17 +224,6 @@ __device__ __forceinline__ uint32_t trim_word(const ColdParams &C, __amdgpu_buff
     // the usual windows: all loads at once, the runs found in registers
     // (right: [pb, pb + 32) with pb = n - 32, or 0 for a short read so no load
     // starts before the read's own offset)
-    auto ok_of = [&](uint32_t x, uint32_t y, bool right) -> uint64_t {
-      uint32_t lo, hi;
-      if (!right) {
-        lo = in_range(x, C.el_lo4, C.el_hi4, C.el_lo_none, C.el_hi_none, C.el_none_in);
-        hi = in_range(y, C.el_lo4, C.el_hi4, C.el_lo_none, C.el_hi_none, C.el_none_in);
-      } else {
-        lo = in_range(x, C.er_lo4, C.er_hi4, C.er_lo_none, C.er_hi_none, C.er_none_in);
-        hi = in_range(y, C.er_lo4, C.er_hi4, C.er_lo_none, C.er_hi_none, C.er_none_in);
-      }
-      return (uint64_t)lo | ((uint64_t)hi << 32);
-    };
     const int pb = n >= 32 ? n - 32 : 0;
     const v4u wl = C.e_left_len > 0 ? __builtin_amdgcn_raw_buffer_load_b128(rq, (uint32_t)off, 0, 0)
                                     : v4u{0u, 0u, 0u, 0u};
@@ -301,33 +284,36 @@ struct MateTag {
   static constexpr int value = M;
 };
 
-// UNAL: unaligned 8-byte loads at the read's byte offset; else dword-aligned
-// loads realigned with DPP wave_shl:1 + v_alignbyte.
-// NM = 2: paired-end.  A block is 54 pairs; the wave runs mate 1's triples,
-// then mate 2's, each mate with its own accumulators / LDS partials / counter
-// set; the epilogue takes the pair decision (both mates pass) and subtracts
-// failed pairs from both sets.
-// EDIT (NM = 1): the block prologue trims each read (trim_word, written to
+// MINW: minimum waves per SIMD the register allocation must allow (occupancy).
+// NM = 2: paired-end.  A block is one block's worth of pairs; the wave runs
+// mate 1's steps, then mate 2's, each mate with its own accumulators / LDS
+// partials / counter set; the epilogue takes the pair decision (both mates
+// pass) and subtracts failed pairs from both sets.
+// EDIT (NM = 1): the unit prologue trims each read (trim_word, written to
 // A.trim when the caller wants it) and describes it by its window [ts, n - te)
 // (offset + ts, length n - ts - te): stats and filter see the trimmed read.
 // NX: the filter also counts N bases and out-of-range qualities per read
 // (max_N, max_out_of_quality; src/filter_fastq.c): a second per-step scan
-// of (N | out-of-range << 16), its segment ends in a second LDS list
-template <int MINW, bool UNAL, int NM, bool EDIT, int NW, bool NX>
+// of (N | out-of-range << 16), its segment ends in a second LDS list.
+// FOLLOW: a follow-up stage (reads deferred by the stage before, by unit masks).
+template <int MINW, int NM, bool EDIT, int G, bool NX, bool FOLLOW>
 __device__ __forceinline__ void tri_body(const EngineArgs &A) {
-  static_assert(!EDIT || NM == 1, "edit on the three-read kernel is single-end");
+  static_assert(!EDIT || NM == 1, "edit on the segmented kernel is single-end");
   static_assert(!(NX && EDIT), "the N / out-of-range filter variant does not edit");
-  using G = Geo<NW>;
-  constexpr int kSegs = G::kSegs, kSegW = G::kSegW, kBlock = G::kBlock, kU = G::kU;
+  using GG = Geo<G>;
+  constexpr int NW = GG::kNW, kSegs = GG::kSegs, kSegW = GG::kSegW, kBlock = GG::kBlock, kU = GG::kU;
+  static_assert(4 * kU <= kNibbleEvery && kBlock / kSegs - 4 * kU <= kNibbleEvery, "nibble widening");
+  static_assert(kSegs * kSegW <= 64 && kBlock < 64 && kBlock % kSegs == 0, "geometry");
+  if (FOLLOW && follow_up_idle(A)) return;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = uni(tid >> 6);
   const int lmax = A.lmax;
   const int hlen = lmax + 1 + HPGQ_MEANQ_BINS + HPGQ_GC_BINS;
-  const int seg = min(lane / kSegW, kSegs);     // kSegs: idle lanes (tri: 63; hex: 60-63)
+  const int seg = min(lane / kSegW, kSegs);     // kSegs: idle lanes
   const int ls = lane - seg * kSegW;
-  const bool owner = seg < kSegs && ls < G::kOwn;
+  const bool owner = seg < kSegs && ls < GG::kOwn;
   const int p0 = owner ? 4 * NW * ls : (1 << 26);   // first position of this lane (8*p0 fits int32)
   const uint32_t lane8 = 4u * NW * (uint32_t)ls;   // byte offset of this lane's window
   const bool stats = A.flags & F_STATS, filter = A.flags & F_FILTER;
@@ -338,35 +324,37 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   const int x_maxn = NX ? uni(A.cold->max_n) : 0, x_maxo = NX ? uni(A.cold->max_oor) : 0;
   const bool x_n = NX && (A.flags & F_NEED_N), x_o = NX && (A.flags & F_NEED_OOR);
   const bool x_all = A.flags & F_OOR_ALL, x_lonone = A.flags & F_OOR_LO_NONE, x_hinone = A.flags & F_OOR_HI_NONE;
-#ifndef HPGQ_TRI_COLD_COPY
-#define HPGQ_TRI_COLD_COPY 1
-#endif
   // EDIT: the trim bounds, read once (see NX above)
   ColdParams cold{};
-  if (EDIT && HPGQ_TRI_COLD_COPY) cold = *A.cold;
+  if (EDIT) cold = *A.cold;
   // raw-sum bounds: pass iff min_len <= n <= max_len and lo_r*n <= S <= hi_r*n
   const int lo_r = A.min_q + A.phred, hi_r = A.max_q + A.phred;
+  const int dlim = A.defer_len;   // longer reads go to the next stage
 
   // LDS per mate: pos_acc [6][lmax] u32 | hist [hlen] u32 | sc [8] u64, then
   // per wave: per mate two read tables [64] x 16 B (seq offset, qual offset,
   // length | alignments, -) alternating between blocks, and segment ends [64]
+  // (+ [64] NX), then a compaction scratch [64] u32 and a deferral word (u64,
+  // disjoint from the scratch: no type-punned aliasing); then the byte-mask table.
   // (pos_acc row 5 holds "other" counts until the epilogue turns it into N)
   const int hist_words = (hlen + 1) & ~1;
   const int mate_words = 6 * lmax + hist_words + 2 * HPGQ_NUM_SCALARS;   // even: sc 8-B aligned
   uint32_t *base = reinterpret_cast<uint32_t *>(lds);
-  auto pos_acc = [&](int m) { return base + m * mate_words; };
-  auto other = [&](int m) { return base + m * mate_words + 5 * lmax; };
-  auto hist = [&](int m) { return base + m * mate_words + 6 * lmax; };
-  auto sc = [&](int m) {
+  auto pos_acc = [&](int m) __attribute__((always_inline)) { return base + m * mate_words; };
+  auto other = [&](int m) __attribute__((always_inline)) { return base + m * mate_words + 5 * lmax; };
+  auto hist = [&](int m) __attribute__((always_inline)) { return base + m * mate_words + 6 * lmax; };
+  auto sc = [&](int m) __attribute__((always_inline)) {
     return reinterpret_cast<unsigned long long *>(base + m * mate_words + 6 * lmax + hist_words);
   };
   constexpr int kMateWaveWords = 2 * 256 + (NX ? 128 : 64);
-  constexpr int kWaveWords = NM * kMateWaveWords;
+  constexpr int kWaveWords = NM * kMateWaveWords + 64 + 4;   // (multiple of 4: 16 B tables)
   const int tab_words = (NM * mate_words + 3) & ~3;   // 16 B aligned (host: + 16 B)
   uint32_t *wtab = base + tab_words + wave * kWaveWords;
-  auto tab = [&](int m, int tb) { return wtab + m * kMateWaveWords + tb * 256; };
-  auto wends = [&](int m) { return wtab + m * kMateWaveWords + 2 * 256; };
-  auto wends2 = [&](int m) { return wtab + m * kMateWaveWords + 2 * 256 + 64; };   // NX only
+  auto tab = [&](int m, int tb) __attribute__((always_inline)) { return wtab + m * kMateWaveWords + tb * 256; };
+  auto wends = [&](int m) __attribute__((always_inline)) { return wtab + m * kMateWaveWords + 2 * 256; };
+  auto wends2 = [&](int m) __attribute__((always_inline)) { return wtab + m * kMateWaveWords + 2 * 256 + 64; };   // NX only
+  uint32_t *scratch = wtab + NM * kMateWaveWords;
+  unsigned long long *dword = reinterpret_cast<unsigned long long *>(scratch + 64);   // 8 B aligned
   // byte masks by valid-byte count c = clamp(n - p0, 0, 4 NW): mtab[c][w]
   // (one LDS read per step instead of a clamp and a 64-bit shift per word)
   uint32_t *mtab = base + tab_words + kWaves * kWaveWords;   // 16 B aligned
@@ -384,8 +372,8 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   for (int m = 0; m < NM; ++m) {
     const int data_end = uni(A.idx[m][A.num_reads]);
     const uintptr_t ps = reinterpret_cast<uintptr_t>(A.seq[m]), pq = reinterpret_cast<uintptr_t>(A.qual[m]);
-    bs[m] = UNAL ? 0 : (int)(ps & 3);
-    bq[m] = UNAL ? 0 : (int)(pq & 3);
+    bs[m] = (int)(ps & 3);
+    bq[m] = (int)(pq & 3);
     rs[m] = __builtin_amdgcn_make_buffer_rsrc((void *)(ps - bs[m]), (short)0,
                                               bs[m] + data_end + kTriSlack, 0x00020000);
     rq[m] = __builtin_amdgcn_make_buffer_rsrc((void *)(pq - bq[m]), (short)0,
@@ -394,62 +382,86 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   TriAcc<NW> acc[NM];
 #pragma unroll
   for (int m = 0; m < NM; ++m) acc[m].zero();
-  int since_flush = 0;   // triples per mate added since the last LDS flush (a byte grows <= 1 per triple)
+  int since_flush = 0;   // steps per mate added since the last LDS flush (a byte grows <= 1 per step)
   uint64_t fx16[NM];
-  uint32_t cnt[NM][7];   // input, passed, failed, edited, stats, long, any-long
+  uint32_t cnt[NM][5];   // input, passed, failed, edited, stats
 #pragma unroll
   for (int m = 0; m < NM; ++m) {
     fx16[m] = 0;
-    for (int k = 0; k < 7; ++k) cnt[m][k] = 0;
+    for (int k = 0; k < 5; ++k) cnt[m][k] = 0;
   }
+  uint32_t ndefer = 0;   // reads this wave handed to the next stage
 
-  const int64_t nblocks = (A.num_reads + kBlock - 1) / kBlock;
-  const int64_t gw = (int64_t)blockIdx.x * kWaves + wave;
-  const int64_t nw = (int64_t)gridDim.x * kWaves;
+  const int ublock = FOLLOW ? A.unit_reads : kBlock;   // reads per unit
+  UnitIter<FOLLOW, kBlock> it;
+  it.init(A, (int)blockIdx.x * kWaves + wave, (int)gridDim.x * kWaves);
 
-  // block prologue: lane j describes read (pair) r0 + j in read table `tb`;
-  // lanes >= nr get length 0, so whatever gathers them contributes nothing.
-  // Returns this lane's lengths (the epilogue needs them).
-  // a block's read offsets (lane j: read r0 + j), fetched one block ahead of
-  // its prologue so the prologue does not wait for them
-  auto fetch_idx = [&](int64_t blk, int32_t (&ia)[NM], int32_t (&ie)[NM]) {
-    const int64_t r0 = blk * kBlock;
-    const int nr = (int)min((int64_t)kBlock, A.num_reads - r0);
-    const int l = min(lane, nr - 1);
+  // a unit's read offsets (lane j: read j), fetched one unit ahead of the
+  // prologue that describes it, so the prologue does not wait for them
+  // (FOLLOW: the compaction leaves the unit's read positions in `scratch` for
+  // the prologue, so no register carries them across the iteration)
+  auto fetch_idx = [&](const Unit &U, int32_t (&ia)[NM], int32_t (&ie)[NM]) __attribute__((always_inline)) {
+    const int r = U.nr > 0 ? unit_read<FOLLOW>(U, U.u * ublock, scratch) : 0;
+    const bool on = lane < U.nr;
 #pragma unroll
     for (int m = 0; m < NM; ++m) {
-      ia[m] = A.idx[m][r0 + l];
-      ie[m] = A.idx[m][r0 + l + 1];
+      ia[m] = on ? A.idx[m][r] : 0;
+      ie[m] = on ? A.idx[m][r + 1] : 0;
     }
   };
-  auto load_block = [&](int64_t blk, int tb, uint32_t (&len)[NM], uint32_t &tw, uint32_t &nraw,
-                        const int32_t (&ia)[NM], const int32_t (&ie)[NM]) {
-    const int64_t r0 = blk * kBlock;
-    const int nr = (int)min((int64_t)kBlock, A.num_reads - r0);
-    const int l = min(lane, nr - 1);
+  // unit prologue: lane j describes read (pair) j in read table `tb`; absent
+  // and deferred reads get length 0 and out-of-range offsets.  Returns this
+  // lane's lengths (the epilogue needs them) and the deferred-lane mask.
+  auto load_block = [&](const Unit &U, int tb, uint32_t (&len)[NM], uint32_t &tw, uint64_t &dm,
+                        const int32_t (&ia)[NM], const int32_t (&ie)[NM]) __attribute__((always_inline)) {
+    const bool on = lane < U.nr;
+    const uint32_t rid = (uint32_t)(U.u * ublock) + (FOLLOW ? scratch[lane] : (uint32_t)lane);
+    bool dfr = false;
+#pragma unroll
+    for (int m = 0; m < NM; ++m) dfr = dfr || (ie[m] - ia[m] > dlim);
+    dfr = dfr && on;
+    dm = __ballot(dfr);
+    const bool live = on && !dfr;
+    if (U.u >= 0) {
+      uint64_t pbits = dm;   // deferred reads by position in the unit
+      if (FOLLOW && dm) {
+        if (lane == 0) *dword = 0ull;
+        __builtin_amdgcn_wave_barrier();
+        if (dfr) atomicOr(dword, 1ull << (rid - (uint32_t)(U.u * ublock)));
+        __builtin_amdgcn_wave_barrier();
+        pbits = uni64(*dword);
+        __builtin_amdgcn_wave_barrier();
+      }
+      if (lane == 0) A.defer_bits[U.u] = pbits;
+      ndefer += (uint32_t)__builtin_popcountll(dm);
+    }
+    tw = 0;
 #pragma unroll
     for (int m = 0; m < NM; ++m) {
       int a = ia[m], e = ie[m];
-      nraw = lane < nr ? (uint32_t)(e - a) : 0u;
       if (EDIT) {   // trim here, then describe the trimmed window
-        tw = lane < nr ? trim_word(HPGQ_TRI_COLD_COPY ? cold : *A.cold, rq[m], bq[m] + a, e - a) : 0u;
-        if (A.trim && lane < nr) A.trim[r0 + l] = tw;
+        tw = live ? trim_word(cold, rq[m], bq[m] + a, e - a) : 0u;
+        if (A.trim && live) A.trim[rid] = tw;
         a += (int)(tw & 0xFFFFu);
         e -= (int)(tw >> 16);
         if (e < a) e = a;
       }
-      const uint32_t n = lane < nr ? (uint32_t)(e - a) : 0u;
-      const uint32_t xs = (uint32_t)(bs[m] + a), xq = (uint32_t)(bq[m] + a);
-      v4u rec;
-      if (UNAL) rec = v4u{xs, xq, n, 0u};
-      else rec = v4u{xs & ~3u, xq & ~3u, n | ((xs & 3u) << 16) | ((xq & 3u) << 20), 0u};
+      const uint32_t n = live ? (uint32_t)(e - a) : 0u;
+      const uint32_t xs = live ? (uint32_t)(bs[m] + a) : 0x80000000u;
+      const uint32_t xq = live ? (uint32_t)(bq[m] + a) : 0x80000000u;
+      // (FOLLOW: the read id rides in the record's spare dword, for the epilogue)
+      const v4u rec = v4u{xs & ~3u, xq & ~3u, n | ((xs & 3u) << 16) | ((xq & 3u) << 20), rid};
       *reinterpret_cast<v4u *>(tab(m, tb) + 4 * lane) = rec;
       len[m] = n;
     }
     __builtin_amdgcn_wave_barrier();   // other lanes read them (LDS is in order per wave)
   };
+  // steps holding the unit's non-deferred reads (0: nothing to stream)
+  auto steps_of = [&](const Unit &U, uint64_t dm) __attribute__((always_inline)) {
+    return __builtin_popcountll(dm) == U.nr ? 0 : (U.nr + kSegs - 1) / kSegs;
+  };
   // lane -> its segment's read (entry `src` of mate m's read table tb)
-  auto gather = [&](int m, int tb, int src, TriPending<NW> &pd) {
+  auto gather = [&](int m, int tb, int src, TriPending<NW> &pd) __attribute__((always_inline)) {
     const v4u rec = *reinterpret_cast<const v4u *>(tab(m, tb) + 4 * src);
     pd.n = rec.z;
     if (NW == 2) {
@@ -468,33 +480,23 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   };
 
   TriPending<NW> grp[2][kU];
-  // issue group g (kU steps) of mate m; steps past the block end gather
-  // lane 63 (length 0), so they add nothing
-#ifndef HPGQ_TRI_PRIO
-#define HPGQ_TRI_PRIO 0   // timing probe: raised wave priority while a group's loads issue
-#endif
-  auto load_group = [&](int m, int tb, int nt, int g, int slot) {
-    if (HPGQ_TRI_PRIO) __builtin_amdgcn_s_setprio(HPGQ_TRI_PRIO);
+  // issue group g (kU steps) of mate m; steps past the unit end gather
+  // lane 63 (length 0: never a read of the unit), so they add nothing
+  auto load_group = [&](int m, int tb, int nt, int g, int slot) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       const int t = g * kU + u;
       gather(m, tb, t < nt ? min(kSegs * t + seg, 63) : 63, grp[slot][u]);
     }
-    if (HPGQ_TRI_PRIO) __builtin_amdgcn_s_setprio(0);
   };
 
-  // one triple: per-lane partial (raw quality | G+C << 18); adds (SUB = false)
+  // one step: per-lane partial (raw quality | G+C << 18); adds (SUB = false)
   // or removes (SUB = true) the lane's positions from mate m's counters
-  auto account = [&](auto mtag, const TriPending<NW> &pd, bool count, auto sub_tag, uint32_t &x2) -> uint32_t {
+  auto account = [&](auto mtag, const TriPending<NW> &pd, bool count, auto sub_tag, uint32_t &x2) __attribute__((always_inline)) -> uint32_t {
     constexpr int m = decltype(mtag)::value;
     constexpr bool SUB = decltype(sub_tag)::value;
     uint32_t sw[NW], qw[NW];
-#pragma unroll
-    for (int w = 0; w < NW; ++w) {
-      sw[w] = pd.s[w];
-      qw[w] = pd.q[w];
-    }
-    if (!UNAL) {   // realign: word w = bytes [al, al+4) of raw words w, w+1 (the last from lane+1)
+    {   // realign: word w = bytes [al, al+4) of raw words w, w+1 (the last from lane+1)
       const uint32_t als = (pd.n >> 16) & 3u, alq = (pd.n >> 20) & 3u;
       const uint32_t ns = next_lane0(pd.s[0]), nq = next_lane0(pd.q[0]);
 #pragma unroll
@@ -504,12 +506,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       }
     }
     uint32_t mk[NW];
-#ifndef HPGQ_TRI_MTAB
-#define HPGQ_TRI_MTAB 1
-#endif
-    if (!HPGQ_TRI_MTAB) {
-      tri_masks<NW>((int)(pd.n & 0xFFFFu) - p0, mk);
-    } else {
+    {
       const int c = min(max((int)(pd.n & 0xFFFFu) - p0, 0), 4 * NW);
       if (NW == 4) {
         const v4u t = *reinterpret_cast<const v4u *>(mtab + 4 * c);
@@ -587,50 +584,46 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   };
 
   uint32_t len[NM], lenn[NM];
-  uint32_t tw = 0, twn = 0, nraw = 0, nrawn = 0;   // EDIT: trim word, untrimmed length
-  int tb = 0;   // read table of the current block
-  int64_t blk = gw;
-  int32_t ia[NM], ie[NM];   // offsets of the block after the next one to be described
-  if (blk < nblocks) {
-    fetch_idx(blk, ia, ie);
-    load_block(blk, tb, len, tw, nraw, ia, ie);
-    fetch_idx(blk + nw < nblocks ? blk + nw : blk, ia, ie);
-    const int nr0 = (int)min((int64_t)kBlock, A.num_reads - blk * kBlock);
-    load_group(0, tb, (nr0 + kSegs - 1) / kSegs, 0, 0);
+  uint32_t tw = 0, twn = 0;   // EDIT: trim word of the lane's read
+  uint64_t dm = 0, dmn = 0;   // deferred lanes of the current / next unit
+  int tb = 0;   // read table of the current unit
+  int32_t ia[NM], ie[NM];   // offsets of the unit after the next one to be described
+  Unit cur = it.next(), nxt = Unit{-1, 0, 0};
+  for (int m = 0; m < NM; ++m) len[m] = lenn[m] = 0;
+  if (cur.u >= 0) {
+    fetch_idx(cur, ia, ie);
+    load_block(cur, tb, len, tw, dm, ia, ie);
+    nxt = it.next();
+    fetch_idx(nxt, ia, ie);
+    load_group(0, tb, steps_of(cur, dm), 0, 0);
   }
-  constexpr uint64_t not_seg_first = not_seg_first_mask<NW>();   // lanes j with j % kSegs != 0
-  for (; blk < nblocks; blk += nw) {
-    const int64_t r0 = blk * kBlock;
-    const int nr = (int)min((int64_t)kBlock, A.num_reads - r0);
-    const int nt = (nr + kSegs - 1) / kSegs;
-    const int64_t nblk = blk + nw < nblocks ? blk + nw : blk;   // next block (or self)
-    const int nnt = ((int)min((int64_t)kBlock, A.num_reads - nblk * kBlock) + kSegs - 1) / kSegs;
-#ifndef HPGQ_TRI_LATE_PROLOGUE
-#define HPGQ_TRI_LATE_PROLOGUE 0   // measured: C4 unchanged, C3 5% slower when late
-#endif
-    // the next block's prologue (offsets and, for edit, the trims, which read
-    // the quality ends): at the start of this block's last group pair, so the
-    // lines the trims touch are still in L2 when the next block streams them
-    if (!HPGQ_TRI_LATE_PROLOGUE) {
-      load_block(nblk, tb ^ 1, lenn, twn, nrawn, ia, ie);
-      fetch_idx(nblk + nw < nblocks ? nblk + nw : nblk, ia, ie);
-    }
+  constexpr uint64_t not_seg_first = not_seg_first_mask<G>();   // lanes j with j % kSegs != 0
+  while (cur.u >= 0) {
+    const int nr = cur.nr;
+    const int nt = steps_of(cur, dm);
+    // the next unit's prologue (offsets and, for edit, the trims, which read
+    // the quality ends), so the lines the trims touch are still in L2 when the
+    // next unit streams them
+    load_block(nxt, tb ^ 1, lenn, twn, dmn, ia, ie);
+    const Unit nn2 = it.next();
+    fetch_idx(nn2, ia, ie);
+    const int nnt = steps_of(nxt, dmn);
     if (stats && since_flush > kByteEvery - kBlock / kSegs) {   // keep every byte <= 255
 #pragma unroll
       for (int m = 0; m < NM; ++m) acc[m].flush(pos_acc(m), lmax, p0);
       since_flush = 0;
     }
-    // an even number of groups per mate, so every mate (and block) starts in
+    // an even number of groups per mate, so every mate (and unit) starts in
     // slot 0 (the padding group gathers length-0 reads)
     const int ngroups = ((nt + kU - 1) / kU + 1) & ~1;
 
-    auto run_mate = [&](auto mtag) {
+    auto run_mate = [&](auto mtag) __attribute__((always_inline)) {
       constexpr int m = decltype(mtag)::value;
-      auto process_group = [&](int g, int slot) {
+      auto process_group = [&](int g, int slot) __attribute__((always_inline)) {
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
           const int t = g * kU + u;
-          // every read is added; failed ones are taken out in the block epilogue
+          // every read is added; failed ones are taken out in the unit epilogue
           uint32_t x2 = 0;
           const uint32_t x = account(MateTag<m>{}, grp[slot][u], stats, AddTag{}, x2);
           const uint32_t P = wave_scan(x);
@@ -642,33 +635,35 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
           }
         }
       };
-      // after this mate's last group: the next mate's first group, or the next block's
-      auto load_next_unit = [&](int slot) {
+      // after this mate's last group: the next mate's first group, or the next unit's
+      auto load_next_unit = [&](int slot) __attribute__((always_inline)) {
         if (m + 1 < NM) load_group(m + 1 < NM ? m + 1 : 0, tb, nt, 0, slot);
         else load_group(0, tb ^ 1, nnt, 0, slot);
       };
       for (int g = 0; g < ngroups; g += 2) {
-        if (HPGQ_TRI_LATE_PROLOGUE && m == NM - 1 && g + 2 >= ngroups) {
-          load_block(nblk, tb ^ 1, lenn, twn, nrawn, ia, ie);
-          fetch_idx(nblk + nw < nblocks ? nblk + nw : nblk, ia, ie);
-        }
         load_group(m, tb, nt, g + 1, 1);
         process_group(g, 0);
         if (g + 2 < ngroups) load_group(m, tb, nt, g + 2, 0);
         else load_next_unit(0);
         process_group(g + 1, 1);
-        // nibbles hold at most 15 triples: widen after groups 0-3 and at the end
-        static_assert(4 * kU <= kNibbleEvery && kBlock / kSegs - 4 * kU <= kNibbleEvery, "");
+        // nibbles hold at most 15 steps: widen after groups 0-3 and at the end
         if (stats && g == 2) acc[m].widen();
       }
       if (stats) acc[m].widen();
     };
-    run_mate(MateTag<0>{});
-    if (NM == 2) run_mate(MateTag<NM - 1>{});
+    if (ngroups > 0) {
+      run_mate(MateTag<0>{});
+      if (NM == 2) run_mate(MateTag<NM - 1>{});
+    } else {
+      load_group(0, tb ^ 1, nnt, 0, 0);   // a wholly deferred unit: straight to the next
+    }
     since_flush += nt;
 
-    // ---- block epilogue (lane j = read / pair r0 + j) --------------------
-    const bool valid = lane < nr;
+    // ---- unit epilogue (lane j = read / pair j) ----------------------------
+    // (a deferred read still has a segment end: its neighbour's sum is a difference of ends)
+    const bool inb = lane < nr;
+    const bool valid = inb && !((dm >> lane) & 1ull);
+    const int my_read = FOLLOW ? (int)tab(0, tb)[4 * lane + 3] : cur.u * ublock + lane;
     __builtin_amdgcn_wave_barrier();
     uint32_t r1[NM];
     bool pass = valid;
@@ -676,7 +671,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     for (int m = 0; m < NM; ++m) {
       // per-read sums: difference of consecutive segment ends within a step
       // (wends[kSegs t + k] = inclusive wave prefix at the end of segment k)
-      const uint32_t ends = valid ? wends(m)[lane] : 0u;
+      const uint32_t ends = inb ? wends(m)[lane] : 0u;
       const uint32_t prev = __builtin_amdgcn_mov_dpp(ends, 0x138, 0xF, 0xF, true);   // lane j-1
       r1[m] = ends - (((not_seg_first >> lane) & 1u) ? prev : 0u);
       const int n = (int)len[m];
@@ -684,30 +679,27 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       if (filter)
         pass = pass && n >= A.min_len && n <= A.max_len && lo_r * n <= sraw && sraw <= hi_r * n;
       if (NX && filter) {
-        const uint32_t e2 = valid ? wends2(m)[lane] : 0u;
+        const uint32_t e2 = inb ? wends2(m)[lane] : 0u;
         const uint32_t p2 = __builtin_amdgcn_mov_dpp(e2, 0x138, 0xF, 0xF, true);   // lane j-1
         const uint32_t r2 = e2 - (((not_seg_first >> lane) & 1u) ? p2 : 0u);
         if (x_n && (int)(r2 & 0xFFFFu) > x_maxn) pass = false;
         if (x_o && (int)(r2 >> 16) > x_maxo) pass = false;
       }
     }
-    if (valid && A.mask) A.mask[r0 + lane] = (uint8_t)pass;
+    if (valid && A.mask) A.mask[my_read] = (uint8_t)pass;
     const uint64_t failed = __ballot(valid && !pass);
     const uint32_t npass = (uint32_t)__builtin_popcountll(__ballot(pass));
+    const uint32_t nvalid = (uint32_t)(nr - __builtin_popcountll(dm));
     if (EDIT) cnt[0][3] += (uint32_t)__builtin_popcountll(__ballot(valid && tw != 0u));
 #pragma unroll
     for (int m = 0; m < NM; ++m) {
       const int n = (int)len[m];
-      // too long for the counters: the untrimmed length decides (as engine_kernel)
-      const bool lg = valid && (EDIT ? (int)nraw : n) > lmax;
-      cnt[m][0] += (uint32_t)nr;
+      cnt[m][0] += nvalid;
       cnt[m][1] += npass;
       cnt[m][2] += (uint32_t)__builtin_popcountll(failed);
-      cnt[m][6] += (uint32_t)__builtin_popcountll(__ballot(lg));
       if (stats) {
         cnt[m][4] += npass;
-        cnt[m][5] += (uint32_t)__builtin_popcountll(__ballot(pass && lg));
-        if (pass && !lg) {
+        if (pass) {   // (reads longer than lmax were deferred: every pass merges)
           const uint32_t gc = r1[m] >> 18, wn = (uint32_t)n, s = r1[m] & 0x3FFFFu;
           uint32_t *h = hist(m);
           atomicAdd(&h[wn], 1u);
@@ -720,7 +712,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
         }
       }
     }
-    if (stats) {
+    if (stats && failed) {
       // take the failed reads (pairs: both mates) back out.  A read must leave
       // through the segment it entered by (its lanes' byte counters hold it;
       // another segment's could borrow), so the failed reads of each segment
@@ -730,8 +722,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       uint32_t *flist = wends(0);
       constexpr uint64_t cls0 = ~not_seg_first;   // lanes j with j % kSegs == 0
       const int cls = lane % kSegs;
-      const uint64_t below = (1ull << lane) - 1ull;
-      const int rank = __builtin_popcountll(failed & (cls0 << cls) & below);
+      const int rank = __builtin_popcountll(failed & (cls0 << cls) & lanes_below(lane));
       __builtin_amdgcn_wave_barrier();
       if (valid && !pass) flist[min(rank * kSegs + cls, 63)] = (uint32_t)lane;
       __builtin_amdgcn_wave_barrier();
@@ -757,18 +748,19 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
 #pragma unroll
     for (int m = 0; m < NM; ++m) len[m] = lenn[m];
     tw = twn;
-    nraw = nrawn;
+    dm = dmn;
     tb ^= 1;
+    cur = nxt;
+    nxt = nn2;
   }
 
   // ---- workgroup epilogue ---------------------------------------------------
+  if (lane == 0 && ndefer) atomicAdd(A.defer_count, ndefer);
 #pragma unroll
   for (int m = 0; m < NM; ++m) {
     acc[m].widen();
     acc[m].flush(pos_acc(m), lmax, p0);
-    const uint32_t lo = (uint32_t)fx16[m], hi = (uint32_t)(fx16[m] >> 32);
-    const uint64_t tot = (uint64_t)wave_sum(lo & 0xFFFFu) + ((uint64_t)wave_sum(lo >> 16) << 16) +
-                         ((uint64_t)wave_sum(hi) << 32);
+    const uint64_t tot = wave_sum64(fx16[m]);
     if (lane == 0) {
       unsigned long long *s = sc(m);
       if (cnt[m][0]) atomicAdd(&s[HPGQ_S_NUM_INPUT], (unsigned long long)cnt[m][0]);
@@ -776,13 +768,10 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       if (cnt[m][2]) atomicAdd(&s[HPGQ_S_NUM_FAILED], (unsigned long long)cnt[m][2]);
       if (cnt[m][3]) atomicAdd(&s[HPGQ_S_NUM_EDITED], (unsigned long long)cnt[m][3]);
       if (cnt[m][4]) atomicAdd(&s[HPGQ_S_NUM_STATS], (unsigned long long)cnt[m][4]);
-      if (cnt[m][5]) atomicAdd(&s[HPGQ_S_LONG_READS], (unsigned long long)cnt[m][5]);
       if (tot) atomicAdd(&s[HPGQ_S_ACC_MEANQ_FX16], (unsigned long long)tot);
-      if (cnt[m][6] && A.err) atomicOr(A.err, 1);
     }
   }
   __syncthreads();
-  const int off_pos = HPGQ_NUM_SCALARS + hlen;
 #pragma unroll
   for (int m = 0; m < NM; ++m) {
     // N at position p = (stats reads longer than p) - A - C - G - T - other
@@ -795,28 +784,30 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     }
   }
   __syncthreads();
-  uint64_t *row = A.slab + (size_t)blockIdx.x * NM * A.clen;
 #pragma unroll
-  for (int m = 0; m < NM; ++m) {
-    uint64_t *rm = row + (size_t)m * A.clen;
-    const unsigned long long *s = sc(m);
-    const uint32_t *h = hist(m), *pa = pos_acc(m);
-    for (int i = tid; i < HPGQ_NUM_SCALARS; i += kWG) rm[i] += s[i];
-    for (int i = tid; i < hlen; i += kWG) rm[HPGQ_NUM_SCALARS + i] += h[i];
-    for (int i = tid; i < 6 * lmax; i += kWG) rm[off_pos + i] += pa[i];
-  }
+  for (int m = 0; m < NM; ++m)
+    add_partials(A.counters + (size_t)m * A.clen, sc(m), hist(m), hlen, pos_acc(m), lmax, tid, kWG);
 }
 
-
-template <int MINW, bool UNAL, int NM, bool EDIT, int NW>
+template <int MINW, int NM, bool EDIT, int G, bool FOLLOW>
 __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
-  tri_body<MINW, UNAL, NM, EDIT, NW, false>(A);
+  tri_body<MINW, NM, EDIT, G, false, FOLLOW>(A);
 }
 
 // the segmented kernel with the N / out-of-range read filters (no edit)
-template <int MINW, int NM, int NW>
+template <int MINW, int NM, int G, bool FOLLOW>
 __global__ void __launch_bounds__(kWG, MINW) engine_tri_x_kernel(EngineArgs A) {
-  tri_body<MINW, false, NM, false, NW, true>(A);
+  tri_body<MINW, NM, false, G, true, FOLLOW>(A);
 }
+
+// kernel selection (one translation unit per geometry, hpgq_engine_geo.hip):
+// the instance for (NM, edit, nx, follow) or nullptr; name gets its signature
+struct SegChoice {
+  const void *fn;
+  int min_waves;
+};
+SegChoice seg_kernel_tri(int nm, bool edit, bool nx, bool follow, char *name, size_t cap);
+SegChoice seg_kernel_hex(int nm, bool edit, bool nx, bool follow, char *name, size_t cap);
+SegChoice seg_kernel_wide(int nm, bool edit, bool nx, bool follow, char *name, size_t cap);
 
 }  // namespace hpgq

@@ -107,6 +107,7 @@ _SIGS = [
     ("hpgq_comm_unique_id", C.c_int, [C.c_char_p]),
     ("hpgq_comm_init", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_char_p]),
     ("hpgq_allreduce", C.c_int, [C.c_void_p]),
+    ("hpgq_global_counters_device", C.c_void_p, [C.c_void_p]),
     ("hpgq_cgr_open", C.c_int, [C.POINTER(C.c_void_p), C.c_int, C.c_int, C.c_int]),
     ("hpgq_cgr_close", None, [C.c_void_p]),
     ("hpgq_cgr_fill_device", C.c_int, [C.c_void_p, C.POINTER(Batch), C.c_void_p, C.c_int]),
@@ -149,6 +150,7 @@ _SIGS = [
     ("hpgq_strerror", C.c_char_p, [C.c_int]),
     ("hpgq_version", C.c_char_p, []),
     ("hpgq_kernel_name", C.c_char_p, [C.c_void_p]),
+    ("hpgq_kernel_chain", C.c_char_p, [C.c_void_p]),
     ("hpgq_host_alloc", C.c_int, [C.POINTER(C.c_void_p), C.c_size_t]),
     ("hpgq_host_free", None, [C.c_void_p]),
     ("hpgq_device_alloc", C.c_int, [C.c_int, C.POINTER(C.c_void_p), C.c_size_t]),

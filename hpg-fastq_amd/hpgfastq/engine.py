@@ -66,6 +66,11 @@ class Engine:
         """The engine kernel instance this ctx launches."""
         return lib.hpgq_kernel_name(self._h).decode()
 
+    @property
+    def kernel_chain(self):
+        """The ctx's kernel chain: first stage -> follow-up stages."""
+        return lib.hpgq_kernel_chain(self._h).decode()
+
     def run_host(self, batch, batch2=None, mask=None, trim=None):
         """Host numpy batch; mask/trim are numpy outputs valid after sync()."""
         check(lib.hpgq_run_host(self._h, C.byref(batch), C.byref(batch2) if batch2 else None,

@@ -58,7 +58,7 @@ extern "C" {
 #define HPGQ_E_INVALID         (-1)   /* bad argument / parameter            */
 #define HPGQ_E_HIP             (-2)   /* HIP runtime error                    */
 #define HPGQ_E_NOMEM           (-3)   /* device or host allocation failed     */
-#define HPGQ_E_READ_TOO_LONG   (-4)   /* a read longer than params.lmax seen  */
+#define HPGQ_E_READ_TOO_LONG   (-4)   /* a merged read longer than lmax      */
 #define HPGQ_E_NO_DEVICE       (-5)   /* no HIP device                        */
 #define HPGQ_E_RCCL            (-6)   /* RCCL communicator / collective error */
 #define HPGQ_E_STATE           (-7)   /* call not valid in this ctx state     */
@@ -147,7 +147,7 @@ void hpgq_params_init(hpgq_params_t *p);
 #define HPGQ_S_NUM_EDITED     3  /* reads whose trim removed >= 1 base         */
 #define HPGQ_S_NUM_STATS      4  /* reads merged into stats (counters->num_reads) */
 #define HPGQ_S_ACC_MEANQ_FX16 5  /* sum of floor(65536*sumQraw/len) (acc_quality) */
-#define HPGQ_S_LONG_READS     6  /* reads longer than lmax (error)             */
+#define HPGQ_S_LONG_READS     6  /* merged reads longer than lmax (error)      */
 #define HPGQ_S_RESERVED       7
 #define HPGQ_NUM_SCALARS      8
 
@@ -214,7 +214,10 @@ int  hpgq_run_device(hpgq_ctx_t *ctx, const hpgq_batch_t *b, const hpgq_batch_t 
 int  hpgq_run_host(hpgq_ctx_t *ctx, const hpgq_batch_t *b, const hpgq_batch_t *b2,
                    uint8_t *mask_out, uint32_t *trim_out);
 
-/* Wait for all work on the ctx stream; reports HPGQ_E_READ_TOO_LONG. */
+/* Wait for all work on the ctx stream.  HPGQ_E_READ_TOO_LONG when stats are on
+ * and a read that passed the filter is longer than lmax (the per-position
+ * counters cannot hold it; it is counted in HPGQ_S_LONG_READS).  Without
+ * stats, reads of any length are filtered and trimmed. */
 int  hpgq_sync(hpgq_ctx_t *ctx);
 
 /* Zero the ctx counters (async on the ctx stream). */
@@ -226,12 +229,13 @@ size_t hpgq_counters_size(const hpgq_ctx_t *ctx);
 /* Copy the counters to host memory (synchronises the ctx). */
 int  hpgq_read_counters(hpgq_ctx_t *ctx, uint64_t *out, size_t n);
 
-/* Fold the per-workgroup partials into the counter buffer (async on the ctx
- * stream).  hpgq_read_counters and hpgq_allreduce fold implicitly. */
+/* No-op kept for ABI compatibility: the kernels add their workgroup partials
+ * into the counters themselves (global atomics), so the counter buffer holds
+ * the totals as soon as the ctx stream has run the batch. */
 int  hpgq_fold(hpgq_ctx_t *ctx);
 
-/* Device pointer of the counter buffer (for an external all-reduce); holds
- * the totals after hpgq_fold(). */
+/* Device pointer of this ctx's own counter buffer (for an external
+ * all-reduce); holds the totals once the ctx stream has run the batches. */
 uint64_t *hpgq_counters_device(hpgq_ctx_t *ctx);
 
 /* HIP stream (hipStream_t) the ctx runs on. */
@@ -246,8 +250,13 @@ void *hpgq_stream(hpgq_ctx_t *ctx);
 /* rank 0 creates the id and ships it to the other ranks out of band */
 int  hpgq_comm_unique_id(char id[HPGQ_COMM_ID_BYTES]);
 int  hpgq_comm_init(hpgq_ctx_t *ctx, int nranks, int rank, const char id[HPGQ_COMM_ID_BYTES]);
-/* in-place ncclAllReduce(sum, uint64) of the packed counters on the ctx stream */
+/* ncclAllReduce(sum, uint64) of the packed counters on the ctx stream, OUT OF
+ * PLACE: the ctx keeps accumulating its own reads, the sum over the ranks goes
+ * to a second buffer that hpgq_read_counters returns until the next run or
+ * reset (so calling it twice, or after more batches, never double-counts). */
 int  hpgq_allreduce(hpgq_ctx_t *ctx);
+/* device pointer of the all-reduced counters */
+uint64_t *hpgq_global_counters_device(hpgq_ctx_t *ctx);
 
 /* ---------------------------------------------------------------------- */
 /* chaos-game (CGR) accumulator, old/chaos_game.c:165-267                 */
@@ -422,8 +431,10 @@ int  hpgq_device_count(void);
 
 const char *hpgq_strerror(int code);
 const char *hpgq_version(void);
-/* the engine kernel instance a ctx runs (for profiles / bench reports) */
+/* the first engine kernel instance of a ctx's chain (for profiles / bench
+ * reports) and the whole chain ("first -> follow-up -> ..."); DESIGN.md §4.0 */
 const char *hpgq_kernel_name(const hpgq_ctx_t *ctx);
+const char *hpgq_kernel_chain(const hpgq_ctx_t *ctx);
 
 /* memory helpers for HIP-free hosts (the C CLI): page-locked host buffers
  * (fast, asynchronous H2D), device buffers, and a device -> host copy queued

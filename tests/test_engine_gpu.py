@@ -47,26 +47,28 @@ STATS_CASES = {
 }
 
 
-@pytest.fixture(params=["auto", "tri", "single"])
+@pytest.fixture(params=["auto", "tri", "wide", "single"])
 def kernel_choice(request, monkeypatch):
-    """Run a test with the default kernel choice (the segmented kernel in its
-    16-byte-lane "hex" geometry where lmax <= 156), with its 8-byte-lane "tri"
-    geometry forced (HPGQ_TRI_GEO=tri) and with the one-read-per-wave kernel
-    forced (HPGQ_KERNEL=single), so every FAST kernel meets the oracle."""
+    """Run a test with the default kernel chain (the segmented kernel in its
+    16-byte-lane "hex" geometry first), with its 8-byte-lane "tri" or its
+    4-segment "wide" geometry forced first (HPGQ_TRI_GEO) and with the
+    one-read-per-wave catch-all alone (HPGQ_KERNEL=single), so every kernel
+    meets the oracle."""
     monkeypatch.delenv("HPGQ_KERNEL", raising=False)
     monkeypatch.delenv("HPGQ_TRI_GEO", raising=False)
     if request.param == "single":
         monkeypatch.setenv("HPGQ_KERNEL", "single")
-    elif request.param == "tri":
-        monkeypatch.setenv("HPGQ_TRI_GEO", "tri")
+    elif request.param in ("tri", "wide"):
+        monkeypatch.setenv("HPGQ_TRI_GEO", request.param)
     return request.param
 
 
-@pytest.fixture(params=["auto", "tri"])
+@pytest.fixture(params=["auto", "tri", "wide"])
 def geo_choice(request, monkeypatch):
-    """The segmented kernel's two geometries (edit runs on both)."""
-    if request.param == "tri":
-        monkeypatch.setenv("HPGQ_TRI_GEO", "tri")
+    """The segmented kernel's geometries as the first stage (edit runs on all)."""
+    monkeypatch.delenv("HPGQ_KERNEL", raising=False)
+    if request.param in ("tri", "wide"):
+        monkeypatch.setenv("HPGQ_TRI_GEO", request.param)
     else:
         monkeypatch.delenv("HPGQ_TRI_GEO", raising=False)
     return request.param
@@ -345,5 +347,121 @@ def test_n_oor_filters_route_to_segmented_kernel(name, geo_choice):
     p = H.stats_params(lmax=150, **STATS_CASES[name])
     with H.Engine(p) as e:
         assert "engine_tri_x_kernel" in e.kernel_name
-        assert ("4>" in e.kernel_name) == (geo_choice == "auto")
+        assert ("hex" if geo_choice == "auto" else geo_choice) in e.kernel_name
     assert_same(p, O.synth(600_000, seed=23, L=150, trunc_pct=5, n_per_1024=12))
+
+
+# ---- routing by the reads' actual lengths ---------------------
+C2 = dict(read_quality_range="20,", read_length_range="50,")
+
+
+def _mixed(n, seed, lengths, weights):
+    """Reads whose lengths are drawn from `lengths` (synthetic bases/qualities)."""
+    rng = np.random.default_rng(seed)
+    ls = rng.choice(lengths, size=n, p=np.asarray(weights, float) / sum(weights))
+    pairs = []
+    for i, L in enumerate(ls):
+        r = O.synth(1, seed=seed * 7919 + i, L=int(L), trunc_pct=0, n_per_1024=8)
+        pairs.append((bytes(r.seq), bytes(r.qual)))
+    return O.Reads.from_pairs(pairs)
+
+
+def test_lmax1024_150bp_runs_segmented(kernel_choice):
+    """The drop-in default (CLI --lmax 1024, INTEGRATION's p->lmax = 1024) on
+    150 bp reads runs the segmented hex kernel, bit-identical to the oracle."""
+    p = H.stats_params(lmax=1024, **C2)
+    if kernel_choice == "auto":
+        with H.Engine(p) as e:
+            assert "engine_tri_kernel" in e.kernel_name and "hex" in e.kernel_name, e.kernel_chain
+            assert "wide, follow" in e.kernel_chain and "engine_kernel" in e.kernel_chain
+    assert_same(p, O.synth(200_000, seed=31, L=150, trunc_pct=5, n_per_1024=4))
+
+
+@pytest.mark.parametrize("lmax", [250, 1024])
+def test_250bp_reads(lmax, kernel_choice):
+    """250 bp reads: wide geometry first (lmax 250) or deferred by hex to the
+    wide follow-up stage (lmax 1024); C2 flags, stats."""
+    p = H.stats_params(lmax=lmax, **C2)
+    if kernel_choice == "auto":
+        with H.Engine(p) as e:
+            assert ("wide" in e.kernel_name) == (lmax == 250), e.kernel_chain
+    assert_same(p, O.synth(120_000, seed=32, L=250, trunc_pct=10, n_per_1024=4))
+
+
+@pytest.mark.parametrize("case", ["stats", "c2", "nx", "filter_only", "edit"])
+def test_mixed_length_batches(case, kernel_choice):
+    """Every stage of the chain in one batch: 20..156 (hex), 157..252 (wide),
+    253..1024 (catch-all pipeline), > 1260 (catch-all chunk loop)."""
+    reads = _mixed(3000, 5, [40, 100, 150, 156, 157, 160, 200, 252, 253, 300, 700, 1024, 1300, 3000],
+                   [10, 20, 40, 5, 5, 5, 10, 5, 5, 5, 3, 2, 1, 1])
+    if case == "stats":   # long reads fail the length filter: no error, all stats exact
+        p = H.stats_params(lmax=1024, read_length_range=",1024")
+    elif case == "c2":
+        p = H.stats_params(lmax=1024, read_quality_range="20,", read_length_range="50,1024")
+    elif case == "nx":
+        p = H.stats_params(lmax=1024, read_length_range=",1024", max_N=1, max_out_of_quality=40)
+    elif case == "filter_only":   # no stats: every length is filtered, no error
+        p = H.filter_params(lmax=150, read_quality_range="20,", read_length_range="50,", max_N=3)
+    else:   # edit without stats: trims of every length
+        p = H.edit_params(lmax=150, stats=False, left_length=10, left_quality_range="20,",
+                          right_length=30, right_quality_range="20,")
+    assert_same(p, reads)
+
+
+def test_mixed_lengths_edit_stats(geo_choice):
+    reads = _mixed(2000, 6, [60, 150, 158, 240, 400], [20, 40, 20, 15, 5])
+    p = H.edit_params(lmax=512, stats=True, left_length=10, left_quality_range="20,",
+                      right_length=30, right_quality_range="20,")
+    assert_same(p, reads)
+
+
+def test_mixed_lengths_paired(geo_choice):
+    r1 = _mixed(2000, 7, [100, 150, 200, 400], [30, 40, 20, 10])
+    # mate 2: same count, its own lengths (a pair defers when either mate is long)
+    r2 = _mixed(2000, 8, [100, 150, 200, 400], [30, 40, 20, 10])
+    p = H.stats_params(lmax=1024, read_quality_range="15,", read_length_range="30,")
+    p.paired = 1
+    assert_same(p, r1, r2)
+
+
+def test_long_read_over_65535_bases():
+    """A read longer than 16 bits: stats on -> HPGQ_E_READ_TOO_LONG (the old
+    kernel packed the length into 16 bits and misread it); filter only -> the
+    chunk loop filters it like the oracle."""
+    big = O.synth(1, seed=3, L=65636, trunc_pct=0)
+    small = O.synth(300, seed=4, L=150)
+    reads = O.Reads.from_pairs([(bytes(big.seq), bytes(big.qual))] + small.pairs())
+    with H.Engine(H.stats_params(lmax=1024)) as e:
+        with pytest.raises(H.HpgqError) as ei:
+            e.process(reads.seq, reads.qual, reads.idx)
+        assert ei.value.code == -4
+    p = H.filter_params(lmax=150, read_quality_range="20,", max_N=100)
+    assert_same(p, reads)
+
+
+def test_failing_long_read_is_no_error():
+    """A read longer than lmax that FAILS the filter is not merged, so the call
+    succeeds (only a merged long read is an error)."""
+    reads = O.Reads.from_pairs([(b"A" * 400, b"#" * 400)] + O.synth(100, seed=5, L=150).pairs())
+    p = H.stats_params(lmax=150, read_quality_range="20,")
+    c = assert_same(p, reads)
+    assert c[H.S_LONG_READS] == 0
+
+
+def test_allreduce_out_of_place_twice():
+    """hpgq_allreduce is out of place: calling it twice, or running another batch
+    after it, never counts a rank's reads twice."""
+    reads = O.synth(20000, seed=33, L=150)
+    p = H.stats_params(lmax=150, **C2)
+    _, _, want = O.run(p, reads)
+    with H.Engine(p) as e:
+        e.comm_init(1, 0, H.engine.comm_unique_id())
+        e.process(reads.seq, reads.qual, reads.idx)
+        e.allreduce()
+        e.allreduce()
+        e.sync()
+        np.testing.assert_array_equal(e.counters(), want)
+        e.process(reads.seq, reads.qual, reads.idx)
+        e.allreduce()
+        e.sync()
+        np.testing.assert_array_equal(e.counters(), 2 * want)

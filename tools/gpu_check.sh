@@ -1,11 +1,12 @@
-# tests + short bench + kernel-trace profile on one GPU (run via gpurun)
+# GPU suite + bench lines (run via gpurun); output under gpurun_out/check
+#   CFGS="c2 c2_1024 ..." selects the extra bench configs (short runs)
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out
-export TMPDIR=/tmp
-timeout -k 10 600 python -m pytest tests -x -q -m gpu > gpurun_out/pytest_gpu.log 2>&1
-echo "pytest rc=$?" >> gpurun_out/pytest_gpu.log
-timeout -k 10 400 python bench.py --steps 3 --warmup 1 --cpu-seconds 5 > gpurun_out/bench1.log 2>&1 || exit 3
-if [ "${PROFILE:-1}" = "1" ]; then
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof1 -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/prof1.log 2>&1
+mkdir -p gpurun_out/check
+if [ -z "$SKIP_TESTS" ]; then
+  timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread ${PYTEST_ARGS} > gpurun_out/check/pytest_gpu.log 2>&1 || exit 3
 fi
+timeout -k 10 300 python bench.py > gpurun_out/check/bench.json 2> gpurun_out/check/bench.err || exit 4
+for c in ${CFGS}; do
+  timeout -k 10 300 python bench.py --config $c --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/check/bench_$c.json 2> gpurun_out/check/bench_$c.err || exit 5
+done
