@@ -79,11 +79,14 @@ def parse():
     ap.add_argument("--batch-reads", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--lmax", type=int, default=None, help="override the config's lmax")
     a = ap.parse_args()
     cfg = CONFIGS[a.config]
     a.reads = a.reads or cfg["reads"]
     a.batch_reads = a.batch_reads or cfg["batch"]
     a.read_length, a.seed = cfg["L"], cfg["seed"]
+    if a.lmax:
+        cfg["lmax"] = a.lmax
     return a
 
 

@@ -29,8 +29,20 @@ struct Stage {
   char name[80] = {0};
 };
 
+// the kernels of one call: s1 takes the batch; s2 (wide segmented) and s3
+// (catch-all) take what the stage before deferred
+struct Chain {
+  Stage s1, s2, s3;
+  bool has2 = false, has3 = false;
+};
+
 // flags words behind the counters (one memset clears both)
 enum { FL_PEND1 = 0, FL_PEND2 = 2, FL_ERR = 4, FL_WORDS = 8 };
+
+// adaptive first stage: a ctx whose reads may be long keeps two chains, hex
+// first (short reads; long ones deferred to wide) and wide first (long reads),
+// and picks per call from the previous calls' deferral reports
+constexpr int kProbeEvery = 16;   // wide-first calls between two hex-first probes
 
 }  // namespace
 
@@ -47,10 +59,11 @@ struct hpgq_ctx {
   uint64_t *d_global = nullptr;   // hpgq_allreduce output
   bool reduced = false;           // d_global is current (no run / reset since)
   hpgq::ColdParams *d_cold = nullptr;
-  // the chain: s1 takes the batch; s2 (wide segmented) and s3 (catch-all) take
-  // what the stage before deferred
-  Stage s1, s2, s3;
-  bool has2 = false, has3 = false;
+  Chain ch[2];              // [0]: the ctx's chain; [1]: wide first (adaptive only)
+  bool adaptive = false;
+  int mode = 0;              // chain of the next call
+  int wide_calls = 0;        // calls since the last probe in wide-first mode
+  uint32_t *h_report = nullptr, *d_report = nullptr;   // mapped host words (deferred, reads)
   int parity = 0;
   uint64_t *d_bits1 = nullptr, *d_bits2 = nullptr;   // deferred reads per s1 unit
   size_t bits_cap = 0;
@@ -220,7 +233,7 @@ static int finish_stage(hpgq_ctx *c, Stage &s, size_t lds, int cus) {
 // cannot hold, the wide geometry takes those up to 252 bases and the
 // catch-all takes the rest.  lmax only sizes the counters, so a ctx opened
 // with the CLI's lmax 1024 runs 150 bp reads on the hex geometry.
-static int plan_chain(hpgq_ctx *c, int cus) {
+static int plan_chain(hpgq_ctx *c, Chain &ch, int cus, int geo_force) {
   const hpgq_params_t &p = c->p;
   const int fl = engine_flags(p);
   const bool stats = fl & hpgq::F_STATS;
@@ -233,36 +246,81 @@ static int plan_chain(hpgq_ctx *c, int cus) {
   const char *force = std::getenv("HPGQ_KERNEL");   // "single": the catch-all alone (tests)
   const bool seg = !lr && !(nx && edit) && !(edit && c->nm == 2) && !(force && std::strcmp(force, "single") == 0);
   if (!seg) {
-    catch_all(c->s1, c->nm, p.lmax, needs_generic(fl), false);
-    return finish_stage(c, c->s1, catch_all_lds(p, c->nm), cus);
+    catch_all(ch.s1, c->nm, p.lmax, needs_generic(fl), false);
+    return finish_stage(c, ch.s1, catch_all_lds(p, c->nm), cus);
   }
   // first geometry: hex for short reads; wide when the counters say reads are
-  // 157..252 long; HPGQ_TRI_GEO=tri|hex|wide forces one (tests, A/B)
-  int geo = (stats && p.lmax > hpgq::Geo<hpgq::GEO_HEX>::kPos && p.lmax <= hpgq::Geo<hpgq::GEO_WIDE>::kPos)
-                ? hpgq::GEO_WIDE
-                : hpgq::GEO_HEX;
-  if (const char *g = std::getenv("HPGQ_TRI_GEO")) {
-    if (!std::strcmp(g, "tri")) geo = hpgq::GEO_TRI;
-    else if (!std::strcmp(g, "hex")) geo = hpgq::GEO_HEX;
-    else if (!std::strcmp(g, "wide")) geo = hpgq::GEO_WIDE;
-  }
-  if (!seg_stage(c->s1, geo, c->nm, edit, nx, false)) return HPGQ_E_INVALID;
+  // 157..252 long (or when forced: adaptive wide-first chain, HPGQ_TRI_GEO)
+  int geo = (stats && p.lmax > hpgq::Geo<hpgq::GEO_HEX>::kPos && p.lmax <= posw) ? hpgq::GEO_WIDE
+                                                                                 : hpgq::GEO_HEX;
+  if (geo_force >= 0) geo = geo_force;
+  if (!seg_stage(ch.s1, geo, c->nm, edit, nx, false)) return HPGQ_E_INVALID;
   const int pos1 = seg_pos(geo);
   // a merged read longer than lmax leaves the segmented kernels (the
   // catch-all counts it as a long read)
-  c->s1.defer_len = stats ? std::min(pos1, p.lmax) : pos1;
-  int rc = finish_stage(c, c->s1, seg_lds(p, c->nm, nx), cus);
+  ch.s1.defer_len = stats ? std::min(pos1, p.lmax) : pos1;
+  int rc = finish_stage(c, ch.s1, seg_lds(p, c->nm, nx), cus);
   if (rc) return rc;
-  c->has2 = geo != hpgq::GEO_WIDE && c->s1.defer_len < posw && !(stats && p.lmax <= pos1);
-  if (c->has2) {
-    if (!seg_stage(c->s2, hpgq::GEO_WIDE, c->nm, edit, nx, true)) return HPGQ_E_INVALID;
-    c->s2.defer_len = stats ? std::min(posw, p.lmax) : posw;
-    rc = finish_stage(c, c->s2, seg_lds(p, c->nm, nx), cus);
+  ch.has2 = geo != hpgq::GEO_WIDE && ch.s1.defer_len < posw && !(stats && p.lmax <= pos1);
+  if (ch.has2) {
+    if (!seg_stage(ch.s2, hpgq::GEO_WIDE, c->nm, edit, nx, true)) return HPGQ_E_INVALID;
+    ch.s2.defer_len = stats ? std::min(posw, p.lmax) : posw;
+    rc = finish_stage(c, ch.s2, seg_lds(p, c->nm, nx), cus);
     if (rc) return rc;
   }
-  c->has3 = true;
-  catch_all(c->s3, c->nm, p.lmax, true, true);
-  return finish_stage(c, c->s3, catch_all_lds(p, c->nm), cus);
+  ch.has3 = true;
+  catch_all(ch.s3, c->nm, p.lmax, true, true);
+  return finish_stage(c, ch.s3, catch_all_lds(p, c->nm), cus);
+}
+
+static int plan(hpgq_ctx *c, int cus) {
+  int geo_force = -1;
+  if (const char *g = std::getenv("HPGQ_TRI_GEO")) {   // tests, A/B: one fixed first geometry
+    if (!std::strcmp(g, "tri")) geo_force = hpgq::GEO_TRI;
+    else if (!std::strcmp(g, "hex")) geo_force = hpgq::GEO_HEX;
+    else if (!std::strcmp(g, "wide")) geo_force = hpgq::GEO_WIDE;
+  }
+  int rc = plan_chain(c, c->ch[0], cus, geo_force);
+  if (rc) return rc;
+  // hex first with a wide follow-up: batches of mostly long reads run better
+  // wide first, so keep that chain too and choose per call
+  const char *ad = std::getenv("HPGQ_ADAPTIVE");   // "0": off (tests, A/B)
+  c->adaptive = c->ch[0].has2 && geo_force < 0 && !(ad && std::atoi(ad) == 0);
+  if (!c->adaptive) return HPGQ_OK;
+  rc = plan_chain(c, c->ch[1], cus, hpgq::GEO_WIDE);
+  if (rc) return rc;
+  void *h = nullptr;
+  HPGQ_HIP_TRY(hipHostMalloc(&h, 64, hipHostMallocMapped));
+  c->h_report = static_cast<uint32_t *>(h);
+  c->h_report[0] = c->h_report[1] = 0;
+  void *d = nullptr;
+  HPGQ_HIP_TRY(hipHostGetDevicePointer(&d, h, 0));
+  c->d_report = static_cast<uint32_t *>(d);
+  return HPGQ_OK;
+}
+
+// the chain for the next call: wide first when the last report says at least
+// half of a batch's reads were deferred past hex; a hex-first probe every
+// kProbeEvery wide-first calls (its report clears the way back)
+static int pick_chain(hpgq_ctx *c) {
+  if (!c->adaptive) return 0;
+  volatile uint32_t *r = c->h_report;
+  const uint32_t deferred = r[0], reads = r[1];
+  const bool known = reads != 0;
+  const bool mostly_long = known && (uint64_t)deferred * 2 >= reads;
+  if (c->mode == 0) {
+    if (mostly_long) {
+      c->mode = 1;
+      c->wide_calls = 0;
+    }
+  } else if (known && !mostly_long) {
+    c->mode = 0;
+  } else if (++c->wide_calls >= kProbeEvery) {
+    c->wide_calls = 0;
+    r[0] = r[1] = 0;   // the probe's own report decides
+    return 0;
+  }
+  return c->mode;
 }
 
 extern "C" {
@@ -310,13 +368,18 @@ const char *hpgq_strerror(int code) {
 
 const char *hpgq_version(void) { return "hpgq 0.2 (gfx950)"; }
 
-const char *hpgq_kernel_name(const hpgq_ctx_t *ctx) { return ctx ? ctx->s1.name : ""; }
+const char *hpgq_kernel_name(const hpgq_ctx_t *ctx) { return ctx ? ctx->ch[0].s1.name : ""; }
 
 const char *hpgq_kernel_chain(const hpgq_ctx_t *ctx) {
-  static thread_local char buf[300];
+  static thread_local char buf[700];
   if (!ctx) return "";
-  std::snprintf(buf, sizeof(buf), "%s%s%s%s%s", ctx->s1.name, ctx->has2 ? " -> " : "", ctx->has2 ? ctx->s2.name : "",
-                ctx->has3 ? " -> " : "", ctx->has3 ? ctx->s3.name : "");
+  int o = 0;
+  for (int k = 0; k < (ctx->adaptive ? 2 : 1); ++k) {
+    const Chain &ch = ctx->ch[k];
+    o += std::snprintf(buf + o, sizeof(buf) - o, "%s%s%s%s%s%s", k ? " | adaptive: " : "", ch.s1.name,
+                       ch.has2 ? " -> " : "", ch.has2 ? ch.s2.name : "", ch.has3 ? " -> " : "",
+                       ch.has3 ? ch.s3.name : "");
+  }
   return buf;
 }
 
@@ -391,7 +454,7 @@ int hpgq_open(hpgq_ctx_t **out, int device, const hpgq_params_t *p) {
   HPGQ_HIP_TRY(hipMemsetAsync(c->d_state, 0, state_bytes(c), c->stream));
   int cus = 0;
   HPGQ_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-  rc = plan_chain(c, cus);
+  rc = plan(c, cus);
   if (rc) {
     hpgq_close(c);
     return rc;
@@ -420,13 +483,15 @@ void hpgq_close(hpgq_ctx_t *c) {
   (void)hipFree(c->d_buf);
   (void)hipFree(c->d_mask);
   (void)hipFree(c->d_trim);
+  if (c->h_report) (void)hipHostFree(c->h_report);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
 
 // per-unit deferral masks for a batch of n reads
 static int ensure_bits(hpgq_ctx *c, int64_t n) {
-  const size_t units = (size_t)((n + c->s1.block - 1) / c->s1.block) + 1;
+  const int block = std::min(c->ch[0].s1.block, c->adaptive ? c->ch[1].s1.block : INT_MAX);
+  const size_t units = (size_t)((n + block - 1) / block) + 1;
   if (units <= c->bits_cap) return HPGQ_OK;
   HPGQ_HIP_TRY(hipStreamSynchronize(c->stream));
   (void)hipFree(c->d_bits1);
@@ -455,14 +520,17 @@ static int launch(hpgq_ctx *c, hpgq::EngineArgs &A) {
   if (A.num_reads > INT32_MAX) return HPGQ_E_INVALID;   // read ids are 32-bit in the follow-up stages
   A.counters = c->d_state;
   A.err = reinterpret_cast<int32_t *>(c->d_flags + FL_ERR);
+  A.report = nullptr;
   c->reduced = false;
-  if (!c->has3) {   // the catch-all alone
+  const int k = pick_chain(c);
+  const Chain &ch = c->ch[k];
+  if (!ch.has3) {   // the catch-all alone
     A.unit_bits = A.unit_and = nullptr;
     A.pending = A.pending_clear = nullptr;
     A.defer_bits = nullptr;
     A.defer_count = nullptr;
     A.defer_len = INT_MAX;
-    return launch_stage(c, c->s1, A);
+    return launch_stage(c, ch.s1, A);
   }
   int rc = ensure_bits(c, A.num_reads);
   if (rc) return rc;
@@ -475,26 +543,27 @@ static int launch(hpgq_ctx *c, hpgq::EngineArgs &A) {
   A1.pending = A1.pending_clear = nullptr;
   A1.defer_bits = c->d_bits1;
   A1.defer_count = f + FL_PEND1 + s;
-  A1.defer_len = c->s1.defer_len;
-  rc = launch_stage(c, c->s1, A1);
+  A1.defer_len = ch.s1.defer_len;
+  rc = launch_stage(c, ch.s1, A1);
   if (rc) return rc;
-  const int64_t nunits = (A.num_reads + c->s1.block - 1) / c->s1.block;
+  const int64_t nunits = (A.num_reads + ch.s1.block - 1) / ch.s1.block;
   const uint64_t *last_bits = c->d_bits1;
   const uint32_t *last_count = f + FL_PEND1 + s;
   uint32_t *last_clear = f + FL_PEND1 + o;
   const uint64_t *and_bits = nullptr;
-  if (c->has2) {   // stage 2: the deferred reads up to 252 bases; longer -> bits2, PEND2[s]
+  if (ch.has2) {   // stage 2: the deferred reads up to 252 bases; longer -> bits2, PEND2[s]
     hpgq::EngineArgs A2 = A;
     A2.unit_bits = c->d_bits1;
     A2.unit_and = nullptr;
     A2.nunits = nunits;
-    A2.unit_reads = c->s1.block;
+    A2.unit_reads = ch.s1.block;
     A2.pending = last_count;
     A2.pending_clear = last_clear;
     A2.defer_bits = c->d_bits2;
     A2.defer_count = f + FL_PEND2 + s;
-    A2.defer_len = c->s2.defer_len;
-    rc = launch_stage(c, c->s2, A2);
+    A2.defer_len = ch.s2.defer_len;
+    A2.report = c->d_report;   // how many reads hex deferred: the next call's choice
+    rc = launch_stage(c, ch.s2, A2);
     if (rc) return rc;
     and_bits = c->d_bits1;   // bits2 words are only written for units with bits1 set
     last_bits = c->d_bits2;
@@ -505,13 +574,13 @@ static int launch(hpgq_ctx *c, hpgq::EngineArgs &A) {
   A3.unit_bits = last_bits;
   A3.unit_and = and_bits;
   A3.nunits = nunits;
-  A3.unit_reads = c->s1.block;
+  A3.unit_reads = ch.s1.block;
   A3.pending = last_count;
   A3.pending_clear = last_clear;
   A3.defer_bits = nullptr;
   A3.defer_count = nullptr;
   A3.defer_len = INT_MAX;
-  return launch_stage(c, c->s3, A3);
+  return launch_stage(c, ch.s3, A3);
 }
 
 int hpgq_run_device(hpgq_ctx_t *c, const hpgq_batch_t *b, const hpgq_batch_t *b2,

@@ -90,6 +90,9 @@ struct EngineArgs {
   uint64_t *defer_bits;
   uint32_t *defer_count;
   int defer_len;
+  // follow-up: host-mapped words [deferred reads, batch reads] for the host's
+  // choice of the next call's first stage (may be null)
+  uint32_t *report;
 };
 
 // ---------------------------------------------------------------------------
@@ -242,7 +245,13 @@ __device__ __forceinline__ int unit_read(const Unit &U, int base, uint32_t *scra
 
 // a follow-up stage with nothing deferred to it exits at once (grid-uniform)
 __device__ __forceinline__ bool follow_up_idle(const EngineArgs &A) {
-  if (A.pending_clear && blockIdx.x == 0 && threadIdx.x == 0) *A.pending_clear = 0u;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    if (A.pending_clear) *A.pending_clear = 0u;
+    if (A.report) {   // (a plain store over PCIe into pinned host memory)
+      A.report[0] = *A.pending;
+      A.report[1] = (uint32_t)A.num_reads;
+    }
+  }
   return A.unit_bits != nullptr && uni((int)*A.pending) == 0;
 }
 

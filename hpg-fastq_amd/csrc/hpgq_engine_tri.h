@@ -186,6 +186,42 @@ __device__ __forceinline__ uint32_t tri_fix(uint32_t s, uint32_t m, uint32_t cod
   return codes & ~ff;
 }
 
+// N at position p = (merged reads longer than p) - A - C - G - T - other, the
+// read count c[p] = sum_{L > p} hist_len[L] by a chunked suffix scan in
+// O(lmax): thread t owns positions [4t, 4t + 4) (lmax <= 1024 = 4 x kWG);
+// wtot: kWaves words of free LDS.  Ends with a barrier.
+__device__ __forceinline__ void derive_n(uint32_t *pa, const uint32_t *h, int lmax, int tid, uint32_t *wtot) {
+  static_assert(4 * kWG >= HPGQ_LMAX_LIMIT, "one 4-position chunk per thread");
+  const int p0 = 4 * tid;
+  uint32_t hv[4], s = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int L = p0 + i + 1;
+    hv[i] = L <= lmax ? h[L] : 0u;
+    s += hv[i];
+  }
+  const uint32_t incl = wave_scan(s);   // reads of lengths (.., p0 + 4] within the wave
+  if ((tid & 63) == 63) wtot[tid >> 6] = incl;
+  __syncthreads();
+  uint32_t total = 0, before = 0;
+#pragma unroll
+  for (int w = 0; w < kWaves; ++w) {
+    const uint32_t t = wtot[w];
+    total += t;
+    if (w < (tid >> 6)) before += t;
+  }
+  uint32_t c = total - before - incl;   // reads longer than p0 + 4
+#pragma unroll
+  for (int i = 3; i >= 0; --i) {
+    const int p = p0 + i;
+    c += hv[i];   // c[p] = h[p + 1] + c[p + 1]
+    if (p < lmax)
+      pa[5 * lmax + p] = c - pa[lmax + p] - pa[2 * lmax + p] - pa[3 * lmax + p] - pa[4 * lmax + p] -
+                         pa[5 * lmax + p];
+  }
+  __syncthreads();
+}
+
 template <bool B>
 struct TriTag {
   static constexpr bool value = B;
@@ -773,17 +809,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   }
   __syncthreads();
 #pragma unroll
-  for (int m = 0; m < NM; ++m) {
-    // N at position p = (stats reads longer than p) - A - C - G - T - other
-    uint32_t *pa = pos_acc(m), *h = hist(m);
-    for (int p = tid; p < lmax; p += kWG) {
-      uint32_t c = 0;
-      for (int L = p + 1; L <= lmax; ++L) c += h[L];
-      pa[5 * lmax + p] = c - pa[lmax + p] - pa[2 * lmax + p] - pa[3 * lmax + p] -
-                         pa[4 * lmax + p] - pa[5 * lmax + p];
-    }
-  }
-  __syncthreads();
+  for (int m = 0; m < NM; ++m) derive_n(pos_acc(m), hist(m), lmax, tid, mtab);   // (mtab is free now)
 #pragma unroll
   for (int m = 0; m < NM; ++m)
     add_partials(A.counters + (size_t)m * A.clen, sc(m), hist(m), hlen, pos_acc(m), lmax, tid, kWG);

@@ -465,3 +465,23 @@ def test_allreduce_out_of_place_twice():
         e.allreduce()
         e.sync()
         np.testing.assert_array_equal(e.counters(), 2 * want)
+
+
+def test_adaptive_first_stage_switches_and_stays_exact():
+    """A ctx that may see long reads (lmax 1024) keeps a hex-first and a
+    wide-first chain and picks per call from the deferral report of earlier
+    calls: batches of 250 bp reads, then 150 bp reads, then mixed, accumulate
+    into one counter set bit-identical to the oracle whatever chain ran."""
+    p = H.stats_params(lmax=1024, **C2)
+    batches = [O.synth(40_000, seed=40 + i, L=250, trunc_pct=5) for i in range(20)]
+    batches += [O.synth(40_000, seed=60 + i, L=150, trunc_pct=5) for i in range(20)]
+    batches += [_mixed(3000, 80 + i, [100, 150, 250, 600], [30, 30, 30, 10]) for i in range(4)]
+    want = np.zeros(H.counters_len(1024), np.uint64)
+    with H.Engine(p) as e:
+        assert "adaptive" in e.kernel_chain, e.kernel_chain
+        for r in batches:
+            m_g, _ = e.process(r.seq, r.qual, r.idx)
+            m_o, _, c_o = O.run(p, r)
+            np.testing.assert_array_equal(m_g, m_o)
+            want += c_o
+        np.testing.assert_array_equal(e.counters(), want)
