@@ -76,11 +76,13 @@ struct hpgq_ctx {
   ncclComm_t comm = nullptr;
 };
 
-// raw thresholds for "raw byte in [phred+lo, phred+hi]" with the clamps folded into flags
+// biased thresholds for "signed byte in [phred+lo, phred+hi]" (the kernels
+// compare b ^ 0x80 = (signed char)b + 128, hpgq_engine_kernel.h kQFlip) with
+// the clamps folded into flags
 static void raw_range(int phred, int lo_q, int hi_q, uint32_t &lo4, uint32_t &hi4, int &lo_none,
                       int &hi_none, int &none_in) {
-  const int64_t lo = (int64_t)phred + lo_q;
-  const int64_t hi1 = (int64_t)phred + hi_q + 1;
+  const int64_t lo = (int64_t)phred + hpgq::kQBias + lo_q;
+  const int64_t hi1 = (int64_t)phred + hpgq::kQBias + hi_q + 1;
   lo_none = lo <= 0;
   hi_none = hi1 > 255;
   none_in = lo > 255 || hi1 <= 0 || lo >= hi1;
@@ -90,7 +92,7 @@ static void raw_range(int phred, int lo_q, int hi_q, uint32_t &lo4, uint32_t &hi
   hi4 = hib * 0x01010101u;
 }
 
-static int clamp_q(int q) { return q < -256 ? -256 : (q > 256 ? 256 : q); }
+static int clamp_q(int q) { return q < -512 ? -512 : (q > 512 ? 512 : q); }
 
 // engine flags from the parameters
 static int engine_flags(const hpgq_params_t &p) {
@@ -121,12 +123,12 @@ static void fill_args(const hpgq_ctx *c, hpgq::EngineArgs &A) {
   const hpgq_params_t &p = c->p;
   A.lmax = p.lmax;
   A.clen = (int)c->clen;
-  A.phred = p.phred;
+  A.phred = p.phred + hpgq::kQBias;   // the kernels sum biased bytes (signed char + 128)
   A.cold = c->d_cold;
   A.flags = engine_flags(p);
   A.min_len = p.min_read_length;
   A.max_len = p.max_read_length;
-  // mean Q = raw - phred lies in [-255, 255]: clamping keeps every product in int32
+  // mean Q = (signed) raw - phred lies in [-383, 127]: clamping keeps every product in int32
   A.min_q = clamp_q(p.min_read_quality);
   A.max_q = clamp_q(p.max_read_quality);
 }
@@ -772,7 +774,7 @@ int hpgq_counters_summary(const uint64_t *set, int lmax, hpgq_summary_t *o) {
   }
   if (o->num_reads) {
     o->mean_length = (double)o->acc_length / (double)o->num_reads;
-    o->mean_quality_raw = (double)set[HPGQ_S_ACC_MEANQ_FX16] / 65536.0 / (double)o->num_reads;
+    o->mean_quality_raw = (double)(int64_t)set[HPGQ_S_ACC_MEANQ_FX16] / 65536.0 / (double)o->num_reads;
   }
   return HPGQ_OK;
 }

@@ -25,7 +25,7 @@
 //     buffer and 252-position chunk with a buffer_load (SRD bounds check, offset
 //     = SGPR read offset + lane*4) and takes its right neighbour's dword by DPP
 //     wave_shl:1; v_alignbyte realigns so lane l < 63 holds positions 4l..4l+3.
-//   * per-read sums (raw quality via v_sad_u8, G/C, N, out-of-range counts) are
+//   * per-read sums (biased quality via v_sad_u8, G/C, N, out-of-range counts) are
 //     reduced with DPP row_shr + row_bcast; the pass/fail decision is then
 //     wave-uniform scalar arithmetic.
 //   * per-position base counters: v_perm_b32 maps each base byte to a field
@@ -96,6 +96,19 @@ struct EngineArgs {
 };
 
 // ---------------------------------------------------------------------------
+// quality bytes
+// ---------------------------------------------------------------------------
+// A quality byte is the reference's `char`, signed on x86-64 gcc: the merge
+// adds fq_read->quality[j] into an int (src/stats_fastq.c:353-355), the CGR
+// accumulator likewise (old/chaos_game.c:253-259); DESIGN.md §2.3, quirk Q13.
+// The kernels work on BIASED bytes b ^ 0x80 = (signed char)b + 128, which
+// v_sad_u8, the SWAR compares and the 16-bit pair counters take as unsigned:
+// the host hands them phred + 128 as `phred` and biased thresholds, and the
+// workgroup epilogues take the 128 per merged base back out (pos_fix).
+constexpr uint32_t kQFlip = 0x80808080u;
+constexpr int kQBias = 128;
+
+// ---------------------------------------------------------------------------
 // SWAR + wave helpers
 // ---------------------------------------------------------------------------
 
@@ -161,6 +174,17 @@ __device__ __forceinline__ int wave_max(int v) {
   v = max(v, __builtin_amdgcn_update_dpp(small, v, 0x142, 0xA, 0xF, false));
   v = max(v, __builtin_amdgcn_update_dpp(small, v, 0x143, 0xC, 0xF, false));
   return __builtin_amdgcn_readlane(v, 63);
+}
+
+// inclusive prefix sum over the wave (row scans + row broadcasts)
+__device__ __forceinline__ uint32_t wave_scan(uint32_t v) {
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xF, 0xF, true);
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xF, 0xF, true);
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xF, 0xF, true);
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xF, 0xF, true);
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xA, 0xF, false);
+  v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xC, 0xF, false);
+  return v;
 }
 
 // lane i <- lane i+1 (wave_shl:1); lane 63 gets 0
@@ -321,14 +345,14 @@ __device__ __forceinline__ void issue(const MateBuf &b, const ReadRef &r, uint32
   }
 }
 
-// window-aligned words: lane bytes = positions p0..p0+3
+// window-aligned words: lane bytes = positions p0..p0+3 (quality biased)
 template <int NCH>
 __device__ __forceinline__ void finish(const ReadRef &r, const Pending<NCH> &p,
                                        uint32_t (&sw)[NCH], uint32_t (&qw)[NCH]) {
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     sw[c] = __builtin_amdgcn_alignbyte(next_lane(p.s[c]), p.s[c], (uint32_t)r.als);
-    qw[c] = __builtin_amdgcn_alignbyte(next_lane(p.q[c]), p.q[c], (uint32_t)r.alq);
+    qw[c] = __builtin_amdgcn_alignbyte(next_lane(p.q[c]), p.q[c], (uint32_t)r.alq) ^ kQFlip;   // biased
   }
 }
 
@@ -402,7 +426,7 @@ struct PosAcc {
 
 // per-read outcome (wave-uniform)
 struct ReadOut {
-  uint32_t r1;   // raw quality sum | GC << 18 (reads <= NCH chunks)
+  uint32_t r1;   // biased quality sum | GC << 19 (reads <= NCH chunks: 1260 x 255 < 2^19)
   int wn, ts, te;
   bool pass;
 };
@@ -429,7 +453,7 @@ __device__ __forceinline__ ReadOut evaluate(const EngineArgs &A, const ColdParam
     const uint32_t m80 = m[c] & 0x80808080u;
     const uint32_t q = qw[c] & m[c];
     p1 += __builtin_amdgcn_sad_u8(q, 0u, 0u);
-    p1 += (uint32_t)__builtin_popcount(zero_bytes((sw[c] | 0x04040404u) ^ 0x47474747u) & m80) << 18;
+    p1 += (uint32_t)__builtin_popcount(zero_bytes((sw[c] | 0x04040404u) ^ 0x47474747u) & m80) << 19;
     if (GEN) {
       if (A.flags & (F_NEED_N | F_NEED_OOR)) {
         uint32_t x = 0;
@@ -459,7 +483,7 @@ __device__ __forceinline__ ReadOut evaluate(const EngineArgs &A, const ColdParam
   o.ts = o.te = 0;
   bool pass = true;
   if (A.flags & F_FILTER) {
-    const int sq = (int)(o.r1 & 0x3FFFFu) - A.phred * wn;
+    const int sq = (int)(o.r1 & 0x7FFFFu) - A.phred * wn;
     pass = (wn >= A.min_len) & (wn <= A.max_len) & (A.min_q * wn <= sq) & (sq <= A.max_q * wn);
     if (GEN) {
       if (A.flags & (F_NEED_N | F_NEED_OOR)) {
@@ -520,7 +544,7 @@ __device__ __forceinline__ void chunk_words(const MateBuf &b, const ReadRef &r, 
   Pending<1> p;
   issue<1>(b, r, lane4, p, c0);
   sw = __builtin_amdgcn_alignbyte(next_lane(p.s[0]), p.s[0], (uint32_t)r.als);
-  qw = __builtin_amdgcn_alignbyte(next_lane(p.q[0]), p.q[0], (uint32_t)r.alq);
+  qw = __builtin_amdgcn_alignbyte(next_lane(p.q[0]), p.q[0], (uint32_t)r.alq) ^ kQFlip;   // biased
 }
 
 // edit (A6) trims of a read of any length (same rule as trim_read)
@@ -601,8 +625,68 @@ __device__ __forceinline__ bool long_eval(const EngineArgs &A, const ColdParams 
   return pass;
 }
 
+// one merged read's quality-histogram bin and acc_quality term from its biased
+// quality sum sb = S + 128 n (n > 0, n <= 1024, sb < 2^19): key = round(S / n) as C's
+// round() (halves away from zero; src/stats_fastq.c:317), bin = key & 255
+// (negative keys need quality bytes >= 128: bins 128..255); fx = floor(65536
+// S / n) in two's complement (the acc_quality term, HPGQ_S_ACC_MEANQ_FX16)
+__device__ __forceinline__ void meanq_terms(uint32_t sb, uint32_t n, uint32_t &bin, uint64_t &fx) {
+  const uint32_t off = (uint32_t)kQBias * n;
+  if (__builtin_expect(sb >= off, 1)) {
+    bin = (2 * sb + n) / (2 * n) - (uint32_t)kQBias;
+  } else {
+    const uint32_t t = off - sb;
+    bin = (256u - (2 * t + n) / (2 * n)) & 255u;
+  }
+  const uint32_t q = sb / n, rem = sb - q * n;
+  fx = ((uint64_t)q << 16) + (((uint32_t)rem << 16) / n) - ((uint64_t)kQBias << 16);
+}
+
+// Per-position fix-ups of a workgroup's partial set in LDS, from the read
+// count c[p] = sum_{L > p} hist_len[L] of its merged reads (a chunked suffix
+// scan in O(lmax): thread t owns positions [4t, 4t + 4), lmax <= 1024 = 4 x
+// kWG): the quality row loses the bias (128 c[p]); DERIVE_N: row 5 holds the
+// "other" counts and becomes N = c[p] - A - C - G - T - other.  wtot: kWaves
+// words of free LDS.  Ends with a barrier.
+template <bool DERIVE_N>
+__device__ __forceinline__ void pos_fix(uint32_t *pa, const uint32_t *h, int lmax, int tid, uint32_t *wtot) {
+  static_assert(4 * kWG >= HPGQ_LMAX_LIMIT, "one 4-position chunk per thread");
+  const int p0 = 4 * tid;
+  uint32_t hv[4], s = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int L = p0 + i + 1;
+    hv[i] = L <= lmax ? h[L] : 0u;
+    s += hv[i];
+  }
+  const uint32_t incl = wave_scan(s);   // reads of lengths (.., p0 + 4] within the wave
+  if ((tid & 63) == 63) wtot[tid >> 6] = incl;
+  __syncthreads();
+  uint32_t total = 0, before = 0;
+#pragma unroll
+  for (int w = 0; w < kWaves; ++w) {
+    const uint32_t t = wtot[w];
+    total += t;
+    if (w < (tid >> 6)) before += t;
+  }
+  uint32_t c = total - before - incl;   // reads longer than p0 + 4
+#pragma unroll
+  for (int i = 3; i >= 0; --i) {
+    const int p = p0 + i;
+    c += hv[i];   // c[p] = h[p + 1] + c[p + 1]
+    if (p < lmax) {
+      pa[p] -= (uint32_t)kQBias * c;
+      if (DERIVE_N)
+        pa[5 * lmax + p] = c - pa[lmax + p] - pa[2 * lmax + p] - pa[3 * lmax + p] - pa[4 * lmax + p] -
+                           pa[5 * lmax + p];
+    }
+  }
+  __syncthreads();
+}
+
 // add one workgroup's partial counter set into the global counters: one
-// no-return u64 atomic per nonzero entry (set layout: include/hpgq.h)
+// no-return u64 atomic per nonzero entry (set layout: include/hpgq.h); the
+// quality row (pos[0, lmax)) is a signed sum: sign-extended
 __device__ __forceinline__ void add_partials(uint64_t *dst, const unsigned long long *sc,
                                              const uint32_t *hist, int hlen, const uint32_t *pos,
                                              int lmax, int tid, int nthreads) {
@@ -613,7 +697,9 @@ __device__ __forceinline__ void add_partials(uint64_t *dst, const unsigned long 
                            (unsigned long long)hist[i]);
   uint64_t *dp = dst + HPGQ_NUM_SCALARS + hlen;
   for (int i = tid; i < 6 * lmax; i += nthreads)
-    if (pos[i]) atomicAdd(reinterpret_cast<unsigned long long *>(dp + i), (unsigned long long)pos[i]);
+    if (pos[i])
+      atomicAdd(reinterpret_cast<unsigned long long *>(dp + i),
+                i < lmax ? (unsigned long long)(long long)(int32_t)pos[i] : (unsigned long long)pos[i]);
 }
 
 template <int NM, int NCH, bool GEN, bool FOLLOW>
@@ -824,13 +910,15 @@ __global__ void __launch_bounds__(kWG) engine_kernel(EngineArgs A) {
         if (pass && !lg) {
           uint32_t *hm = hist + m * hlen;
           const uint32_t r1 = res_r1[m];
-          const uint32_t s = r1 & 0x3FFFFu, gc = r1 >> 18, n = (uint32_t)wn;
+          const uint32_t s = r1 & 0x7FFFFu, gc = r1 >> 19, n = (uint32_t)wn;
           atomicAdd(&hm[n], 1u);
           if (n > 0) {
-            atomicAdd(&hm[lmax + 1 + (2 * s + n) / (2 * n)], 1u);
+            uint32_t bin;
+            uint64_t fx;
+            meanq_terms(s, n, bin, fx);
+            atomicAdd(&hm[lmax + 1 + bin], 1u);
             atomicAdd(&hm[lmax + 1 + HPGQ_MEANQ_BINS + (100 * gc) / n], 1u);
-            const uint32_t q = s / n, rem = s - q * n;
-            fx16[m] += ((uint64_t)q << 16) + (((uint32_t)rem << 16) / n);
+            fx16[m] += fx;
           }
         }
       }
@@ -866,6 +954,9 @@ __global__ void __launch_bounds__(kWG) engine_kernel(EngineArgs A) {
     }
   }
   __syncthreads();
+  // (the compaction scratch is free now: pos_fix's wave totals)
+  uint32_t *wtot = reinterpret_cast<uint32_t *>(cold + 1);
+  for (int m = 0; m < NM; ++m) pos_fix<false>(pos_acc + m * 6 * lmax, hist + m * hlen, lmax, tid, wtot);
   for (int m = 0; m < NM; ++m)
     add_partials(A.counters + (size_t)m * A.clen, sc + m * HPGQ_NUM_SCALARS, hist + m * hlen, hlen,
                  pos_acc + m * 6 * lmax, lmax, tid, kWG);

@@ -32,8 +32,8 @@
 //     count - A - C - G - T - other, count from the length histogram.
 //   * nibble counters (<= 15 steps) are widened into 8-bit per-base counters
 //     (<= 255 steps) and those flushed to LDS u32 arrays (ds_add); quality
-//     sums are 16-bit pairs.
-//   * per-read sums (raw quality | G+C << 18) use ONE inclusive DPP prefix scan
+//     sums are 16-bit pairs of biased bytes (b ^ 0x80, hpgq_engine_kernel.h).
+//   * per-read sums (biased quality | G+C << 18) use ONE inclusive DPP prefix scan
 //     for the wave; the last lane of each segment stores its segment end to
 //     LDS (no wait) and the block epilogue takes differences.  (Per wave at
 //     most 64 x 16 x 255 < 2^18 quality units: the fields never carry.)
@@ -96,17 +96,6 @@ struct TriPending {
 
 __device__ __forceinline__ uint32_t next_lane0(uint32_t v) {   // lane i <- lane i+1, lane 63 <- 0
   return __builtin_amdgcn_mov_dpp(v, 0x130, 0xF, 0xF, true);
-}
-
-// inclusive prefix sum over the wave (row scans + row broadcasts)
-__device__ __forceinline__ uint32_t wave_scan(uint32_t v) {
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xF, 0xF, true);
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xF, 0xF, true);
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xF, 0xF, true);
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xF, 0xF, true);
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xA, 0xF, false);
-  v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xC, 0xF, false);
-  return v;
 }
 
 // 0xFF in every byte of d that is non-zero
@@ -186,42 +175,6 @@ __device__ __forceinline__ uint32_t tri_fix(uint32_t s, uint32_t m, uint32_t cod
   return codes & ~ff;
 }
 
-// N at position p = (merged reads longer than p) - A - C - G - T - other, the
-// read count c[p] = sum_{L > p} hist_len[L] by a chunked suffix scan in
-// O(lmax): thread t owns positions [4t, 4t + 4) (lmax <= 1024 = 4 x kWG);
-// wtot: kWaves words of free LDS.  Ends with a barrier.
-__device__ __forceinline__ void derive_n(uint32_t *pa, const uint32_t *h, int lmax, int tid, uint32_t *wtot) {
-  static_assert(4 * kWG >= HPGQ_LMAX_LIMIT, "one 4-position chunk per thread");
-  const int p0 = 4 * tid;
-  uint32_t hv[4], s = 0;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int L = p0 + i + 1;
-    hv[i] = L <= lmax ? h[L] : 0u;
-    s += hv[i];
-  }
-  const uint32_t incl = wave_scan(s);   // reads of lengths (.., p0 + 4] within the wave
-  if ((tid & 63) == 63) wtot[tid >> 6] = incl;
-  __syncthreads();
-  uint32_t total = 0, before = 0;
-#pragma unroll
-  for (int w = 0; w < kWaves; ++w) {
-    const uint32_t t = wtot[w];
-    total += t;
-    if (w < (tid >> 6)) before += t;
-  }
-  uint32_t c = total - before - incl;   // reads longer than p0 + 4
-#pragma unroll
-  for (int i = 3; i >= 0; --i) {
-    const int p = p0 + i;
-    c += hv[i];   // c[p] = h[p + 1] + c[p + 1]
-    if (p < lmax)
-      pa[5 * lmax + p] = c - pa[lmax + p] - pa[2 * lmax + p] - pa[3 * lmax + p] - pa[4 * lmax + p] -
-                         pa[5 * lmax + p];
-  }
-  __syncthreads();
-}
-
 template <bool B>
 struct TriTag {
   static constexpr bool value = B;
@@ -239,14 +192,15 @@ using SubTag = TriTag<true>;
 // read), so the lines it touches are still in L2 when the steps stream the read.
 __device__ __forceinline__ uint32_t trim_word(const ColdParams &C, __amdgpu_buffer_rsrc_t rq,
                                               int off, int n) {
-  auto ok_of = [&](uint32_t x, uint32_t y, bool right) __attribute__((always_inline)) -> uint64_t {   // 0x80 per in-range byte
+  // 0x80 per in-range byte of raw quality words x, y (biased here, as the thresholds)
+  auto ok_of = [&](uint32_t x, uint32_t y, bool right) __attribute__((always_inline)) -> uint64_t {
     uint32_t lo, hi;
     if (!right) {
-      lo = in_range(x, C.el_lo4, C.el_hi4, C.el_lo_none, C.el_hi_none, C.el_none_in);
-      hi = in_range(y, C.el_lo4, C.el_hi4, C.el_lo_none, C.el_hi_none, C.el_none_in);
+      lo = in_range(x ^ kQFlip, C.el_lo4, C.el_hi4, C.el_lo_none, C.el_hi_none, C.el_none_in);
+      hi = in_range(y ^ kQFlip, C.el_lo4, C.el_hi4, C.el_lo_none, C.el_hi_none, C.el_none_in);
     } else {
-      lo = in_range(x, C.er_lo4, C.er_hi4, C.er_lo_none, C.er_hi_none, C.er_none_in);
-      hi = in_range(y, C.er_lo4, C.er_hi4, C.er_lo_none, C.er_hi_none, C.er_none_in);
+      lo = in_range(x ^ kQFlip, C.er_lo4, C.er_hi4, C.er_lo_none, C.er_hi_none, C.er_none_in);
+      hi = in_range(y ^ kQFlip, C.er_lo4, C.er_hi4, C.er_lo_none, C.er_hi_none, C.er_none_in);
     }
     return (uint64_t)lo | ((uint64_t)hi << 32);
   };
@@ -363,7 +317,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   // EDIT: the trim bounds, read once (see NX above)
   ColdParams cold{};
   if (EDIT) cold = *A.cold;
-  // raw-sum bounds: pass iff min_len <= n <= max_len and lo_r*n <= S <= hi_r*n
+  // biased-sum bounds (A.phred is phred + 128): pass iff min_len <= n <= max_len and lo_r*n <= S <= hi_r*n
   const int lo_r = A.min_q + A.phred, hi_r = A.max_q + A.phred;
   const int dlim = A.defer_len;   // longer reads go to the next stage
 
@@ -558,7 +512,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     uint32_t bad = 0;
 #pragma unroll
     for (int w = 0; w < NW; ++w) {
-      qm[w] = qw[w] & mk[w];
+      qm[w] = __builtin_amdgcn_bitop3_b32(qw[w], kQFlip, mk[w], 0x28);   // (qw ^ 0x80..) & mk: biased quality bytes
       cd[w] = tri_codes(sw[w], mk[w], bad);
     }
     if (__builtin_expect(bad != 0, 0)) {
@@ -608,8 +562,8 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
             b = 0x80808080u;
           } else {
             b = 0;
-            if (!x_lonone) b |= ~ge_bytes(qw[w], x_lo4) & 0x80808080u;
-            if (!x_hinone) b |= ge_bytes(qw[w], x_hi4);
+            if (!x_lonone) b |= ~ge_bytes(qm[w], x_lo4) & 0x80808080u;   // (biased; m80 drops the masked bytes)
+            if (!x_hinone) b |= ge_bytes(qm[w], x_hi4);
           }
           oo += (uint32_t)__builtin_popcount(b & m80);
         }
@@ -740,10 +694,12 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
           uint32_t *h = hist(m);
           atomicAdd(&h[wn], 1u);
           if (wn > 0) {
-            atomicAdd(&h[lmax + 1 + (2 * s + wn) / (2 * wn)], 1u);
+            uint32_t bin;
+            uint64_t fx;
+            meanq_terms(s, wn, bin, fx);
+            atomicAdd(&h[lmax + 1 + bin], 1u);
             atomicAdd(&h[lmax + 1 + HPGQ_MEANQ_BINS + (100 * gc) / wn], 1u);
-            const uint32_t q = s / wn, rem = s - q * wn;
-            fx16[m] += ((uint64_t)q << 16) + (((uint32_t)rem << 16) / wn);
+            fx16[m] += fx;
           }
         }
       }
@@ -809,7 +765,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   }
   __syncthreads();
 #pragma unroll
-  for (int m = 0; m < NM; ++m) derive_n(pos_acc(m), hist(m), lmax, tid, mtab);   // (mtab is free now)
+  for (int m = 0; m < NM; ++m) pos_fix<true>(pos_acc(m), hist(m), lmax, tid, mtab);   // (mtab is free now)
 #pragma unroll
   for (int m = 0; m < NM; ++m)
     add_partials(A.counters + (size_t)m * A.clen, sc(m), hist(m), hlen, pos_acc(m), lmax, tid, kWG);

@@ -86,6 +86,19 @@ void oracle_synth(const hpgq_synth_t *s, int64_t first, int64_t n,
 /* per-read arithmetic                                                */
 /* ------------------------------------------------------------------ */
 
+/* A quality byte as the reference's `char`, signed on x86-64 gcc: the merge
+ * adds fq_read->quality[j] into an int (src/stats_fastq.c:353-355), and the
+ * CGR accumulator adds quality[qpos] the same way (old/chaos_game.c:253-259).
+ * Every quality rule below (filter sums, trims, out-of-range counts, the
+ * per-read mean) uses this value: DESIGN.md §2.3, quirk Q13. */
+static inline int32_t o_q(unsigned char c) { return (int32_t)(signed char)c; }
+
+/* floor(a / b) for b > 0 (C division truncates towards zero) */
+static inline int64_t o_floor_div(int64_t a, int64_t b) {
+  int64_t q = a / b;
+  return (a % b != 0 && a < 0) ? q - 1 : q;
+}
+
 typedef struct {
   int32_t ts, te;     /* trim start / end (A6) */
   int     pass;
@@ -112,7 +125,7 @@ static void o_trim(const hpgq_params_t *p, const unsigned char *q, int32_t n,
   if (p->edit_left_length > 0) {
     int32_t lim = p->edit_left_length < n ? p->edit_left_length : n;
     while (ts < lim) {
-      int32_t Q = (int32_t)q[ts] - p->phred;
+      int32_t Q = o_q(q[ts]) - p->phred;
       if (Q >= p->edit_min_left_quality && Q <= p->edit_max_left_quality) break;
       ts++;
     }
@@ -121,7 +134,7 @@ static void o_trim(const hpgq_params_t *p, const unsigned char *q, int32_t n,
     int32_t rem = n - ts;
     int32_t lim = p->edit_right_length < rem ? p->edit_right_length : rem;
     while (te < lim) {
-      int32_t Q = (int32_t)q[n - 1 - te] - p->phred;
+      int32_t Q = o_q(q[n - 1 - te]) - p->phred;
       if (Q >= p->edit_min_right_quality && Q <= p->edit_max_right_quality) break;
       te++;
     }
@@ -140,7 +153,7 @@ static int o_filter(const hpgq_params_t *p, const unsigned char *s,
   if (n < p->min_read_length || n > p->max_read_length) return 0;
   int64_t sumq = 0, nN = 0, oor = 0;
   for (int32_t j = 0; j < n; j++) {
-    int32_t Q = (int32_t)q[j] - p->phred;
+    int32_t Q = o_q(q[j]) - p->phred;
     sumq += Q;
     if (s[j] == 'N') nN++;
     if (Q < p->min_read_quality || Q > p->max_read_quality) oor++;
@@ -151,13 +164,13 @@ static int o_filter(const hpgq_params_t *p, const unsigned char *s,
   if (p->left_length > 0) {
     int32_t k = p->left_length < n ? p->left_length : n;
     int64_t sl = 0;
-    for (int32_t j = 0; j < k; j++) sl += (int32_t)q[j] - p->phred;
+    for (int32_t j = 0; j < k; j++) sl += o_q(q[j]) - p->phred;
     if (k > 0 && !o_mean_in(sl, k, p->min_left_quality, p->max_left_quality)) return 0;
   }
   if (p->right_length > 0) {
     int32_t k = p->right_length < n ? p->right_length : n;
     int64_t sr = 0;
-    for (int32_t j = n - k; j < n; j++) sr += (int32_t)q[j] - p->phred;
+    for (int32_t j = n - k; j < n; j++) sr += o_q(q[j]) - p->phred;
     if (k > 0 && !o_mean_in(sr, k, p->min_right_quality, p->max_right_quality)) return 0;
   }
   return 1;
@@ -166,10 +179,13 @@ static int o_filter(const hpgq_params_t *p, const unsigned char *s,
 /*
  * Per-read stats + the consumer merge (A3 + A4), src/stats_fastq.c:283-382:
  *   length histogram             :306-314 (key = read_length)
- *   quality histogram            :316-324 (key = round(quality_average), raw units)
+ *   quality histogram            :316-324 (key = round(quality_average), raw units;
+ *                                 C round(): halves away from zero; bin = key & 255)
  *   GC histogram                 :326-334 (key = 100*(G+C)/read_length, integer division)
- *   per position j < read_length :338-382 (quality[j] raw; A/T/C/G/N exact uppercase)
- *   acc_quality (float, :297)    -> exact fixed point sum, HPGQ_S_ACC_MEANQ_FX16
+ *   per position j < read_length :338-382 (quality[j] raw, signed char :353-355;
+ *                                 A/T/C/G/N exact uppercase)
+ *   acc_quality (float, :297)    -> exact fixed point sum, HPGQ_S_ACC_MEANQ_FX16 =
+ *                                 sum of floor(65536*S/n), two's complement
  * len 0 reads get no quality/GC bin (quirk Q8: the reference divides by zero).
  */
 static void o_merge(uint64_t *c, int lmax, const unsigned char *s,
@@ -177,11 +193,12 @@ static void o_merge(uint64_t *c, int lmax, const unsigned char *s,
   c[HPGQ_S_NUM_STATS]++;
   if (n > lmax) { c[HPGQ_S_LONG_READS]++; return; }
   c[hpgq_off_hist_len(lmax) + n]++;
-  uint64_t sraw = 0, gc = 0;
+  int64_t sraw = 0;
+  uint64_t gc = 0;
   uint64_t *pq = c + hpgq_off_pos_qsum(lmax);
   for (int32_t j = 0; j < n; j++) {
-    sraw += q[j];
-    pq[j] += q[j];
+    sraw += o_q(q[j]);
+    pq[j] += (uint64_t)(int64_t)o_q(q[j]);   /* u64 wrap = the int sum's two's complement */
     int b = -1;
     switch (s[j]) {
       case 'A': b = HPGQ_BASE_A; break;
@@ -194,10 +211,11 @@ static void o_merge(uint64_t *c, int lmax, const unsigned char *s,
     if (b >= 0) c[hpgq_off_pos_base(lmax, b) + j]++;
   }
   if (n > 0) {
-    uint64_t key = (2 * sraw + (uint64_t)n) / (2 * (uint64_t)n);   /* round(sraw/n) */
-    c[hpgq_off_hist_meanq(lmax) + key]++;
+    int64_t key = sraw >= 0 ? (2 * sraw + n) / (2 * (int64_t)n)            /* round(sraw/n) */
+                            : -((-2 * sraw + n) / (2 * (int64_t)n));
+    c[hpgq_off_hist_meanq(lmax) + ((uint64_t)key & 255u)]++;
     c[hpgq_off_hist_gc(lmax) + (100 * gc) / (uint64_t)n]++;
-    c[HPGQ_S_ACC_MEANQ_FX16] += (sraw << 16) / (uint64_t)n;
+    c[HPGQ_S_ACC_MEANQ_FX16] += (uint64_t)o_floor_div(sraw * 65536, n);
   }
 }
 

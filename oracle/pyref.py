@@ -35,6 +35,18 @@ def layout(lmax):
     return o
 
 
+def sq(c):
+    """A quality byte as the reference's `char` (signed on x86-64 gcc): the
+    merge adds fq_read->quality[j] into an int, src/stats_fastq.c:353-355
+    (DESIGN.md §2.3, quirk Q13).  Every quality rule uses this value."""
+    return c - 256 if c >= 128 else c
+
+
+def c_round_div(s, n):
+    """C round(s / n) for n > 0: halves away from zero."""
+    return (2 * s + n) // (2 * n) if s >= 0 else -((-2 * s + n) // (2 * n))
+
+
 def default_params(**kw):
     p = dict(phred=33, lmax=256, stats_on=1, filter_on=0, edit_on=0, paired=0,
              min_read_length=0, max_read_length=100000,
@@ -56,14 +68,14 @@ def trim(p, q):
     if p["edit_left_length"] > 0:
         lim = min(p["edit_left_length"], n)
         while ts < lim:
-            Q = q[ts] - p["phred"]
+            Q = sq(q[ts]) - p["phred"]
             if p["edit_min_left_quality"] <= Q <= p["edit_max_left_quality"]:
                 break
             ts += 1
     if p["edit_right_length"] > 0:
         lim = min(p["edit_right_length"], n - ts)
         while te < lim:
-            Q = q[n - 1 - te] - p["phred"]
+            Q = sq(q[n - 1 - te]) - p["phred"]
             if p["edit_min_right_quality"] <= Q <= p["edit_max_right_quality"]:
                 break
             te += 1
@@ -75,7 +87,7 @@ def passes(p, s, q):
     n = len(s)
     if n < p["min_read_length"] or n > p["max_read_length"]:
         return False
-    Q = [c - p["phred"] for c in q]
+    Q = [sq(c) - p["phred"] for c in q]
     if sum(1 for c in s if c == ord("N")) > p["max_N"]:
         return False
     tot = sum(Q)
@@ -107,15 +119,15 @@ def merge(c, lay, lmax, s, q):
     c[lay["hist_len"] + n] += 1
     gc = 0
     for j in range(n):
-        c[lay["pos_qsum"] + j] += q[j]
+        c[lay["pos_qsum"] + j] += sq(q[j])
         ch = chr(s[j])
         if ch in BASES:
             c[lay["pos_" + ch] + j] += 1
         if ch in "GC":
             gc += 1
     if n > 0:
-        sraw = sum(q)
-        c[lay["hist_meanq"] + (2 * sraw + n) // (2 * n)] += 1
+        sraw = sum(sq(x) for x in q)
+        c[lay["hist_meanq"] + (c_round_div(sraw, n) & 255)] += 1
         c[lay["hist_gc"] + (100 * gc) // n] += 1
         c[S_ACC_MEANQ_FX16] += (sraw << 16) // n
 
@@ -149,7 +161,7 @@ def run(p, reads, reads2=None):
                 c[S_NUM_EDITED] += 1
             if p["stats_on"] and ok:
                 merge(c, lay, lmax, ws, wq)
-    out = [x for st in sets for x in st]
+    out = [x & 0xFFFFFFFFFFFFFFFF for st in sets for x in st]   # u64 wrap
     return mask, trims + trims2, out
 
 

@@ -287,6 +287,31 @@ def test_kat_gpu(section, kernel_choice):
         np.testing.assert_array_equal(trim, exp["trim"])
 
 
+@pytest.mark.parametrize("section", ["stats", "filter", "edit"])
+def test_kat_signed_gpu(section, kernel_choice):
+    """Quality bytes >= 128 count as signed `char` (src/stats_fastq.c:353-355,
+    DESIGN.md Q13) on every kernel, by the hand-derived KAT."""
+    import json
+    import os
+    from fastq_io import read_fastq, check_partial
+    k = json.load(open(os.path.join(_gold(), "kat_expected.json")))["signed"]
+    reads = read_fastq(os.path.join(_gold(), k["reads"]))
+    lmax = k["lmax"]
+    if section == "stats":
+        p = H.stats_params(lmax=lmax)
+    elif section == "filter":
+        p = H.stats_params(lmax=lmax, **k["filter"]["flags"])
+    else:
+        p = H.edit_params(lmax=lmax, stats=True, **k["edit"]["flags"])
+    mask, trim, ctr = gpu_host_path(p, reads)
+    exp = k[section]
+    check_partial(ctr, exp, lmax, H.layout(lmax))
+    if "mask" in exp:
+        np.testing.assert_array_equal(mask, exp["mask"])
+    if "trim" in exp:
+        np.testing.assert_array_equal(trim, exp["trim"])
+
+
 @pytest.mark.parametrize("name", ["synth_c2_filter.npz", "synth_c4_edit.npz", "synth_c3_pe.npz",
                                   "synth_filter_all_250.npz"])
 def test_committed_vectors_gpu(name, kernel_choice):

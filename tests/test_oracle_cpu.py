@@ -51,6 +51,31 @@ def test_kat_c_oracle_and_pyref(section):
             np.testing.assert_array_equal(trim, exp["trim"])
 
 
+def _signed_params(section):
+    k = KAT["signed"]
+    if section == "stats":
+        return H.stats_params(lmax=k["lmax"])
+    if section == "filter":
+        return H.stats_params(lmax=k["lmax"], **k["filter"]["flags"])
+    return H.edit_params(lmax=k["lmax"], stats=True, **k["edit"]["flags"])
+
+
+@pytest.mark.parametrize("section", ["stats", "filter", "edit"])
+def test_kat_signed_qualities(section):
+    """Quality bytes >= 128 as signed `char` (src/stats_fastq.c:353-355, Q13)."""
+    k = KAT["signed"]
+    reads = read_fastq(os.path.join(GOLD, k["reads"]))
+    p = _signed_params(section)
+    lay = H.layout(k["lmax"])
+    for mask, trim, ctr in (O.run(p, reads), _pyref_run(p, reads)):
+        exp = k[section]
+        check_partial(ctr, exp, k["lmax"], lay)
+        if "mask" in exp:
+            np.testing.assert_array_equal(mask, exp["mask"])
+        if "trim" in exp:
+            np.testing.assert_array_equal(trim, exp["trim"])
+
+
 def test_kat_cgr():
     c = KAT["cgr"]
     reads = read_fastq(os.path.join(GOLD, c["reads"]))
