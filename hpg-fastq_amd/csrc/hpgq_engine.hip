@@ -179,14 +179,15 @@ static void catch_all(Stage &s, int nm, int lmax, bool gen, bool follow) {
                 follow ? " (follow-up)" : "");
 }
 
-static size_t seg_lds(const hpgq_params_t &p, int nm, bool nx) {
+static size_t seg_lds(const hpgq_params_t &p, int nm, int xm) {
   const size_t hlen = (size_t)p.lmax + 1 + HPGQ_MEANQ_BINS + HPGQ_GC_BINS;
   const size_t mate_words = (size_t)6 * p.lmax + ((hlen + 1) & ~(size_t)1) + 2 * HPGQ_NUM_SCALARS;
   // per mate [6][lmax] + hist + scalars, 16 B alignment, the byte-mask table,
-  // per wave and mate two read tables (2 x 1 KB) + segment ends (+ NX ends),
-  // per wave a compaction scratch and a deferral word
+  // per wave and mate two read tables (2 x 1 KB) + segment ends (+ one list per
+  // extra scan), per wave a compaction scratch and a deferral word
+  const size_t lists = 1 + ((xm & hpgq::X_NOOR) ? 1 : 0) + ((xm & hpgq::X_LR) ? 1 : 0);
   return (size_t)nm * mate_words * 4 + 16 + 17 * 16 +
-         (size_t)hpgq::kWaves * ((size_t)nm * (2 * 256 + (nx ? 128 : 64)) + 64 + 4) * 4;
+         (size_t)hpgq::kWaves * ((size_t)nm * (2 * 256 + 64 * lists) + 64 + 4) * 4;
 }
 
 static size_t catch_all_lds(const hpgq_params_t &p, int nm) {
@@ -208,11 +209,11 @@ static int seg_pos(int geo) {
                                                       : hpgq::Geo<hpgq::GEO_WIDE>::kPos);
 }
 
-static bool seg_stage(Stage &s, int geo, int nm, bool edit, bool nx, bool follow) {
+static bool seg_stage(Stage &s, int geo, int nm, bool edit, int xm, bool follow) {
   hpgq::SegChoice ch{};
-  if (geo == hpgq::GEO_TRI) ch = hpgq::seg_kernel_tri(nm, edit, nx, follow, s.name, sizeof(s.name));
-  else if (geo == hpgq::GEO_HEX) ch = hpgq::seg_kernel_hex(nm, edit, nx, follow, s.name, sizeof(s.name));
-  else ch = hpgq::seg_kernel_wide(nm, edit, nx, follow, s.name, sizeof(s.name));
+  if (geo == hpgq::GEO_TRI) ch = hpgq::seg_kernel_tri(nm, edit, xm, follow, s.name, sizeof(s.name));
+  else if (geo == hpgq::GEO_HEX) ch = hpgq::seg_kernel_hex(nm, edit, xm, follow, s.name, sizeof(s.name));
+  else ch = hpgq::seg_kernel_wide(nm, edit, xm, follow, s.name, sizeof(s.name));
   s.fn = ch.fn;
   s.follow = follow;
   s.block = seg_block(geo);
@@ -244,9 +245,11 @@ static int plan_chain(hpgq_ctx *c, Chain &ch, int cus, int geo_force) {
   // bases) when they are below 252; else the plain variant runs
   const int posw = hpgq::Geo<hpgq::GEO_WIDE>::kPos;
   const bool nx = p.filter_on && (p.max_N < posw || p.max_out_of_quality < posw);
+  // extra per-step scans: N / out-of-range counts, window sums
+  const int xm = (nx ? hpgq::X_NOOR : 0) | (lr ? hpgq::X_LR : 0);
   const bool edit = fl & hpgq::F_EDIT;
   const char *force = std::getenv("HPGQ_KERNEL");   // "single": the catch-all alone (tests)
-  const bool seg = !lr && !(nx && edit) && !(edit && c->nm == 2) && !(force && std::strcmp(force, "single") == 0);
+  const bool seg = !(xm && edit) && !(edit && c->nm == 2) && !(force && std::strcmp(force, "single") == 0);
   if (!seg) {
     catch_all(ch.s1, c->nm, p.lmax, needs_generic(fl), false);
     return finish_stage(c, ch.s1, catch_all_lds(p, c->nm), cus);
@@ -256,18 +259,18 @@ static int plan_chain(hpgq_ctx *c, Chain &ch, int cus, int geo_force) {
   int geo = (stats && p.lmax > hpgq::Geo<hpgq::GEO_HEX>::kPos && p.lmax <= posw) ? hpgq::GEO_WIDE
                                                                                  : hpgq::GEO_HEX;
   if (geo_force >= 0) geo = geo_force;
-  if (!seg_stage(ch.s1, geo, c->nm, edit, nx, false)) return HPGQ_E_INVALID;
+  if (!seg_stage(ch.s1, geo, c->nm, edit, xm, false)) return HPGQ_E_INVALID;
   const int pos1 = seg_pos(geo);
   // a merged read longer than lmax leaves the segmented kernels (the
   // catch-all counts it as a long read)
   ch.s1.defer_len = stats ? std::min(pos1, p.lmax) : pos1;
-  int rc = finish_stage(c, ch.s1, seg_lds(p, c->nm, nx), cus);
+  int rc = finish_stage(c, ch.s1, seg_lds(p, c->nm, xm), cus);
   if (rc) return rc;
   ch.has2 = geo != hpgq::GEO_WIDE && ch.s1.defer_len < posw && !(stats && p.lmax <= pos1);
   if (ch.has2) {
-    if (!seg_stage(ch.s2, hpgq::GEO_WIDE, c->nm, edit, nx, true)) return HPGQ_E_INVALID;
+    if (!seg_stage(ch.s2, hpgq::GEO_WIDE, c->nm, edit, xm, true)) return HPGQ_E_INVALID;
     ch.s2.defer_len = stats ? std::min(posw, p.lmax) : posw;
-    rc = finish_stage(c, ch.s2, seg_lds(p, c->nm, nx), cus);
+    rc = finish_stage(c, ch.s2, seg_lds(p, c->nm, xm), cus);
     if (rc) return rc;
   }
   ch.has3 = true;

@@ -20,15 +20,21 @@ constexpr int kSeW = G == GEO_TRI ? 5 : 4;   // single-end
 constexpr int kPeW = 3;                      // paired-end
 constexpr const char *kGeoName = G == GEO_TRI ? "tri" : (G == GEO_HEX ? "hex" : "wide");
 
+template <bool F, int XM>
+const void *x_kernel(int nm) {
+  return nm == 2 ? (const void *)engine_tri_x_kernel<kPeW, 2, G, F, XM> : (const void *)engine_tri_x_kernel<kSeW, 1, G, F, XM>;
+}
+
 template <bool F>
-SegChoice pick(int nm, bool edit, bool nx, char *name, size_t cap) {
+SegChoice pick(int nm, bool edit, int xm, char *name, size_t cap) {
   constexpr int kSe = kSeW;
   const void *fn = nullptr;
   int w = nm == 2 ? kPeW : kSe;
-  if (nx) {
+  if (xm) {
     if (edit) return SegChoice{nullptr, 0};
-    fn = nm == 2 ? (const void *)engine_tri_x_kernel<kPeW, 2, G, F> : (const void *)engine_tri_x_kernel<kSe, 1, G, F>;
-    std::snprintf(name, cap, "hpgq::engine_tri_x_kernel<%d, %d, %s%s>", w, nm, kGeoName, F ? ", follow" : "");
+    fn = xm == X_NOOR ? x_kernel<F, X_NOOR>(nm) : xm == X_LR ? x_kernel<F, X_LR>(nm) : x_kernel<F, X_NOOR | X_LR>(nm);
+    std::snprintf(name, cap, "hpgq::engine_tri_x_kernel<%d, %d, %s%s%s%s>", w, nm, kGeoName, F ? ", follow" : "",
+                  (xm & X_NOOR) ? ", noor" : "", (xm & X_LR) ? ", window" : "");
   } else {
     if (edit && nm == 2) return SegChoice{nullptr, 0};
     if (nm == 2) fn = (const void *)engine_tri_kernel<kPeW, 2, false, G, F>;
@@ -43,16 +49,16 @@ SegChoice pick(int nm, bool edit, bool nx, char *name, size_t cap) {
 }  // namespace
 
 #if HPGQ_GEO == 0
-SegChoice seg_kernel_tri(int nm, bool edit, bool nx, bool follow, char *name, size_t cap) {
-  return follow ? SegChoice{nullptr, 0} : pick<false>(nm, edit, nx, name, cap);
+SegChoice seg_kernel_tri(int nm, bool edit, int xm, bool follow, char *name, size_t cap) {
+  return follow ? SegChoice{nullptr, 0} : pick<false>(nm, edit, xm, name, cap);
 }
 #elif HPGQ_GEO == 1
-SegChoice seg_kernel_hex(int nm, bool edit, bool nx, bool follow, char *name, size_t cap) {
-  return follow ? SegChoice{nullptr, 0} : pick<false>(nm, edit, nx, name, cap);
+SegChoice seg_kernel_hex(int nm, bool edit, int xm, bool follow, char *name, size_t cap) {
+  return follow ? SegChoice{nullptr, 0} : pick<false>(nm, edit, xm, name, cap);
 }
 #else
-SegChoice seg_kernel_wide(int nm, bool edit, bool nx, bool follow, char *name, size_t cap) {
-  return follow ? pick<true>(nm, edit, nx, name, cap) : pick<false>(nm, edit, nx, name, cap);
+SegChoice seg_kernel_wide(int nm, bool edit, int xm, bool follow, char *name, size_t cap) {
+  return follow ? pick<true>(nm, edit, xm, name, cap) : pick<false>(nm, edit, xm, name, cap);
 }
 #endif
 

@@ -49,6 +49,7 @@ namespace hpgq {
 constexpr int kTriSlack = 8;    // readable bytes past the data end the loads may touch
 
 constexpr int GEO_TRI = 0, GEO_HEX = 1, GEO_WIDE = 2;
+constexpr int X_NOOR = 1, X_LR = 2;   // extra filter scans (engine_tri_x_kernel)
 
 // kBlock reads (<= 64: lane j <-> read j in the epilogue) in steps of kSegs
 // reads, kU steps per pipeline group, an even number of groups per block.
@@ -282,14 +283,22 @@ struct MateTag {
 // EDIT (NM = 1): the unit prologue trims each read (trim_word, written to
 // A.trim when the caller wants it) and describes it by its window [ts, n - te)
 // (offset + ts, length n - ts - te): stats and filter see the trimmed read.
-// NX: the filter also counts N bases and out-of-range qualities per read
-// (max_N, max_out_of_quality; src/filter_fastq.c): a second per-step scan
-// of (N | out-of-range << 16), its segment ends in a second LDS list.
+// XM (extra filter scans; the plain kernels have none):
+//   X_NOOR: the filter also counts N bases and out-of-range qualities per read
+//     (max_N, max_out_of_quality; src/filter_fastq.c:140-145): a second
+//     per-step scan of (N | out-of-range << 16), its segment ends in a second
+//     LDS list;
+//   X_LR: the 5'/3' window filters (left/right length + quality range,
+//     src/filter_fastq.c:140-145 args 6-11): a per-step scan of the window
+//     quality sums (left | right << 16; each < 255 x 252 < 2^16, and the
+//     segment sums come out exact as differences mod 2^32), the windows cut
+//     by two more rows of the byte-mask table.
 // FOLLOW: a follow-up stage (reads deferred by the stage before, by unit masks).
-template <int MINW, int NM, bool EDIT, int G, bool NX, bool FOLLOW>
+template <int MINW, int NM, bool EDIT, int G, int XM, bool FOLLOW>
 __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   static_assert(!EDIT || NM == 1, "edit on the segmented kernel is single-end");
-  static_assert(!(NX && EDIT), "the N / out-of-range filter variant does not edit");
+  constexpr bool NX = XM & X_NOOR, LR = XM & X_LR;
+  static_assert(!(XM && EDIT), "the extra-scan filter variants do not edit");
   using GG = Geo<G>;
   constexpr int NW = GG::kNW, kSegs = GG::kSegs, kSegW = GG::kSegW, kBlock = GG::kBlock, kU = GG::kU;
   static_assert(4 * kU <= kNibbleEvery && kBlock / kSegs - 4 * kU <= kNibbleEvery, "nibble widening");
@@ -314,6 +323,10 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   const int x_maxn = NX ? uni(A.cold->max_n) : 0, x_maxo = NX ? uni(A.cold->max_oor) : 0;
   const bool x_n = NX && (A.flags & F_NEED_N), x_o = NX && (A.flags & F_NEED_OOR);
   const bool x_all = A.flags & F_OOR_ALL, x_lonone = A.flags & F_OOR_LO_NONE, x_hinone = A.flags & F_OOR_HI_NONE;
+  // LR: the window filters, read once (see NX above); length 0 = off
+  const int w_ll = LR ? max(uni(A.cold->left_len), 0) : 0, w_rl = LR ? max(uni(A.cold->right_len), 0) : 0;
+  const int w_lmin = LR ? uni(A.cold->min_left) : 0, w_lmax = LR ? uni(A.cold->max_left) : 0;
+  const int w_rmin = LR ? uni(A.cold->min_right) : 0, w_rmax = LR ? uni(A.cold->max_right) : 0;
   // EDIT: the trim bounds, read once (see NX above)
   ColdParams cold{};
   if (EDIT) cold = *A.cold;
@@ -324,7 +337,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   // LDS per mate: pos_acc [6][lmax] u32 | hist [hlen] u32 | sc [8] u64, then
   // per wave: per mate two read tables [64] x 16 B (seq offset, qual offset,
   // length | alignments, -) alternating between blocks, and segment ends [64]
-  // (+ [64] NX), then a compaction scratch [64] u32 and a deferral word (u64,
+  // (+ [64] NX, + [64] LR), then a compaction scratch [64] u32 and a deferral word (u64,
   // disjoint from the scratch: no type-punned aliasing); then the byte-mask table.
   // (pos_acc row 5 holds "other" counts until the epilogue turns it into N)
   const int hist_words = (hlen + 1) & ~1;
@@ -336,13 +349,16 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   auto sc = [&](int m) __attribute__((always_inline)) {
     return reinterpret_cast<unsigned long long *>(base + m * mate_words + 6 * lmax + hist_words);
   };
-  constexpr int kMateWaveWords = 2 * 256 + (NX ? 128 : 64);
+  constexpr int kMateWaveWords = 2 * 256 + 64 * (1 + (NX ? 1 : 0) + (LR ? 1 : 0));
   constexpr int kWaveWords = NM * kMateWaveWords + 64 + 4;   // (multiple of 4: 16 B tables)
   const int tab_words = (NM * mate_words + 3) & ~3;   // 16 B aligned (host: + 16 B)
   uint32_t *wtab = base + tab_words + wave * kWaveWords;
   auto tab = [&](int m, int tb) __attribute__((always_inline)) { return wtab + m * kMateWaveWords + tb * 256; };
   auto wends = [&](int m) __attribute__((always_inline)) { return wtab + m * kMateWaveWords + 2 * 256; };
   auto wends2 = [&](int m) __attribute__((always_inline)) { return wtab + m * kMateWaveWords + 2 * 256 + 64; };   // NX only
+  auto wends3 = [&](int m) __attribute__((always_inline)) {   // LR only
+    return wtab + m * kMateWaveWords + 2 * 256 + (NX ? 128 : 64);
+  };
   uint32_t *scratch = wtab + NM * kMateWaveWords;
   unsigned long long *dword = reinterpret_cast<unsigned long long *>(scratch + 64);   // 8 B aligned
   // byte masks by valid-byte count c = clamp(n - p0, 0, 4 NW): mtab[c][w]
@@ -480,9 +496,25 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     }
   };
 
-  // one step: per-lane partial (raw quality | G+C << 18); adds (SUB = false)
-  // or removes (SUB = true) the lane's positions from mate m's counters
-  auto account = [&](auto mtag, const TriPending<NW> &pd, bool count, auto sub_tag, uint32_t &x2) __attribute__((always_inline)) -> uint32_t {
+  // byte masks of the lane's words for the positions < p0 + c (c clamped to [0, 4 NW])
+  auto mask_row = [&](int c, uint32_t (&mk)[NW]) __attribute__((always_inline)) {
+    c = min(max(c, 0), 4 * NW);
+    if (NW == 4) {
+      const v4u t = *reinterpret_cast<const v4u *>(mtab + 4 * c);
+#pragma unroll
+      for (int w = 0; w < NW; ++w) mk[w] = t[w & 3];
+    } else {
+      const v2u t = *reinterpret_cast<const v2u *>(mtab + 2 * c);
+#pragma unroll
+      for (int w = 0; w < NW; ++w) mk[w] = t[w & 1];
+    }
+  };
+
+  // one step: per-lane partial (biased quality | G+C << 18); adds (SUB = false)
+  // or removes (SUB = true) the lane's positions from mate m's counters;
+  // NX: x2 = N | out-of-range << 16; LR: x3 = left | right window sums
+  auto account = [&](auto mtag, const TriPending<NW> &pd, bool count, auto sub_tag, uint32_t &x2,
+                     uint32_t &x3) __attribute__((always_inline)) -> uint32_t {
     constexpr int m = decltype(mtag)::value;
     constexpr bool SUB = decltype(sub_tag)::value;
     uint32_t sw[NW], qw[NW];
@@ -496,18 +528,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       }
     }
     uint32_t mk[NW];
-    {
-      const int c = min(max((int)(pd.n & 0xFFFFu) - p0, 0), 4 * NW);
-      if (NW == 4) {
-        const v4u t = *reinterpret_cast<const v4u *>(mtab + 4 * c);
-#pragma unroll
-        for (int w = 0; w < NW; ++w) mk[w] = t[w & 3];
-      } else {
-        const v2u t = *reinterpret_cast<const v2u *>(mtab + 2 * c);
-#pragma unroll
-        for (int w = 0; w < NW; ++w) mk[w] = t[w & 1];
-      }
-    }
+    mask_row((int)(pd.n & 0xFFFFu) - p0, mk);
     uint32_t qm[NW], cd[NW];
     uint32_t bad = 0;
 #pragma unroll
@@ -570,6 +591,18 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       }
       x2 = nn | (oo << 16);
     }
+    if (LR && !SUB) {   // window sums: positions < min(left, n) and >= n - min(right, n)
+      const int n = (int)(pd.n & 0xFFFFu);
+      uint32_t ml[NW], mr[NW], sl = 0, sr = 0;
+      mask_row(min(w_ll, n) - p0, ml);
+      mask_row(n - min(w_rl, n) - p0, mr);
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        sl = __builtin_amdgcn_sad_u8(qm[w] & ml[w], 0u, sl);
+        sr = __builtin_amdgcn_sad_u8(__builtin_amdgcn_bitop3_b32(qm[w], mr[w], 0u, 0x30), 0u, sr);   // qm & ~mr
+      }
+      x3 = sl | (sr << 16);
+    }
     return qs + (gc << 18);
   };
 
@@ -614,14 +647,18 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
         for (int u = 0; u < kU; ++u) {
           const int t = g * kU + u;
           // every read is added; failed ones are taken out in the unit epilogue
-          uint32_t x2 = 0;
-          const uint32_t x = account(MateTag<m>{}, grp[slot][u], stats, AddTag{}, x2);
+          uint32_t x2 = 0, x3 = 0;
+          const uint32_t x = account(MateTag<m>{}, grp[slot][u], stats, AddTag{}, x2, x3);
           const uint32_t P = wave_scan(x);
           // segment ends (the last lane of each segment) -> wends[kSegs t + seg], no wait needed
           if (ls == kSegW - 1 && seg < kSegs && t < nt) wends(m)[kSegs * t + seg] = P;
           if (NX) {
             const uint32_t P2 = wave_scan(x2);
             if (ls == kSegW - 1 && seg < kSegs && t < nt) wends2(m)[kSegs * t + seg] = P2;
+          }
+          if (LR) {
+            const uint32_t P3 = wave_scan(x3);
+            if (ls == kSegW - 1 && seg < kSegs && t < nt) wends3(m)[kSegs * t + seg] = P3;
           }
         }
       };
@@ -675,6 +712,16 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
         if (x_n && (int)(r2 & 0xFFFFu) > x_maxn) pass = false;
         if (x_o && (int)(r2 >> 16) > x_maxo) pass = false;
       }
+      if (LR && filter) {   // min*k <= S - phred*k <= max*k over each window (k = min(len, n))
+        const uint32_t e3 = inb ? wends3(m)[lane] : 0u;
+        const uint32_t p3 = __builtin_amdgcn_mov_dpp(e3, 0x138, 0xF, 0xF, true);   // lane j-1
+        const uint32_t r3 = e3 - (((not_seg_first >> lane) & 1u) ? p3 : 0u);
+        const int kl = min(w_ll, n), kr = min(w_rl, n);
+        if (kl > 0 && !mean_in((int64_t)(r3 & 0xFFFFu), kl, A.phred, w_lmin, w_lmax))
+          pass = false;
+        if (kr > 0 && !mean_in((int64_t)(r3 >> 16), kr, A.phred, w_rmin, w_rmax))
+          pass = false;
+      }
     }
     if (valid && A.mask) A.mask[my_read] = (uint8_t)pass;
     const uint64_t failed = __ballot(valid && !pass);
@@ -725,15 +772,15 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
         nsub = max(nsub, n);
         if (c == seg) mycnt = n;
       }
-      uint32_t sub_x2 = 0;   // (unused: failed reads leave the counters only)
+      uint32_t sub_x2 = 0, sub_x3 = 0;   // (unused: failed reads leave the counters only)
       for (int k = 0; k < nsub; ++k) {
         const int src = seg < kSegs && k < mycnt ? (int)flist[min(k * kSegs + seg, 63)] : 63;
         TriPending<NW> pd;
         gather(0, tb, src, pd);
-        (void)account(MateTag<0>{}, pd, true, SubTag{}, sub_x2);
+        (void)account(MateTag<0>{}, pd, true, SubTag{}, sub_x2, sub_x3);
         if (NM == 2) {
           gather(NM - 1, tb, src, pd);
-          (void)account(MateTag<NM - 1>{}, pd, true, SubTag{}, sub_x2);
+          (void)account(MateTag<NM - 1>{}, pd, true, SubTag{}, sub_x2, sub_x3);
         }
       }
     }
@@ -773,23 +820,23 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
 
 template <int MINW, int NM, bool EDIT, int G, bool FOLLOW>
 __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
-  tri_body<MINW, NM, EDIT, G, false, FOLLOW>(A);
+  tri_body<MINW, NM, EDIT, G, 0, FOLLOW>(A);
 }
 
-// the segmented kernel with the N / out-of-range read filters (no edit)
-template <int MINW, int NM, int G, bool FOLLOW>
+// the segmented kernel with extra filter scans (XM: X_NOOR | X_LR; no edit)
+template <int MINW, int NM, int G, bool FOLLOW, int XM>
 __global__ void __launch_bounds__(kWG, MINW) engine_tri_x_kernel(EngineArgs A) {
-  tri_body<MINW, NM, false, G, true, FOLLOW>(A);
+  tri_body<MINW, NM, false, G, XM, FOLLOW>(A);
 }
 
 // kernel selection (one translation unit per geometry, hpgq_engine_geo.hip):
-// the instance for (NM, edit, nx, follow) or nullptr; name gets its signature
+// the instance for (NM, edit, xm, follow) or nullptr; name gets its signature
 struct SegChoice {
   const void *fn;
   int min_waves;
 };
-SegChoice seg_kernel_tri(int nm, bool edit, bool nx, bool follow, char *name, size_t cap);
-SegChoice seg_kernel_hex(int nm, bool edit, bool nx, bool follow, char *name, size_t cap);
-SegChoice seg_kernel_wide(int nm, bool edit, bool nx, bool follow, char *name, size_t cap);
+SegChoice seg_kernel_tri(int nm, bool edit, int xm, bool follow, char *name, size_t cap);
+SegChoice seg_kernel_hex(int nm, bool edit, int xm, bool follow, char *name, size_t cap);
+SegChoice seg_kernel_wide(int nm, bool edit, int xm, bool follow, char *name, size_t cap);
 
 }  // namespace hpgq

@@ -376,6 +376,42 @@ def test_n_oor_filters_route_to_segmented_kernel(name, geo_choice):
     assert_same(p, O.synth(600_000, seed=23, L=150, trunc_pct=5, n_per_1024=12))
 
 
+WINDOW_CASES = {
+    "c2_left10": dict(read_quality_range="20,", read_length_range="50,", left_length=10,
+                      left_quality_range="20,"),
+    "right30": dict(right_length=30, right_quality_range="18,35"),
+    "both_wide": dict(left_length=40, left_quality_range="25,", right_length=100,
+                      right_quality_range=",30"),
+    "longer_than_reads": dict(left_length=300, left_quality_range="20,", right_length=1,
+                              right_quality_range="5,"),
+    "with_n_oor": dict(read_quality_range="10,38", max_N=1, max_out_of_quality=10, left_length=10,
+                       left_quality_range="20,", right_length=7, right_quality_range="12,"),
+}
+
+
+@pytest.mark.parametrize("name", sorted(WINDOW_CASES))
+def test_window_filters_route_to_segmented_kernel(name, geo_choice):
+    """The 5'/3' window filters (src/filter_fastq.c:140-145 args 6-11) run on the
+    segmented kernel's window-scan variant, bit-identical to the oracle, at a
+    size that gives every wave several blocks."""
+    p = H.stats_params(lmax=150, **WINDOW_CASES[name])
+    with H.Engine(p) as e:
+        assert "engine_tri_x_kernel" in e.kernel_name and "window" in e.kernel_name, e.kernel_chain
+        assert ("noor" in e.kernel_name) == (name == "with_n_oor")
+        assert ("hex" if geo_choice == "auto" else geo_choice) in e.kernel_name
+    assert_same(p, O.synth(600_000, seed=24, L=150, trunc_pct=5, n_per_1024=12))
+
+
+def test_window_filters_paired(geo_choice):
+    p = H.stats_params(lmax=150, **WINDOW_CASES["c2_left10"])
+    p.paired = 1
+    r1 = O.synth(300_000, seed=25, L=150, trunc_pct=5, mate=0)
+    r2 = O.synth(300_000, seed=25, L=150, trunc_pct=5, mate=1)
+    with H.Engine(p) as e:
+        assert "window" in e.kernel_name, e.kernel_chain
+    assert_same(p, r1, r2)
+
+
 # ---- routing by the reads' actual lengths (DESIGN §4.0) ---------------------
 C2 = dict(read_quality_range="20,", read_length_range="50,")
 
@@ -413,7 +449,7 @@ def test_250bp_reads(lmax, kernel_choice):
     assert_same(p, O.synth(120_000, seed=32, L=250, trunc_pct=10, n_per_1024=4))
 
 
-@pytest.mark.parametrize("case", ["stats", "c2", "nx", "filter_only", "edit"])
+@pytest.mark.parametrize("case", ["stats", "c2", "nx", "window", "filter_only", "edit"])
 def test_mixed_length_batches(case, kernel_choice):
     """Every stage of the chain in one batch: 20..156 (hex), 157..252 (wide),
     253..1024 (catch-all pipeline), > 1260 (catch-all chunk loop)."""
@@ -425,6 +461,9 @@ def test_mixed_length_batches(case, kernel_choice):
         p = H.stats_params(lmax=1024, read_quality_range="20,", read_length_range="50,1024")
     elif case == "nx":
         p = H.stats_params(lmax=1024, read_length_range=",1024", max_N=1, max_out_of_quality=40)
+    elif case == "window":
+        p = H.stats_params(lmax=1024, read_length_range=",1024", left_length=12, left_quality_range="22,",
+                           right_length=20, right_quality_range="15,")
     elif case == "filter_only":   # no stats: every length is filtered, no error
         p = H.filter_params(lmax=150, read_quality_range="20,", read_length_range="50,", max_N=3)
     else:   # edit without stats: trims of every length
