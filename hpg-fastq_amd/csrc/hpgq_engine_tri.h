@@ -327,6 +327,9 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   const int w_ll = LR ? max(uni(A.cold->left_len), 0) : 0, w_rl = LR ? max(uni(A.cold->right_len), 0) : 0;
   const int w_lmin = LR ? uni(A.cold->min_left) : 0, w_lmax = LR ? uni(A.cold->max_left) : 0;
   const int w_rmin = LR ? uni(A.cold->min_right) : 0, w_rmax = LR ? uni(A.cold->max_right) : 0;
+  // a left window within a lane's positions and no right window: no scan (the
+  // segment's first lane stores its sum)
+  const bool w_direct = LR && w_rl == 0 && w_ll <= 4 * NW;
   // EDIT: the trim bounds, read once (see NX above)
   ColdParams cold{};
   if (EDIT) cold = *A.cold;
@@ -593,13 +596,19 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     }
     if (LR && !SUB) {   // window sums: positions < min(left, n) and >= n - min(right, n)
       const int n = (int)(pd.n & 0xFFFFu);
-      uint32_t ml[NW], mr[NW], sl = 0, sr = 0;
-      mask_row(min(w_ll, n) - p0, ml);
-      mask_row(n - min(w_rl, n) - p0, mr);
+      uint32_t sl = 0, sr = 0;
+      if (w_ll > 0) {   // (uniform: scalar branches)
+        uint32_t ml[NW];
+        mask_row(min(w_ll, n) - p0, ml);
 #pragma unroll
-      for (int w = 0; w < NW; ++w) {
-        sl = __builtin_amdgcn_sad_u8(qm[w] & ml[w], 0u, sl);
-        sr = __builtin_amdgcn_sad_u8(__builtin_amdgcn_bitop3_b32(qm[w], mr[w], 0u, 0x30), 0u, sr);   // qm & ~mr
+        for (int w = 0; w < NW; ++w) sl = __builtin_amdgcn_sad_u8(qm[w] & ml[w], 0u, sl);
+      }
+      if (w_rl > 0) {
+        uint32_t mr[NW];
+        mask_row(n - min(w_rl, n) - p0, mr);
+#pragma unroll
+        for (int w = 0; w < NW; ++w)
+          sr = __builtin_amdgcn_sad_u8(__builtin_amdgcn_bitop3_b32(qm[w], mr[w], 0u, 0x30), 0u, sr);   // qm & ~mr
       }
       x3 = sl | (sr << 16);
     }
@@ -657,8 +666,12 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
             if (ls == kSegW - 1 && seg < kSegs && t < nt) wends2(m)[kSegs * t + seg] = P2;
           }
           if (LR) {
-            const uint32_t P3 = wave_scan(x3);
-            if (ls == kSegW - 1 && seg < kSegs && t < nt) wends3(m)[kSegs * t + seg] = P3;
+            if (w_direct) {   // the segment's first lane holds the whole window sum
+              if (ls == 0 && seg < kSegs && t < nt) wends3(m)[kSegs * t + seg] = x3;
+            } else {
+              const uint32_t P3 = wave_scan(x3);
+              if (ls == kSegW - 1 && seg < kSegs && t < nt) wends3(m)[kSegs * t + seg] = P3;
+            }
           }
         }
       };
@@ -715,7 +728,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       if (LR && filter) {   // min*k <= S - phred*k <= max*k over each window (k = min(len, n))
         const uint32_t e3 = inb ? wends3(m)[lane] : 0u;
         const uint32_t p3 = __builtin_amdgcn_mov_dpp(e3, 0x138, 0xF, 0xF, true);   // lane j-1
-        const uint32_t r3 = e3 - (((not_seg_first >> lane) & 1u) ? p3 : 0u);
+        const uint32_t r3 = w_direct ? e3 : e3 - (((not_seg_first >> lane) & 1u) ? p3 : 0u);
         const int kl = min(w_ll, n), kr = min(w_rl, n);
         if (kl > 0 && !mean_in((int64_t)(r3 & 0xFFFFu), kl, A.phred, w_lmin, w_lmax))
           pass = false;

@@ -8,8 +8,13 @@
  * <in>.nucleotides.data (:336-352), and with --kmers <in>.kmers.txt and
  * <in>.kmers.per.nt.data (:492-530) plus the summary's k-mer list (:144-150).  Values come from the dense device
  * counters: per-position maps are read by position, not by
- * khash bucket (quirk Q3); the mean quality is the exact fixed-point mean
- * (quirk Q2).  The gnuplot images are not produced (gnuplot is absent).
+ * khash bucket (quirk Q3); the mean quality comes from the exact fixed-point
+ * sum of per-read means, converted to float once (quirk Q2).  The arithmetic is
+ * the reference's: `1.0f * a / b` and `100.0f * a / b` in float, `%i` of a
+ * size_t count prints its low 32 bits; empty runs print 0 where the reference
+ * divides by zero (quirk Q14).  tests/test_cli_gpu.py compares every file byte
+ * for byte with oracle/report_ref.py.  The gnuplot images are not produced
+ * (gnuplot is absent).
  */
 #include <math.h>
 #include <stdio.h>
@@ -19,6 +24,12 @@
 #include "hpgq_cli.h"
 
 #define NORM_Q(q, phred) ((int)round((q) - (phred)))   /* _normalize_quality, :26 */
+
+/* `%i` of a size_t count (src/stats_report.c:176,229,385): its low 32 bits */
+static int i32(uint64_t v) { return (int)(uint32_t)v; }
+
+/* `1.0f * a / b`, 0 when b = 0 (Q14) */
+static float fdiv(uint64_t a, uint64_t b) { return b ? 1.0f * a / b : 0.0f; }
 
 static FILE *open_out(const cli_options_t *o, const char *base, const char *suffix) {
   char path[4096];
@@ -184,7 +195,10 @@ int cli_report(const cli_options_t *o, const hpgq_params_t *p, const uint64_t *c
   fprintf(f, "Read length (min., mean, max.): (%i, %0.2f, %i)\n", s.num_reads ? s.min_length : 0,
           s.num_reads ? 1.0f * s.acc_length / s.num_reads : 0.0f, maxlen);
   fprintf(f, "\n");
-  int qual = NORM_Q(s.mean_quality_raw, phred);
+  /* acc_quality (float in the reference, :297): the exact sum of per-read raw
+   * means (fixed point, two's complement), converted to float once (Q2) */
+  const float acc_q = (float)((double)(int64_t)c[HPGQ_S_ACC_MEANQ_FX16] / 65536.0);
+  int qual = NORM_Q(s.num_reads ? 1.0f * acc_q / s.num_reads : 0.0f, phred);
   fprintf(f, "Mean quality = %i [%c]\n", qual, qual + phred);
   fprintf(f, "\n");
   fprintf(f, "Nucleotide content (A, C, G, T, N)\n");
@@ -198,7 +212,7 @@ int cli_report(const cli_options_t *o, const hpgq_params_t *p, const uint64_t *c
   fprintf(f, "\n");
   fprintf(f, "Mean quality per nucleotide position\n");
   for (int k = 0; k < maxlen; k++) {
-    qual = cnt[k] ? NORM_Q(1.0 * pq[k] / cnt[k], phred) : 0;
+    qual = NORM_Q(fdiv(pq[k], cnt[k]), phred);
     fprintf(f, "\tpos. %i: %i [%c]\t", k + 1, qual, qual + phred);
     if ((k + 1) % 5 == 0) fprintf(f, "\n");
   }
@@ -226,22 +240,24 @@ int cli_report(const cli_options_t *o, const hpgq_params_t *p, const uint64_t *c
   }
 
   if ((f = open_out(o, base, "length.histogram.data"))) {
-    for (int i = 1; i <= maxlen; i++) fprintf(f, "%i\t%lu\n", i, (unsigned long)hl[i]);
+    for (int i = 1; i <= maxlen; i++) fprintf(f, "%i\t%i\n", i, i32(hl[i]));
     fclose(f);
   }
   if ((f = open_out(o, base, "read.quality.histogram.data"))) {
-    int lo = -1, hi = -1;
+    /* keys are signed (bin = key & 255, Q13); min..max key as :368-385 */
+    int lo = 1000, hi = -1000;
     for (int i = 0; i < HPGQ_MEANQ_BINS; i++)
       if (hq[i]) {
-        if (lo < 0) lo = i;
-        hi = i;
+        const int key = i >= 128 ? i - 256 : i;
+        if (key < lo) lo = key;
+        if (key > hi) hi = key;
       }
-    for (int i = lo; lo >= 0 && i <= hi; i++) fprintf(f, "%i\t%lu\n", i - phred, (unsigned long)hq[i]);
+    for (int key = lo; key <= hi; key++) fprintf(f, "%i\t%i\n", key - phred, i32(hq[key & 255]));
     fclose(f);
   }
   if ((f = open_out(o, base, "GC.histogram.data"))) {
     for (int i = 1; i < 100; i++)
-      if (hg[i]) fprintf(f, "%i\t%lu\n", i, (unsigned long)hg[i]);
+      if (hg[i]) fprintf(f, "%i\t%i\n", i, i32(hg[i]));
     fclose(f);
   }
   if ((f = open_out(o, base, "GC.per.nt.data"))) {
@@ -254,15 +270,16 @@ int cli_report(const cli_options_t *o, const hpgq_params_t *p, const uint64_t *c
   }
   if ((f = open_out(o, base, "quality.per.nt.data"))) {
     for (int k = 0; k < maxlen; k++)
-      fprintf(f, "%i\t%i\n", k, cnt[k] ? NORM_Q(1.0 * pq[k] / cnt[k], phred) : 0);
+      fprintf(f, "%i\t%i\n", k, NORM_Q(fdiv(pq[k], cnt[k]), phred));
     fclose(f);
   }
   if ((f = open_out(o, base, "nucleotides.data"))) {
     for (int k = 0; k < maxlen; k++) {
       const uint64_t t = pA[k] + pC[k] + pG[k] + pT[k] + pN[k];
-      const float d = t ? 100.0f / t : 0.0f;
-      fprintf(f, "%i\t%0.2f\t%0.2f\t%0.2f\t%0.2f\t%0.2f\n", k + 1, d * pA[k], d * pT[k], d * pG[k],
-              d * pC[k], d * pN[k]);
+#define PCT(x) (t ? 100.0f * (x) / t : 0.0f)
+      fprintf(f, "%i\t%0.2f\t%0.2f\t%0.2f\t%0.2f\t%0.2f\n", k + 1, PCT(pA[k]), PCT(pT[k]), PCT(pG[k]),
+              PCT(pC[k]), PCT(pN[k]));
+#undef PCT
     }
     fclose(f);
   }

@@ -384,6 +384,7 @@ WINDOW_CASES = {
                       right_quality_range=",30"),
     "longer_than_reads": dict(left_length=300, left_quality_range="20,", right_length=1,
                               right_quality_range="5,"),
+    "left16_n": dict(left_length=16, left_quality_range="28,", max_N=2),   # no scan on hex
     "with_n_oor": dict(read_quality_range="10,38", max_N=1, max_out_of_quality=10, left_length=10,
                        left_quality_range="20,", right_length=7, right_quality_range="12,"),
 }
@@ -397,7 +398,7 @@ def test_window_filters_route_to_segmented_kernel(name, geo_choice):
     p = H.stats_params(lmax=150, **WINDOW_CASES[name])
     with H.Engine(p) as e:
         assert "engine_tri_x_kernel" in e.kernel_name and "window" in e.kernel_name, e.kernel_chain
-        assert ("noor" in e.kernel_name) == (name == "with_n_oor")
+        assert ("noor" in e.kernel_name) == (name in ("with_n_oor", "left16_n"))
         assert ("hex" if geo_choice == "auto" else geo_choice) in e.kernel_name
     assert_same(p, O.synth(600_000, seed=24, L=150, trunc_pct=5, n_per_1024=12))
 

@@ -4,7 +4,7 @@ set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/check
 if [ -z "$SKIP_TESTS" ]; then
-  timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread ${PYTEST_ARGS} > gpurun_out/check/pytest_gpu.log 2>&1 || exit 3
+  timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/check/pytest_gpu.log 2>&1 || exit 3
 fi
 timeout -k 10 300 python bench.py > gpurun_out/check/bench.json 2> gpurun_out/check/bench.err || exit 4
 for c in ${CFGS}; do
