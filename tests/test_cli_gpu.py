@@ -46,9 +46,35 @@ def test_cli_stats_matches_oracle(tmp_path, chunk_mb):
     np.testing.assert_array_equal(got, want)
     summ = (out / "in.fq.summary.txt").read_text()
     assert f"Number of processed reads: {int(want[H.S_NUM_PASSED])}" in summ
-    for f in ("length.histogram.data", "read.quality.histogram.data", "GC.histogram.data",
-              "GC.per.nt.data", "quality.per.nt.data", "nucleotides.data"):
-        assert (out / f"in.fq.{f}").exists(), f
+    # every report file, byte for byte, as the restatement of src/stats_report.c
+    # makes it from the same counters
+    from oracle import report_ref
+    exp = report_ref.report_files(got, 150, 33, "in.fq",
+                                  {"filter_on": True, "read_quality_range": "20,",
+                                   "read_length_range": "50,"})
+    for suffix, data in exp.items():
+        assert (out / f"in.fq.{suffix}").read_bytes() == data, suffix
+
+
+@pytest.mark.parametrize("case", ["plain", "filter"])
+def test_cli_report_golden(tmp_path, case):
+    """`hpg-fastq stats` report files == the committed golden set
+    (tests/golden/report/, made by tests/golden/make_report_golden.py from the
+    restatements of src/stats_fastq.c:257-417 and src/stats_report.c:60-390),
+    byte for byte."""
+    import filecmp
+    import importlib.util
+    gold = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    spec = importlib.util.spec_from_file_location("mrg", os.path.join(gold, "make_report_golden.py"))
+    mrg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mrg)
+    flags = mrg.CASES[case][0]
+    run_cli(["stats", "-f", os.path.join(gold, "report", mrg.FQ), "-o", tmp_path, *flags, "--quiet"])
+    want_dir = os.path.join(gold, "report", case)
+    names = sorted(os.listdir(want_dir))
+    assert len(names) == 7
+    for name in names:
+        assert filecmp.cmp(os.path.join(want_dir, name), tmp_path / name, shallow=False), name
 
 
 @pytest.mark.parametrize("crlf", [False, True])

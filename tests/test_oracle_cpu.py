@@ -76,6 +76,23 @@ def test_kat_signed_qualities(section):
             np.testing.assert_array_equal(trim, exp["trim"])
 
 
+@pytest.mark.parametrize("case", ["plain", "filter"])
+def test_report_golden_files(case):
+    """The committed report files (tests/golden/report/) are what the
+    restatement of src/stats_report.c (oracle/report_ref.py) makes of the
+    pure-Python counters of their input."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("mrg", os.path.join(GOLD, "make_report_golden.py"))
+    mrg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mrg)
+    rd = read_fastq(os.path.join(GOLD, "report", mrg.FQ))
+    files = mrg.expected(case, rd)
+    assert len(files) == 7
+    for suffix, data in files.items():
+        with open(os.path.join(GOLD, "report", case, f"{mrg.FQ}.{suffix}"), "rb") as f:
+            assert f.read() == data, suffix
+
+
 def test_kat_cgr():
     c = KAT["cgr"]
     reads = read_fastq(os.path.join(GOLD, c["reads"]))
