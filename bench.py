@@ -274,15 +274,14 @@ def main():
         kernel_name = "hpgq::cgr::stream::cgr_stream_kernel<7> (+span_first)"
         # algorithmic bytes per read: seq + quality + offset (tables stay in LDS)
         alg = [nb for (_n, _m, nb) in batches]
-        red = torch.zeros(2 * 128 * 128 + 1, dtype=torch.int64, device=dev) if world > 1 else None
     else:
         eng = H.Engine(params, device=local)
         kernel_name = eng.kernel_name
-        if world > 1:
-            uid = H.engine.comm_unique_id() if rank == 0 else b"\0" * 128
-            obj = [uid]
-            dist.broadcast_object_list(obj, src=0)
-            eng.comm_init(world, rank, obj[0])
+    if world > 1:   # one RCCL communicator inside libhpgq (counters / CGR tables)
+        uid = H.engine.comm_unique_id() if rank == 0 else b"\0" * 128
+        obj = [uid]
+        dist.broadcast_object_list(obj, src=0)
+        eng.comm_init(world, rank, obj[0])
         # + 1 B mask per read (pair), + 4 B trim per read when editing
         alg = [nb + n + (4 * n * mates if params.edit_on else 0) for (n, _m, nb) in batches]
     ext = torch.cuda.ExternalStream(eng.stream, device=dev)
@@ -304,15 +303,8 @@ def main():
                                d_trim.data_ptr() + 4 * int(offs[i]) if params.edit_on else None)
             if timed:
                 ev[i][1].record(ext)
-        if world > 1:
-            if cgr:   # the one exchange step: sum the tables (RCCL via torch.distributed)
-                ts, tq, wc = eng.tables()
-                red.copy_(torch.from_numpy(np.concatenate(
-                    [ts.reshape(-1).astype(np.int64), tq.reshape(-1).astype(np.int64),
-                     np.array([wc], np.int64)])))
-                dist.all_reduce(red)
-            else:
-                eng.allreduce()
+        if world > 1:   # the one exchange step: RCCL sum of the counters / u32 CGR tables
+            eng.allreduce()
 
     for _ in range(args.warmup):
         step(False)
@@ -377,7 +369,8 @@ def main():
         "data": "synthetic (counter-based generator, resident in HBM)",
         "config": {"workload": cfg["workload"], "reads_per_gpu": args.reads, "read_length": L,
                    "batch_reads": args.batch_reads,
-                   "parallelism": f"read-sharded x{world}, RCCL all-reduce of counters"},
+                   "parallelism": f"read-sharded x{world}, RCCL all-reduce of "
+                                  + ("the u32 CGR tables" if cgr else "the counters")},
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "kernel": kernel_name,

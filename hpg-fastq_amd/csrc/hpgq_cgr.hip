@@ -32,6 +32,8 @@
 // keeps the relative history through a run of halvings) and then pay a serial
 // replay for those reads only.  The word count does not depend on f, so it is
 // exact from the first kernel.
+#include <rccl/rccl.h>
+#include <cstring>
 #include "hpgq_common.h"
 
 #include <algorithm>
@@ -675,6 +677,11 @@ struct hpgq_cgr {
   bool ran_exact = false;                 // an exact simulation ran since the last sync
   int last_exact = 0;
   int s_grid = 0;
+  // RCCL (hpgq_cgr_allreduce): [table_seq | table_q | word count] u32, packed
+  // and summed out of place; reads return the sum until the next fill / reset
+  ncclComm_t comm = nullptr;
+  uint32_t *d_pack = nullptr, *d_global = nullptr;
+  bool reduced = false;
 };
 
 static int cgr_ensure(hpgq_cgr *c, int64_t n) {
@@ -796,6 +803,9 @@ void hpgq_cgr_close(hpgq_cgr_t *c) {
   (void)hipFree(c->d_span_first);
   (void)hipFree(c->d_scratch);
   (void)hipFree(c->d_slots);
+  (void)hipFree(c->d_pack);
+  (void)hipFree(c->d_global);
+  if (c->comm) ncclCommDestroy(c->comm);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -806,6 +816,7 @@ int hpgq_cgr_fill_device(hpgq_cgr_t *c, const hpgq_batch_t *b, const uint8_t *st
   if (b->num_reads == 0) return HPGQ_OK;
   if (!b->seq || !b->quality || !b->data_indices) return HPGQ_E_INVALID;
   HPGQ_HIP_TRY(hipSetDevice(c->device));
+  c->reduced = false;
   const bool streamed = c->path == HPGQ_CGR_PATH_AUTO && mode == HPGQ_CGR_ALL_READS &&
                         c->k <= hpgq::cgr::stream::kMaxK;
   if (!streamed) return cgr_exact(c, b, status, mode);
@@ -873,6 +884,7 @@ int hpgq_cgr_reset(hpgq_cgr_t *c) {
   HPGQ_HIP_TRY(hipMemsetAsync(c->d_ts, 0, cells * 4, c->stream));
   HPGQ_HIP_TRY(hipMemsetAsync(c->d_tq, 0, cells * 4, c->stream));
   HPGQ_HIP_TRY(hipMemsetAsync(c->d_words, 0, 8, c->stream));
+  c->reduced = false;
   return HPGQ_OK;
 }
 
@@ -881,6 +893,12 @@ int hpgq_cgr_read(hpgq_cgr_t *c, uint32_t *table_seq, uint32_t *table_q, uint32_
   int rc = hpgq_cgr_sync(c);
   if (rc) return rc;
   const size_t cells = (size_t)c->dim * c->dim;
+  if (c->reduced) {   // the all-reduced tables (hpgq_cgr_allreduce)
+    if (table_seq) HPGQ_HIP_TRY(hipMemcpy(table_seq, c->d_global, cells * 4, hipMemcpyDeviceToHost));
+    if (table_q) HPGQ_HIP_TRY(hipMemcpy(table_q, c->d_global + cells, cells * 4, hipMemcpyDeviceToHost));
+    if (word_count) HPGQ_HIP_TRY(hipMemcpy(word_count, c->d_global + 2 * cells, 4, hipMemcpyDeviceToHost));
+    return HPGQ_OK;
+  }
   if (table_seq) HPGQ_HIP_TRY(hipMemcpy(table_seq, c->d_ts, cells * 4, hipMemcpyDeviceToHost));
   if (table_q) HPGQ_HIP_TRY(hipMemcpy(table_q, c->d_tq, cells * 4, hipMemcpyDeviceToHost));
   if (word_count) {
@@ -902,5 +920,48 @@ int hpgq_cgr_set_path(hpgq_cgr_t *c, int path) {
 }
 
 int hpgq_cgr_last_exact(hpgq_cgr_t *c) { return c ? c->last_exact : HPGQ_E_INVALID; }
+
+// ---------------------------------------------------------------------------
+// RCCL (one process per GPU): the table sum of read-sharded fills
+// ---------------------------------------------------------------------------
+
+int hpgq_cgr_comm_init(hpgq_cgr_t *c, int nranks, int rank, const char id[HPGQ_COMM_ID_BYTES]) {
+  if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return HPGQ_E_INVALID;
+  if (c->comm) return HPGQ_E_STATE;
+  HPGQ_HIP_TRY(hipSetDevice(c->device));
+  const size_t words = 2 * (size_t)c->dim * c->dim + 1;
+  if (!c->d_pack) HPGQ_HIP_TRY(hipMalloc(&c->d_pack, words * 4));
+  if (!c->d_global) HPGQ_HIP_TRY(hipMalloc(&c->d_global, words * 4));
+  ncclUniqueId u;
+  std::memcpy(&u, id, sizeof(u));
+  if (ncclCommInitRank(&c->comm, nranks, u, rank) != ncclSuccess) {
+    c->comm = nullptr;
+    return HPGQ_E_RCCL;
+  }
+  return HPGQ_OK;
+}
+
+// Sum of every rank's tables and word count as u32, so the sum wraps like the
+// reference's unsigned tables and fq_word_count (old/chaos_game.c:253-258).
+// Settles this rank's fills first (a gated fill's exact simulation runs in
+// the sync); the result stays on the device for hpgq_cgr_read.
+int hpgq_cgr_allreduce(hpgq_cgr_t *c) {
+  if (!c) return HPGQ_E_INVALID;
+  if (!c->comm) return HPGQ_E_STATE;
+  int rc = hpgq_cgr_sync(c);
+  if (rc) return rc;
+  const size_t cells = (size_t)c->dim * c->dim;
+  HPGQ_HIP_TRY(hipMemcpyAsync(c->d_pack, c->d_ts, cells * 4, hipMemcpyDeviceToDevice, c->stream));
+  HPGQ_HIP_TRY(hipMemcpyAsync(c->d_pack + cells, c->d_tq, cells * 4, hipMemcpyDeviceToDevice, c->stream));
+  // the u64 device word count's low half (little endian) is the u32 fq_word_count
+  HPGQ_HIP_TRY(hipMemcpyAsync(c->d_pack + 2 * cells, c->d_words, 4, hipMemcpyDeviceToDevice, c->stream));
+  if (ncclAllReduce(c->d_pack, c->d_global, 2 * cells + 1, ncclUint32, ncclSum, c->comm, c->stream) != ncclSuccess)
+    return HPGQ_E_RCCL;
+  HPGQ_HIP_TRY(hipStreamSynchronize(c->stream));
+  c->reduced = true;
+  return HPGQ_OK;
+}
+
+uint32_t *hpgq_cgr_global_device(hpgq_cgr_t *c) { return c ? c->d_global : nullptr; }
 
 }  // extern "C"

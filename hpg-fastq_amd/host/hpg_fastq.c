@@ -64,6 +64,14 @@ int main(int argc, char **argv) {
     if (!f || fwrite(r.kmers, sizeof(uint64_t), kn, f) != kn) rc = 1;
     if (f) fclose(f);
   }
+  if (o->cg_out && r.cg_seq) {   /* [table_seq | table_q | word count] u32 */
+    const size_t cells = (size_t)1 << (2 * o->k_cg);
+    FILE *f = fopen(o->cg_out, "wb");
+    if (!f || fwrite(r.cg_seq, 4, cells, f) != cells || fwrite(r.cg_q, 4, cells, f) != cells ||
+        fwrite(&r.cg_words, 4, 1, f) != 1)
+      rc = 1;
+    if (f) fclose(f);
+  }
   if (cmd == CMD_STATS && cli_report(o, &p, counters, &r)) rc = 1;
 
   if (!o->quiet) {
@@ -91,9 +99,9 @@ int main(int argc, char **argv) {
         printf("\tNum. failed reads : %lu (%s/failed.fq)\n", (unsigned long)r.num_failed, o->out_dirname);
       }
     }
-    printf("\nThroughput: %lu reads, %.3f GB of FastQ in %.3f s = %.2f Mreads/s\n",
+    printf("\nThroughput: %lu reads, %.3f GB of FastQ in %.3f s = %.2f Mreads/s (%d GPU worker%s)\n",
            (unsigned long)r.num_reads, r.fastq_bytes / 1e9, r.seconds,
-           r.seconds > 0 ? r.num_reads / r.seconds / 1e6 : 0.0);
+           r.seconds > 0 ? r.num_reads / r.seconds / 1e6 : 0.0, r.num_gpus, r.num_gpus == 1 ? "" : "s");
     printf("=================================================\n");
   }
   free(counters);

@@ -42,12 +42,15 @@ typedef struct {
   int max_N, max_out_of_quality;
   int filter_on;
   /* MI355X build options */
-  int device;
+  int device;               /* first GPU */
+  int num_gpus;             /* GPU workers (0: every visible device) */
+  int64_t cg_batch_size;    /* --cg: FASTQ text bytes per chaos-game call */
   int lmax;                 /* per-position arrays (longest read kept) */
   int chunk_mb;             /* FASTQ text per parse unit */
   int print_params;         /* print hpgq_params_t and exit (no device) */
   char *counters_out;       /* raw u64 counter dump (tests) */
   char *kmers_out;          /* raw u64 k-mer table dump (tests) */
+  char *cg_out;             /* raw u32 chaos-game tables dump (tests) */
   int quiet;
 } cli_options_t;
 
@@ -70,6 +73,7 @@ typedef struct {
   uint32_t *cg_seq, *cg_q;  /* --cg: table_seq / table_q [dim*dim] (malloc'd) */
   uint32_t cg_words;        /* fq_word_count */
   int cg_exact_calls;       /* chaos-game calls the exact simulation redid */
+  int num_gpus;             /* GPU workers that ran */
 } cli_result_t;
 
 int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, cli_result_t *res);

@@ -77,6 +77,7 @@ static void usage(const cli_options_t *o) {
     printf("  --cg, --chaos-game              Genomic signature (chaos game) tables and images\n");
     printf("  --k=<int>                       Chaos game word size (1-12, default 7)\n");
     printf("  --gs-filename=<file>            Reference genomic signature: difference table and image\n");
+    printf("  --cg-batch-size=<int>           FastQ text bytes per chaos-game call (default 64000000)\n");
   }
   printf("  --read-length-range=<string>    Read length range, eg. 80,110\n");
   printf("  --read-quality-range=<string>   Read quality range, eg. 20,40\n");
@@ -89,7 +90,8 @@ static void usage(const cli_options_t *o) {
   printf("  --max-N=<int>                   Maximum number of Ns in the sequences\n");
   printf("  --max-out-of-quality=<int>      Maximum number of nucleotides out of the read quality range\n");
   printf("\n  MI355X build:\n");
-  printf("  --gpu=<int>                     HIP device (default 0)\n");
+  printf("  --gpu=<int>                     First HIP device (default 0)\n");
+  printf("  --gpus=<int>                    GPU workers, chunks round-robin (default: every visible device)\n");
   printf("  --lmax=<int>                    Longest read kept per position (default %d)\n",
          HPGQ_LMAX_LIMIT);
   printf("  --chunk-mb=<int>                FastQ text per GPU parse unit (default 256)\n");
@@ -97,6 +99,8 @@ static void usage(const cli_options_t *o) {
   printf("  --counters-out=<file>           Write the raw u64 counter set\n");
   if (o->command == CMD_STATS)
     printf("  --kmers-out=<file>              Write the raw u64 k-mer table [1024][lmax-4]\n");
+  if (o->command == CMD_STATS)
+    printf("  --cg-out=<file>                 Write the raw u32 chaos-game tables + word count\n");
   printf("  --quiet                         No parameter / result display\n");
   exit(-1);
 }
@@ -109,7 +113,7 @@ static int exists(const char *path) {
 enum {
   O_THREADS = 1000, O_BATCH, O_QENC, O_KMERS, O_LRANGE, O_QRANGE, O_LLEN, O_LQRANGE, O_RLEN,
   O_RQRANGE, O_MAXN, O_MAXOOQ, O_GPU, O_LMAX, O_CHUNK, O_PRINT, O_COUNTERS, O_QUIET,
-  O_KMERSOUT, O_CG, O_KCG, O_GS
+  O_KMERSOUT, O_CG, O_KCG, O_GS, O_GPUS, O_CGBATCH, O_CGOUT
 };
 
 cli_options_t *cli_parse(int command, const char *exec_name, int argc, char **argv) {
@@ -128,6 +132,7 @@ cli_options_t *cli_parse(int command, const char *exec_name, int argc, char **ar
   o->lmax = HPGQ_LMAX_LIMIT;
   o->chunk_mb = 256;
   o->k_cg = 7;   /* DEFAULT_K_IN_CHAOS_GAME */
+  o->cg_batch_size = 64000000;   /* DEFAULT_BATCH_SIZE_MB * 1000000, old/main_hpg_fastq_old.c:116 */
   static const struct option longopts[] = {
       {"help", no_argument, 0, 'h'},
       {"fastq-file", required_argument, 0, 'f'},
@@ -149,6 +154,9 @@ cli_options_t *cli_parse(int command, const char *exec_name, int argc, char **ar
       {"max-N", required_argument, 0, O_MAXN},
       {"max-out-of-quality", required_argument, 0, O_MAXOOQ},
       {"gpu", required_argument, 0, O_GPU},
+      {"gpus", required_argument, 0, O_GPUS},
+      {"cg-batch-size", required_argument, 0, O_CGBATCH},
+      {"cg-out", required_argument, 0, O_CGOUT},
       {"lmax", required_argument, 0, O_LMAX},
       {"chunk-mb", required_argument, 0, O_CHUNK},
       {"print-params", no_argument, 0, O_PRINT},
@@ -186,11 +194,14 @@ cli_options_t *cli_parse(int command, const char *exec_name, int argc, char **ar
       case O_MAXN: o->max_N = atoi(optarg); break;
       case O_MAXOOQ: o->max_out_of_quality = atoi(optarg); break;
       case O_GPU: o->device = atoi(optarg); break;
+      case O_GPUS: o->num_gpus = atoi(optarg); break;
+      case O_CGBATCH: o->cg_batch_size = atoll(optarg); break;
       case O_LMAX: o->lmax = atoi(optarg); break;
       case O_CHUNK: o->chunk_mb = atoi(optarg); break;
       case O_PRINT: o->print_params = 1; break;
       case O_COUNTERS: o->counters_out = strdup(optarg); break;
       case O_KMERSOUT: o->kmers_out = strdup(optarg); break;
+      case O_CGOUT: o->cg_out = strdup(optarg); break;
       case O_QUIET: o->quiet = 1; break;
       default: usage(o);
     }
@@ -236,6 +247,13 @@ cli_options_t *cli_parse(int command, const char *exec_name, int argc, char **ar
     exit(-1);
   }
   if (o->num_threads < 1) o->num_threads = 1;
+  if (o->num_gpus < 0) o->num_gpus = 0;
+  /* the old tool's floor (old/main_hpg_fastq_old.c:474-477 takes 64 MB below 64) */
+  if (o->cg_batch_size < 64) o->cg_batch_size = 64000000;
+  if (o->cg_batch_size > ((int64_t)1536 << 20)) {
+    printf("\nError: --cg-batch-size must be at most %lld\n", (long long)1536 << 20);
+    exit(-1);
+  }
   if (o->cg_on && (o->k_cg < 1 || o->k_cg > 12)) {
     printf("\nError: --k must be in 1..12\n");
     exit(-1);
@@ -301,7 +319,8 @@ void cli_display(const cli_options_t *o) {
     printf("\tGenomic signature   : %s\n", o->gs_filename ? o->gs_filename : "(none)");
   }
   printf("\nArchitecture options\n");
-  printf("\tGPU                 : %d (gfx950)\n", o->device);
+  printf("\tGPU                 : %d (gfx950), workers: %s\n", o->device,
+         o->num_gpus > 0 ? "--gpus" : "every visible device");
   printf("\tReader threads      : %d\n", o->num_threads);
   printf("\tChunk size          : %d MB of FastQ text\n", o->chunk_mb);
   printf("=================================================\n");
@@ -370,6 +389,7 @@ void cli_free(cli_options_t *o) {
   free(o->right_quality_range);
   free(o->counters_out);
   free(o->kmers_out);
+  free(o->cg_out);
   free(o->gs_filename);
   free(o);
 }

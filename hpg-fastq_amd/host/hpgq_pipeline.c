@@ -9,9 +9,20 @@
  *              --num-threads parallel pread()s, cut at the last whole record
  *              (hpgq_fastq_complete_prefix); the partial record is carried
  *              into the next chunk.
- *   GPU        hpgq_parse_host (H2D + parse into a device batch) and
- *              hpgq_run_device (filter / edit / stats fused) on one stream;
- *              for filter / edit the mask, trims and record offsets come back.
+ *   GPU        one worker thread per GPU (--gpus; default every visible
+ *              device), chunk k on worker k mod G: hpgq_parse_host (H2D +
+ *              parse into a device batch) and hpgq_run_device (filter / edit /
+ *              stats fused) on the worker's ctx stream; for filter / edit the
+ *              mask, trims and record offsets come back.  At the end the
+ *              workers' device counters (k-mer tables, CGR tables) are summed
+ *              on the host: the read-sharded merge of DESIGN.md §6.
+ *   --cg       one chaos_game_fill_tables call per batch of --cg-batch-size
+ *              bytes of FASTQ text (default 64,000,000, the old tool's
+ *              batch_size, old/main_hpg_fastq_old.c:116): batch j holds the
+ *              records ending in ((j-1)B, jB], so the calls (whose double
+ *              state starts afresh, old/chaos_game.c:180-181) do not depend on
+ *              --chunk-mb or --gpus; the reader then cuts every chunk at a
+ *              batch end.
  *   writer     (filter / edit) passed.fq / failed.fq / edit.fq in input
  *              order: filter copies whole input records; edit writes the
  *              header and '+' lines as read and the trimmed sequence /
@@ -31,7 +42,8 @@
 
 #include "hpgq_cli.h"
 
-#define NSLOTS 3
+#define MAX_WORKERS 16
+#define MAX_SLOTS (2 * MAX_WORKERS + 2)
 #define MAX_CARRY (64u << 20)   /* longest record the reader can carry over */
 
 typedef struct {
@@ -39,6 +51,7 @@ typedef struct {
   size_t cap, len, use;
   int eof;
   int state;          /* 0 free, 1 filled (reader -> GPU), 2 processed (GPU -> writer) */
+  int64_t chunk;      /* the chunk it holds */
   /* GPU results for the writer */
   int64_t nreads;
   uint8_t *mask;
@@ -51,7 +64,8 @@ typedef struct {
   const cli_options_t *o;
   int fd;
   off_t size, pos;
-  slot_t slot[NSLOTS];
+  int nslots, nworkers;
+  slot_t slot[MAX_SLOTS];
   char *carry;
   size_t carry_len;
   pthread_mutex_t mu;
@@ -60,6 +74,7 @@ typedef struct {
   int64_t chunks;
   FILE *out_pass, *out_fail;
   uint64_t written_pass, written_fail;
+  int64_t cg_batch;   /* --cg: bytes of FASTQ text per chaos-game call (0: off) */
 } pipe_t;
 
 static double now_s(void) {
@@ -121,10 +136,18 @@ static ssize_t read_parallel(pipe_t *P, char *dst, size_t n) {
   return total;
 }
 
+static void reader_fail(pipe_t *P, int code) {
+  pthread_mutex_lock(&P->mu);
+  P->error = code;
+  pthread_cond_broadcast(&P->cv);
+  pthread_mutex_unlock(&P->mu);
+}
+
 static void *reader_main(void *arg) {
   pipe_t *P = arg;
+  int64_t target = 0;   /* --cg: file offset of the current chaos-game batch end */
   for (int64_t k = 0;; ++k) {
-    slot_t *s = &P->slot[k % NSLOTS];
+    slot_t *s = &P->slot[k % P->nslots];
     pthread_mutex_lock(&P->mu);
     while (s->state != 0 && !P->error) pthread_cond_wait(&P->cv, &P->mu);
     const int err = P->error;
@@ -132,20 +155,38 @@ static void *reader_main(void *arg) {
     if (err) break;
     memcpy(s->buf, P->carry, P->carry_len);
     s->len = P->carry_len;
-    const size_t room = s->cap - 1 - s->len;   /* 1 byte for a final newline */
-    const ssize_t got = read_parallel(P, s->buf + s->len, room);
-    if (got < 0) {
-      pthread_mutex_lock(&P->mu);
-      P->error = -1;
-      pthread_cond_broadcast(&P->cv);
-      pthread_mutex_unlock(&P->mu);
-      break;
+    const off_t g0 = P->pos - (off_t)P->carry_len;   /* file offset of buf[0] */
+    int64_t use = 0;
+    if (P->cg_batch > 0) {
+      /* the next batch end(s): the last record ending at or before target */
+      for (;;) {
+        target += P->cg_batch;
+        const size_t want = (size_t)(target - g0) < s->cap - 1 ? (size_t)(target - g0) : s->cap - 1;
+        if (want > s->len) {
+          const ssize_t got = read_parallel(P, s->buf + s->len, want - s->len);
+          if (got < 0) break;
+          P->pos += got;
+          s->len += (size_t)got;
+        }
+        s->eof = P->pos >= P->size;
+        if (s->eof) break;
+        use = hpgq_fastq_complete_prefix(s->buf, (int64_t)s->len, 0);
+        if (use > 0 || s->len >= s->cap - 1) break;
+        /* no record ends in this batch (one longer than the batch): the next */
+      }
+    } else {
+      const size_t room = s->cap - 1 - s->len;   /* 1 byte for a final newline */
+      const ssize_t got = read_parallel(P, s->buf + s->len, room);
+      if (got < 0) {
+        reader_fail(P, -1);
+        break;
+      }
+      P->pos += got;
+      s->len += (size_t)got;
+      s->eof = P->pos >= P->size;
     }
-    P->pos += got;
-    s->len += (size_t)got;
-    s->eof = P->pos >= P->size;
     if (s->eof && s->len > 0 && s->buf[s->len - 1] != '\n') s->buf[s->len++] = '\n';
-    const int64_t use = hpgq_fastq_complete_prefix(s->buf, (int64_t)s->len, s->eof);
+    if (s->eof || P->cg_batch <= 0) use = hpgq_fastq_complete_prefix(s->buf, (int64_t)s->len, s->eof);
     if (use <= 0 && !s->eof) {
       fprintf(stderr, "hpg-fastq: a record longer than --chunk-mb, or not FASTQ\n");
       pthread_mutex_lock(&P->mu);
@@ -165,6 +206,7 @@ static void *reader_main(void *arg) {
     }
     memcpy(P->carry, s->buf + s->use, P->carry_len);
     pthread_mutex_lock(&P->mu);
+    s->chunk = k;
     s->state = 1;
     P->chunks = k + 1;
     if (s->eof) P->reader_done = 1;
@@ -221,11 +263,11 @@ static int write_slot(pipe_t *P, slot_t *s) {
 static void *writer_main(void *arg) {
   pipe_t *P = arg;
   for (int64_t k = 0;; ++k) {
-    slot_t *s = &P->slot[k % NSLOTS];
+    slot_t *s = &P->slot[k % P->nslots];
     pthread_mutex_lock(&P->mu);
-    while (s->state != 2 && !P->error && !(P->reader_done && k >= P->chunks))
+    while (!(s->state == 2 && s->chunk == k) && !P->error && !(P->reader_done && k >= P->chunks))
       pthread_cond_wait(&P->cv, &P->mu);
-    const int stop = P->error || (s->state != 2);
+    const int stop = P->error || !(s->state == 2 && s->chunk == k);
     pthread_mutex_unlock(&P->mu);
     if (stop) break;
     const int rc = write_slot(P, s);
@@ -265,6 +307,119 @@ static int ensure_results(slot_t *s, int64_t n) {
              : -1;
 }
 
+/* one GPU worker: its own ctx, parser, k-mer and CGR accumulators on one device */
+typedef struct {
+  pipe_t *P;
+  const hpgq_params_t *p;
+  int w, device;
+  hpgq_ctx_t *ctx;
+  hpgq_parser_t *ps;
+  hpgq_kmers_t *km;
+  hpgq_cgr_t *cg;
+  uint8_t *d_mask;
+  uint32_t *d_trim;
+  size_t dcap;
+  int rc;
+  pthread_t th;
+  uint64_t num_reads;
+  int cg_exact_calls;
+  double fastq_bytes;
+} worker_t;
+
+static int worker_open(worker_t *W) {
+  const cli_options_t *o = W->P->o;
+  int rc = hpgq_open(&W->ctx, W->device, W->p);
+  if (rc == 0) rc = hpgq_parser_open(&W->ps, W->device, hpgq_stream(W->ctx));
+  /* --kmers counts the reads the stats merge (passed ones when filtering,
+   * src/stats_fastq.c:268-272,384-410) on the engine's stream, after it */
+  if (rc == 0 && o->kmers_on) rc = hpgq_kmers_open(&W->km, W->device, W->p->lmax, hpgq_stream(W->ctx));
+  /* --cg: chaos_game_fill_tables per batch (= chunk), the base quality from
+   * --quality-encoding; with a filter only the passed reads (ONLY_VALID_READS
+   * with the mask as read_status, old/chaos_game.c:188) */
+  if (rc == 0 && o->cg_on) rc = hpgq_cgr_open(&W->cg, W->device, o->k_cg, W->p->phred);
+  return rc;
+}
+
+static void worker_close(worker_t *W) {
+  hpgq_device_free(W->d_mask);
+  hpgq_device_free(W->d_trim);
+  hpgq_parser_close(W->ps);
+  hpgq_kmers_close(W->km);
+  hpgq_cgr_close(W->cg);
+  hpgq_close(W->ctx);
+}
+
+/* one chunk on the worker's GPU (parse, engine, k-mers, CGR; results for the writer) */
+static int worker_chunk(worker_t *W, slot_t *s) {
+  const cli_options_t *o = W->P->o;
+  const int writes = o->command != CMD_STATS;
+  const int edit = o->command == CMD_EDIT;
+  const int need_mask = writes || ((W->km || W->cg) && o->filter_on);
+  hpgq_batch_t b;
+  int rc = hpgq_parse_host(W->ps, s->buf, (int64_t)s->use, &b);
+  if (rc || b.num_reads == 0) {
+    s->nreads = 0;
+    return rc;
+  }
+  if (need_mask && (size_t)b.num_reads > W->dcap) {
+    hpgq_device_free(W->d_mask);
+    hpgq_device_free(W->d_trim);
+    W->d_mask = NULL;
+    W->d_trim = NULL;
+    W->dcap = (size_t)b.num_reads + (size_t)b.num_reads / 4 + 1024;
+    rc = hpgq_device_alloc(W->device, (void **)&W->d_mask, W->dcap);
+    if (rc == 0) rc = hpgq_device_alloc(W->device, (void **)&W->d_trim, W->dcap * 4);
+  }
+  if (rc == 0) rc = hpgq_run_device(W->ctx, &b, NULL, need_mask ? W->d_mask : NULL, edit ? W->d_trim : NULL);
+  if (rc == 0 && W->km) rc = hpgq_kmers_count_device(W->km, &b, o->filter_on ? W->d_mask : NULL);
+  if (rc == 0 && writes) {
+    s->nreads = b.num_reads;
+    if (ensure_results(s, b.num_reads)) rc = HPGQ_E_NOMEM;
+    if (rc == 0) rc = hpgq_copy_to_host(W->ctx, s->mask, W->d_mask, (size_t)b.num_reads);
+    if (rc == 0 && edit) {
+      rc = hpgq_copy_to_host(W->ctx, s->trim, W->d_trim, (size_t)b.num_reads * 4);
+      if (rc == 0) rc = hpgq_copy_to_host(W->ctx, s->idx, b.data_indices, ((size_t)b.num_reads + 1) * 4);
+    }
+    if (rc == 0) rc = hpgq_parse_records(W->ps, s->rec_start, s->seq_start, s->plus_start, s->qual_start);
+  }
+  if (rc == 0) rc = hpgq_sync(W->ctx);
+  if (rc == 0 && W->cg) {   /* after the parse and the mask; settled before the next parse reuses b */
+    rc = hpgq_cgr_fill_device(W->cg, &b, o->filter_on ? W->d_mask : NULL,
+                              o->filter_on ? HPGQ_CGR_ONLY_VALID_READS : HPGQ_CGR_ALL_READS);
+    if (rc == 0) rc = hpgq_cgr_sync(W->cg);
+    if (rc == 0) W->cg_exact_calls += hpgq_cgr_last_exact(W->cg);
+  }
+  W->num_reads += (uint64_t)b.num_reads;
+  return rc;
+}
+
+static void *worker_main(void *arg) {
+  worker_t *W = arg;
+  pipe_t *P = W->P;
+  const int writes = P->o->command != CMD_STATS;
+  for (int64_t k = W->w;; k += P->nworkers) {
+    slot_t *s = &P->slot[k % P->nslots];
+    pthread_mutex_lock(&P->mu);
+    while (!(s->state == 1 && s->chunk == k) && !P->error && !(P->reader_done && k >= P->chunks))
+      pthread_cond_wait(&P->cv, &P->mu);
+    const int stop = P->error || !(s->state == 1 && s->chunk == k);
+    pthread_mutex_unlock(&P->mu);
+    if (stop) break;
+    const int rc = worker_chunk(W, s);
+    W->fastq_bytes += (double)s->use;
+    pthread_mutex_lock(&P->mu);
+    if (rc && !P->error) P->error = rc;
+    s->state = writes && rc == 0 ? 2 : 0;
+    pthread_cond_broadcast(&P->cv);
+    pthread_mutex_unlock(&P->mu);
+    if (rc) {
+      W->rc = rc;
+      break;
+    }
+  }
+  return NULL;
+}
+
 int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, cli_result_t *res) {
   pipe_t P;
   memset(&P, 0, sizeof(P));
@@ -278,31 +433,37 @@ int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, 
   pthread_mutex_init(&P.mu, NULL);
   pthread_cond_init(&P.cv, NULL);
 
-  hpgq_ctx_t *ctx = NULL;
-  hpgq_parser_t *ps = NULL;
-  hpgq_kmers_t *km = NULL;
-  hpgq_cgr_t *cg = NULL;
-  int rc = hpgq_open(&ctx, o->device, p);
-  if (rc == 0) rc = hpgq_parser_open(&ps, o->device, hpgq_stream(ctx));
-  /* --kmers counts the reads the stats merge (passed ones when filtering,
-   * src/stats_fastq.c:268-272,384-410) on the engine's stream, after it */
-  if (rc == 0 && o->kmers_on) rc = hpgq_kmers_open(&km, o->device, p->lmax, hpgq_stream(ctx));
-  /* --cg: chaos_game_fill_tables per parsed chunk (one call = one chunk), the
-   * base quality from --quality-encoding; with a filter only the passed reads
-   * (ONLY_VALID_READS with the mask as read_status, old/chaos_game.c:188) */
-  if (rc == 0 && o->cg_on) rc = hpgq_cgr_open(&cg, o->device, o->k_cg, p->phred);
-  const size_t chunk = (size_t)o->chunk_mb << 20;
-  for (int i = 0; i < NSLOTS && rc == 0; ++i) {
+  /* GPU workers: --gpus (0: every visible device), worker w on device (gpu + w) mod ndev */
+  const int ndev = hpgq_device_count();
+  if (ndev <= 0) {
+    close(P.fd);
+    return HPGQ_E_NO_DEVICE;
+  }
+  int G = o->num_gpus > 0 ? o->num_gpus : ndev;
+  if (G > MAX_WORKERS) G = MAX_WORKERS;
+  P.nworkers = G;
+  P.nslots = 2 * G + 1;   /* reader + G workers + writer, with room to run ahead */
+  P.cg_batch = o->cg_on ? o->cg_batch_size : 0;
+  worker_t W[MAX_WORKERS];
+  memset(W, 0, sizeof(W));
+  int rc = 0;
+  for (int w = 0; w < G && rc == 0; ++w) {
+    W[w].P = &P;
+    W[w].p = p;
+    W[w].w = w;
+    W[w].device = (o->device + w) % ndev;
+    rc = worker_open(&W[w]);
+  }
+  /* a chunk holds --chunk-mb of text (with --cg: one chaos-game batch) */
+  size_t chunk = (size_t)o->chunk_mb << 20;
+  if (P.cg_batch > 0 && (size_t)P.cg_batch > chunk) chunk = (size_t)P.cg_batch;
+  for (int i = 0; i < P.nslots && rc == 0; ++i) {
     P.slot[i].cap = chunk + MAX_CARRY;
     rc = hpgq_host_alloc((void **)&P.slot[i].buf, P.slot[i].cap);
   }
   P.carry = malloc(MAX_CARRY + 16);
-  uint8_t *d_mask = NULL;
-  uint32_t *d_trim = NULL;
-  size_t dcap = 0;
   const int writes = o->command != CMD_STATS;
   const int edit = o->command == CMD_EDIT;
-  const int need_mask = writes || ((km || cg) && o->filter_on);
   if (rc == 0 && writes) {
     char path[4096];
     snprintf(path, sizeof(path), "%s/%s.fq", o->out_dirname, edit ? "edit" : "passed");
@@ -321,72 +482,64 @@ int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, 
   pthread_t reader, writer;
   pthread_create(&reader, NULL, reader_main, &P);
   if (writes) pthread_create(&writer, NULL, writer_main, &P);
-  for (int64_t k = 0;; ++k) {
-    slot_t *s = &P.slot[k % NSLOTS];
-    pthread_mutex_lock(&P.mu);
-    while (s->state != 1 && !P.error && !(P.reader_done && k >= P.chunks))
-      pthread_cond_wait(&P.cv, &P.mu);
-    const int stop = P.error || s->state != 1;
-    pthread_mutex_unlock(&P.mu);
-    if (stop) break;
-    hpgq_batch_t b;
-    rc = hpgq_parse_host(ps, s->buf, (int64_t)s->use, &b);
-    if (rc == 0 && b.num_reads > 0) {
-      if (need_mask && (size_t)b.num_reads > dcap) {
-        hpgq_device_free(d_mask);
-        hpgq_device_free(d_trim);
-        dcap = (size_t)b.num_reads + (size_t)b.num_reads / 4 + 1024;
-        rc = hpgq_device_alloc(o->device, (void **)&d_mask, dcap);
-        if (rc == 0) rc = hpgq_device_alloc(o->device, (void **)&d_trim, dcap * 4);
-      }
-      if (rc == 0) rc = hpgq_run_device(ctx, &b, NULL, need_mask ? d_mask : NULL, edit ? d_trim : NULL);
-      if (rc == 0 && km) rc = hpgq_kmers_count_device(km, &b, o->filter_on ? d_mask : NULL);
-      if (rc == 0 && writes) {
-        s->nreads = b.num_reads;
-        if (ensure_results(s, b.num_reads)) rc = HPGQ_E_NOMEM;
-        if (rc == 0) rc = hpgq_copy_to_host(ctx, s->mask, d_mask, (size_t)b.num_reads);
-        if (rc == 0 && edit) {
-          rc = hpgq_copy_to_host(ctx, s->trim, d_trim, (size_t)b.num_reads * 4);
-          if (rc == 0) rc = hpgq_copy_to_host(ctx, s->idx, b.data_indices, ((size_t)b.num_reads + 1) * 4);
-        }
-        if (rc == 0) rc = hpgq_parse_records(ps, s->rec_start, s->seq_start, s->plus_start, s->qual_start);
-      }
-      if (rc == 0) rc = hpgq_sync(ctx);
-      if (rc == 0 && cg) {   /* after the parse and the mask; settled before the next parse reuses b */
-        rc = hpgq_cgr_fill_device(cg, &b, o->filter_on ? d_mask : NULL,
-                                  o->filter_on ? HPGQ_CGR_ONLY_VALID_READS : HPGQ_CGR_ALL_READS);
-        if (rc == 0) rc = hpgq_cgr_sync(cg);
-        if (rc == 0) res->cg_exact_calls += hpgq_cgr_last_exact(cg);
-      }
-      res->num_reads += (uint64_t)b.num_reads;
-    } else if (rc == 0) {
-      s->nreads = 0;
-    }
-    res->fastq_bytes += (double)s->use;
-    pthread_mutex_lock(&P.mu);
-    if (rc) P.error = rc;
-    s->state = writes && rc == 0 ? 2 : 0;
-    pthread_cond_broadcast(&P.cv);
-    pthread_mutex_unlock(&P.mu);
-    if (rc) break;
-  }
+  for (int w = 0; w < G; ++w) pthread_create(&W[w].th, NULL, worker_main, &W[w]);
+  for (int w = 0; w < G; ++w) pthread_join(W[w].th, NULL);
+  /* (a worker that stopped on an error left P.error set: reader and writer end) */
+  pthread_mutex_lock(&P.mu);
+  pthread_cond_broadcast(&P.cv);
+  pthread_mutex_unlock(&P.mu);
   pthread_join(reader, NULL);
   if (writes) pthread_join(writer, NULL);
+  for (int w = 0; w < G && rc == 0; ++w) rc = W[w].rc;
   if (rc == 0 && P.error) rc = P.error < 0 && P.error != HPGQ_E_FORMAT ? HPGQ_E_INVALID : P.error;
-  if (rc == 0) rc = hpgq_sync(ctx);   /* surfaces HPGQ_E_READ_TOO_LONG */
-  if (rc == 0) rc = hpgq_read_counters(ctx, counters, hpgq_counters_size(ctx));
-  if (rc == 0 && km) {
-    res->kmers_npos = p->lmax > HPGQ_KMER_K - 1 ? p->lmax - (HPGQ_KMER_K - 1) : 0;
-    res->kmers = calloc(hpgq_kmers_size(km) + 1, sizeof(uint64_t));
-    rc = res->kmers ? hpgq_kmers_read(km, res->kmers, hpgq_kmers_size(km)) : HPGQ_E_NOMEM;
+
+  /* the read-sharded merge: device counters, k-mer and CGR tables summed over
+   * the workers (u64; CGR u32, which wraps like the reference's tables) */
+  const size_t clen = hpgq_counters_size(W[0].ctx);
+  uint64_t *part = rc == 0 ? calloc(clen, sizeof(uint64_t)) : NULL;
+  if (rc == 0 && !part) rc = HPGQ_E_NOMEM;
+  if (rc == 0) memset(counters, 0, clen * sizeof(uint64_t));
+  for (int w = 0; w < G && rc == 0; ++w) {
+    rc = hpgq_sync(W[w].ctx);   /* surfaces HPGQ_E_READ_TOO_LONG */
+    if (rc == 0) rc = hpgq_read_counters(W[w].ctx, part, clen);
+    for (size_t i = 0; rc == 0 && i < clen; ++i) counters[i] += part[i];
+    res->num_reads += W[w].num_reads;
+    res->fastq_bytes += W[w].fastq_bytes;
+    res->cg_exact_calls += W[w].cg_exact_calls;
   }
-  if (rc == 0 && cg) {
+  free(part);
+  if (rc == 0 && o->kmers_on) {
+    const size_t kn = hpgq_kmers_size(W[0].km);
+    res->kmers_npos = p->lmax > HPGQ_KMER_K - 1 ? p->lmax - (HPGQ_KMER_K - 1) : 0;
+    res->kmers = calloc(kn + 1, sizeof(uint64_t));
+    uint64_t *kp = calloc(kn + 1, sizeof(uint64_t));
+    if (!res->kmers || !kp) rc = HPGQ_E_NOMEM;
+    for (int w = 0; w < G && rc == 0; ++w) {
+      rc = hpgq_kmers_read(W[w].km, kp, kn);
+      for (size_t i = 0; rc == 0 && i < kn; ++i) res->kmers[i] += kp[i];
+    }
+    free(kp);
+  }
+  if (rc == 0 && o->cg_on) {
     const size_t cells = (size_t)1 << (2 * o->k_cg);
     res->cg_seq = calloc(cells, sizeof(uint32_t));
     res->cg_q = calloc(cells, sizeof(uint32_t));
-    rc = res->cg_seq && res->cg_q ? hpgq_cgr_read(cg, res->cg_seq, res->cg_q, &res->cg_words) : HPGQ_E_NOMEM;
+    uint32_t *ts = calloc(cells, sizeof(uint32_t)), *tq = calloc(cells, sizeof(uint32_t));
+    if (!res->cg_seq || !res->cg_q || !ts || !tq) rc = HPGQ_E_NOMEM;
+    for (int w = 0; w < G && rc == 0; ++w) {
+      uint32_t words = 0;
+      rc = hpgq_cgr_read(W[w].cg, ts, tq, &words);
+      for (size_t i = 0; rc == 0 && i < cells; ++i) {
+        res->cg_seq[i] += ts[i];
+        res->cg_q[i] += tq[i];
+      }
+      res->cg_words += words;
+    }
+    free(ts);
+    free(tq);
   }
   res->seconds = now_s() - t0;
+  res->num_gpus = G;
   if (rc == 0) {
     res->num_passed = counters[HPGQ_S_NUM_PASSED];
     res->num_failed = counters[HPGQ_S_NUM_FAILED];
@@ -396,9 +549,7 @@ int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, 
 done:
   if (P.out_pass) fclose(P.out_pass);
   if (P.out_fail) fclose(P.out_fail);
-  hpgq_device_free(d_mask);
-  hpgq_device_free(d_trim);
-  for (int i = 0; i < NSLOTS; ++i) {
+  for (int i = 0; i < P.nslots; ++i) {
     hpgq_host_free(P.slot[i].buf);
     free(P.slot[i].mask);
     free(P.slot[i].trim);
@@ -409,10 +560,7 @@ done:
     free(P.slot[i].idx);
   }
   free(P.carry);
-  hpgq_parser_close(ps);
-  hpgq_kmers_close(km);
-  hpgq_cgr_close(cg);
-  hpgq_close(ctx);
+  for (int w = 0; w < G; ++w) worker_close(&W[w]);
   close(P.fd);
   return rc;
 }

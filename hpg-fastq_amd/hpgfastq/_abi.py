@@ -118,6 +118,9 @@ _SIGS = [
     ("hpgq_cgr_last_replays", C.c_int64, [C.c_void_p]),
     ("hpgq_cgr_set_path", C.c_int, [C.c_void_p, C.c_int]),
     ("hpgq_cgr_last_exact", C.c_int, [C.c_void_p]),
+    ("hpgq_cgr_comm_init", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_char_p]),
+    ("hpgq_cgr_allreduce", C.c_int, [C.c_void_p]),
+    ("hpgq_cgr_global_device", C.c_void_p, [C.c_void_p]),
     ("hpgq_cgr_load_gs", C.c_int, [C.c_char_p, C.c_int, C.c_void_p, C.c_void_p]),
     ("hpgq_cgr_write_gs", C.c_int, [C.c_char_p, C.c_int, C.c_void_p, C.c_uint32]),
     ("hpgq_cgr_table_dif", C.c_int, [C.c_int, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32,

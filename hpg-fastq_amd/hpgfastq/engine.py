@@ -162,6 +162,15 @@ class ChaosGame:
     def reset(self):
         check(lib.hpgq_cgr_reset(self._h), "hpgq_cgr_reset")
 
+    def comm_init(self, nranks, rank, uid):
+        """RCCL communicator for the table sum (uid from comm_unique_id())."""
+        check(lib.hpgq_cgr_comm_init(self._h, nranks, rank, uid), "hpgq_cgr_comm_init")
+
+    def allreduce(self):
+        """u32 sum of every rank's tables and word count (hpgq_cgr_allreduce);
+        tables() returns it until the next fill or reset."""
+        check(lib.hpgq_cgr_allreduce(self._h), "hpgq_cgr_allreduce")
+
     def last_replays(self):
         return int(lib.hpgq_cgr_last_replays(self._h))
 

@@ -291,6 +291,18 @@ void *hpgq_cgr_stream(hpgq_cgr_t *cg);
 int64_t hpgq_cgr_last_replays(hpgq_cgr_t *cg);
 
 /*
+ * Multi-GPU (read-sharded fills, one process per GPU): RCCL communicator
+ * from a unique id (hpgq_comm_unique_id), then one all-reduce of
+ * [table_seq | table_q | word_count] as uint32 sums, which wrap like the
+ * reference's unsigned tables (old/chaos_game.c:253-258).  Out of place:
+ * hpgq_cgr_read returns the sums until the next fill or reset.
+ */
+int  hpgq_cgr_comm_init(hpgq_cgr_t *cg, int nranks, int rank, const char id[HPGQ_COMM_ID_BYTES]);
+int  hpgq_cgr_allreduce(hpgq_cgr_t *cg);
+/* device pointer of the all-reduced [table_seq | table_q | word_count] */
+uint32_t *hpgq_cgr_global_device(hpgq_cgr_t *cg);
+
+/*
  * Path selection.  AUTO (default): for k <= 7 and ALL_READS a coalesced
  * integer pass computes each word's cell from its own k bases, which is
  * provably the reference's (int)f cell unless some axis sees a run of

@@ -289,3 +289,28 @@ def test_cgr_stream_long_n_stretch():
     log = []
     assert_cgr(7, [reads], exact_log=log)
     assert log == [0]
+
+
+def test_cgr_allreduce_single_rank():
+    """hpgq_cgr_comm_init + hpgq_cgr_allreduce on a one-rank communicator (the
+    path bench.py takes at N > 1): the u32 sum leaves the tables equal to the
+    oracle's, tables() returns the reduced copy until the next fill, and a
+    second all-reduce does not double count."""
+    rng = np.random.default_rng(77)
+    batches = [O.synth(20000, seed=int(s), L=150, n_per_1024=8) for s in rng.integers(1, 1000, 2)]
+    cg = H.ChaosGame(7, 33)
+    cg.comm_init(1, 0, H.engine.comm_unique_id())
+    keep = []
+    for reads in batches:
+        t = _dev(reads)
+        keep.append(t)
+        cg.fill_device(H.engine.device_batch(reads.n, t["seq"].data_ptr(), t["qual"].data_ptr(),
+                                             t["idx"].data_ptr()))
+    cg.allreduce()
+    cg.allreduce()
+    ts, tq, wc = cg.tables()
+    cg.close()
+    os_, oq, ow = oracle_cgr(7, batches)
+    assert wc == ow
+    np.testing.assert_array_equal(ts.reshape(-1), os_)
+    np.testing.assert_array_equal(tq.reshape(-1), oq)

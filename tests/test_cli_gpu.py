@@ -202,3 +202,86 @@ def test_cli_chaos_game(tmp_path, filtered):
     txt = (out / "cg.fq.chaos_game.txt").read_text()
     assert f"Words read in FastQ file: {wc}" in txt
     assert f"Interval of variation of diff matrix values = [{hi}, {lo}]" in txt
+
+
+# ---- multi-GPU workers and chaos-game batches -----------------
+def _homopolymer_reads(n, seed):
+    """Reads whose long poly-A / poly-T stretches carry the CGR double state to
+    the clamp, so the tables depend on where the fill calls start."""
+    rng = np.random.default_rng(seed)
+    pairs = []
+    for i in range(n):
+        L = int(rng.integers(60, 160))
+        if i % 3 == 0:
+            s = (b"A" if rng.integers(2) else b"T") * L
+        else:
+            s = rng.choice(np.frombuffer(b"ACGTN", np.uint8), size=L,
+                           p=[0.3, 0.2, 0.2, 0.29, 0.01]).tobytes()
+        q = rng.integers(35, 75, size=L, dtype=np.uint8).tobytes()
+        pairs.append((s, q))
+    return O.Reads.from_pairs(pairs)
+
+
+def _cg_batches(text_ends, reads, B):
+    """Records ending in ((j-1)B, jB] form chaos-game call j (hpgq_pipeline.c)."""
+    groups = {}
+    for i, e in enumerate(text_ends):
+        groups.setdefault((e - 1) // B, []).append(i)
+    return [O.Reads.from_pairs([reads.read(i) for i in idx]) for _j, idx in sorted(groups.items())]
+
+
+@pytest.mark.parametrize("chunk_mb,gpus", [(1, 1), (1, 2), (4, 3), (256, 1)])
+def test_cli_cg_batches_independent_of_chunks_and_workers(tmp_path, chunk_mb, gpus):
+    """--cg makes one chaos_game_fill_tables call per --cg-batch-size bytes of
+    FASTQ text (records ending in ((j-1)B, jB]), whatever --chunk-mb and
+    --gpus are: the tables equal the oracle's calls over those batches on an
+    input whose tables depend on the call boundaries (homopolymer runs)."""
+    reads = _homopolymer_reads(12000, 5)
+    text, ends = to_fastq(reads)
+    fq = tmp_path / "hp.fq"
+    fq.write_bytes(text)
+    B = 300_000
+    cgo = tmp_path / "cg.bin"
+    run_cli(["stats", "-f", fq, "-o", tmp_path, "--cg", "--k", 6, "--cg-batch-size", B,
+             "--chunk-mb", chunk_mb, "--gpus", gpus, "--lmax", 160, "--cg-out", cgo, "--quiet"])
+    got = np.fromfile(cgo, np.uint32)
+    dim2 = 1 << 12
+    ts, tq, wc = np.zeros(dim2, np.uint32), np.zeros(dim2, np.uint32), np.zeros(1, np.uint32)
+    for b in _cg_batches(ends, reads, B):
+        O.cgr(6, b, 33, tables=(ts, tq, wc))
+    np.testing.assert_array_equal(got[:dim2], ts)
+    np.testing.assert_array_equal(got[dim2:2 * dim2], tq)
+    assert int(got[-1]) == int(wc[0])
+    # and the split matters on this input: one call over everything differs
+    ts1, _, _ = O.cgr(6, reads, 33)
+    assert not np.array_equal(ts1, ts)
+
+
+@pytest.mark.parametrize("cmd", ["stats", "filter", "edit"])
+def test_cli_workers_merge(tmp_path, cmd):
+    """--gpus 3 (three workers; on a one-GPU box they share device 0) with small
+    chunks: counters, k-mer tables and output files equal one worker's."""
+    reads = O.synth(30000, seed=27, L=150, n_per_1024=6)
+    fq = _write(tmp_path, reads)
+    outs = []
+    for g in (1, 3):
+        d = tmp_path / f"g{g}"
+        d.mkdir()
+        args = [cmd, "-f", fq, "-o", d, "--chunk-mb", 1, "--gpus", g, "--counters-out", d / "ctr.bin",
+                "--quiet", "--read-quality-range", "20,", "--read-length-range", "50,"]
+        if cmd == "stats":
+            args += ["--kmers", "--kmers-out", d / "km.bin", "--lmax", 150]
+        if cmd == "edit":
+            args += ["--left-length", 10, "--left-quality-range", "20,"]
+        run_cli(args)
+        outs.append(d)
+    a, b = outs
+    np.testing.assert_array_equal(np.fromfile(a / "ctr.bin", np.uint64), np.fromfile(b / "ctr.bin", np.uint64))
+    names = sorted(n for n in os.listdir(a) if not n.endswith(".bin") or n == "km.bin")
+    assert names == sorted(n for n in os.listdir(b) if not n.endswith(".bin") or n == "km.bin")
+    for n in names:
+        assert (a / n).read_bytes() == (b / n).read_bytes(), n
+    if cmd == "stats":
+        p = H.stats_params(lmax=150, read_quality_range="20,", read_length_range="50,")
+        _, _, want = O.run(p, reads)
+        np.testing.assert_array_equal(np.fromfile(b / "ctr.bin", np.uint64), want)
