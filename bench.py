@@ -63,6 +63,12 @@ CONFIGS = {
     "c2_250_1024": dict(metric="Mreads/s (250 bp) stats+filter, lmax 1024",
                         unit="Mreads/s", reads=50_000_000, batch=5_000_000, L=250, seed=6, lmax=1024,
                         workload="C2 flags on 250 bp reads with --lmax 1024 (hex defers to wide)"),
+    # probes: C1 flags (stats, no filter) and a filter every read passes
+    "c1_gpu": dict(metric="Mreads/s (150 bp) stats only", unit="Mreads/s", reads=100_000_000,
+                   batch=10_000_000, L=150, seed=2, workload="C1 flags (stats, no filter) on the GPU"),
+    "c2_nofail": dict(metric="Mreads/s (150 bp) stats + a filter every read passes", unit="Mreads/s",
+                      reads=100_000_000, batch=10_000_000, L=150, seed=2,
+                      workload="stats + --read-quality-range 0, --read-length-range 1, (no failures)"),
     "c2_lr": dict(metric="Mreads/s (150 bp) stats+filter with a 5' window filter",
                   unit="Mreads/s", reads=100_000_000, batch=10_000_000, L=150, seed=2,
                   workload="C2 flags + --left-length 10 --left-quality-range 20,"),
@@ -95,6 +101,10 @@ def params_for(cfg, L):
     if cfg == "c4":
         return H.edit_params(lmax=lmax, stats=True, left_length=10, left_quality_range="20,",
                              right_length=30, right_quality_range="20,")
+    if cfg == "c1_gpu":
+        return H.stats_params(lmax=lmax)
+    if cfg == "c2_nofail":
+        return H.stats_params(lmax=lmax, read_quality_range="0,", read_length_range="1,")
     extra = dict(left_length=10, left_quality_range="20,") if cfg == "c2_lr" else {}
     p = H.stats_params(lmax=lmax, read_quality_range="20,", read_length_range="50,", **extra)
     if cfg == "c3":
@@ -277,13 +287,13 @@ def main():
     else:
         eng = H.Engine(params, device=local)
         kernel_name = eng.kernel_name
+        # + 1 B mask per read (pair), + 4 B trim per read when editing
+        alg = [nb + n + (4 * n * mates if params.edit_on else 0) for (n, _m, nb) in batches]
     if world > 1:   # one RCCL communicator inside libhpgq (counters / CGR tables)
         uid = H.engine.comm_unique_id() if rank == 0 else b"\0" * 128
         obj = [uid]
         dist.broadcast_object_list(obj, src=0)
         eng.comm_init(world, rank, obj[0])
-        # + 1 B mask per read (pair), + 4 B trim per read when editing
-        alg = [nb + n + (4 * n * mates if params.edit_on else 0) for (n, _m, nb) in batches]
     ext = torch.cuda.ExternalStream(eng.stream, device=dev)
     hb = [[H.engine.device_batch(n, sq.data_ptr(), ql.data_ptr(), ix.data_ptr())
            for (sq, ql, ix) in mm] for (n, mm, _nb) in batches]
