@@ -28,8 +28,9 @@
 /* `%i` of a size_t count (src/stats_report.c:176,229,385): its low 32 bits */
 static int i32(uint64_t v) { return (int)(uint32_t)v; }
 
-/* `1.0f * a / b`, 0 when b = 0 (Q14) */
-static float fdiv(uint64_t a, uint64_t b) { return b ? 1.0f * a / b : 0.0f; }
+/* `1.0f * a / b` (0 when b = 0, Q14) for a per-position quality sum, which is
+ * signed (Q13: two's complement in the u64 counter) */
+static float fdiv_q(uint64_t a, uint64_t b) { return b ? 1.0f * (int64_t)a / b : 0.0f; }
 
 static FILE *open_out(const cli_options_t *o, const char *base, const char *suffix) {
   char path[4096];
@@ -212,7 +213,7 @@ int cli_report(const cli_options_t *o, const hpgq_params_t *p, const uint64_t *c
   fprintf(f, "\n");
   fprintf(f, "Mean quality per nucleotide position\n");
   for (int k = 0; k < maxlen; k++) {
-    qual = NORM_Q(fdiv(pq[k], cnt[k]), phred);
+    qual = NORM_Q(fdiv_q(pq[k], cnt[k]), phred);
     fprintf(f, "\tpos. %i: %i [%c]\t", k + 1, qual, qual + phred);
     if ((k + 1) % 5 == 0) fprintf(f, "\n");
   }
@@ -270,7 +271,7 @@ int cli_report(const cli_options_t *o, const hpgq_params_t *p, const uint64_t *c
   }
   if ((f = open_out(o, base, "quality.per.nt.data"))) {
     for (int k = 0; k < maxlen; k++)
-      fprintf(f, "%i\t%i\n", k, NORM_Q(fdiv(pq[k], cnt[k]), phred));
+      fprintf(f, "%i\t%i\n", k, NORM_Q(fdiv_q(pq[k], cnt[k]), phred));
     fclose(f);
   }
   if ((f = open_out(o, base, "nucleotides.data"))) {

@@ -73,7 +73,10 @@ def report_files(ctr, lmax, phred, base, opts):
     hl = c[lay["hist_len"]:lay["hist_len"] + lmax + 1]
     hq = c[lay["hist_meanq"]:lay["hist_meanq"] + pyref.MEANQ_BINS]
     hg = c[lay["hist_gc"]:lay["hist_gc"] + pyref.GC_BINS]
-    pq = c[lay["pos_qsum"]:lay["pos_qsum"] + lmax]
+    # per-position quality sums are signed (Q13): two's complement -> int before
+    # the float conversion (the reference's size_t of a negative int sum would
+    # overflow the int result of round(), which has no defined value)
+    pq = [x - (1 << 64) if x >= 1 << 63 else x for x in c[lay["pos_qsum"]:lay["pos_qsum"] + lmax]]
     pb = {b: c[lay["pos_" + b]:lay["pos_" + b] + lmax] for b in pyref.BASES}
     num_reads = c[pyref.S_NUM_STATS]
     passed, failed = c[pyref.S_NUM_PASSED], c[pyref.S_NUM_FAILED]
