@@ -220,12 +220,41 @@ void hpgq_parser_close(hpgq_parser_t *p) {
   delete p;
 }
 
+// length of the text without trailing blank lines ("...\n\n", "\r\n\r\n" at the
+// end of a file hold no record); tail: its last `nt` bytes
+static int64_t trim_blank_tail(const char *tail, int64_t nt, int64_t n, bool &more) {
+  more = false;
+  const int64_t base = n - nt;   // text offset of tail[0]
+  for (;;) {
+    if (n < 1 || tail[n - 1 - base] != '\n') break;
+    int64_t b = n - 1;   // content end of the last line
+    if (b > base && tail[b - 1 - base] == '\r') --b;
+    if (b == 0 || (b > base && tail[b - 1 - base] == '\n')) {
+      n = b;
+      if (n <= base) {   // the blank tail runs past the bytes fetched
+        more = n > 0;
+        break;
+      }
+    } else {
+      break;
+    }
+  }
+  return n;
+}
+
 int hpgq_parse_device(hpgq_parser_t *p, const char *text, int64_t n, hpgq_batch_t *out) {
   using namespace hpgq::parse;
   if (!p || !out || n < 0 || n >= ((int64_t)1 << 31)) return HPGQ_E_INVALID;
   *out = hpgq_batch_t{0, nullptr, nullptr, nullptr};
   p->last_n = 0;
   HPGQ_HIP_TRY(hipSetDevice(p->device));
+  for (bool more = n > 0; more;) {   // drop trailing blank lines
+    char tail[64];
+    const int64_t nt = n < 64 ? n : 64;
+    HPGQ_HIP_TRY(hipMemcpyAsync(tail, text + n - nt, (size_t)nt, hipMemcpyDeviceToHost, p->stream));
+    HPGQ_HIP_TRY(hipStreamSynchronize(p->stream));
+    n = trim_blank_tail(tail, nt, n, more);
+  }
   const uint8_t *t = reinterpret_cast<const uint8_t *>(text);
   // 1. newline count per tile, tile offsets, total
   const int64_t ntiles = (n + kTile - 1) / kTile;

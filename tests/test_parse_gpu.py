@@ -68,3 +68,21 @@ def test_parse_malformed(bad):
         with pytest.raises(H.HpgqError) as e:
             ps.parse(bad)
         assert e.value.code == -8
+
+
+@pytest.mark.parametrize("tail", [b"\n", b"\n\n\n", b"\r\n", b"\r\n\r\n", b"\n" * 100])
+def test_parse_trailing_blank_lines(tail):
+    """A file ending in blank lines parses to the same records; a
+    blank line between records stays a format error."""
+    reads = O.synth(3000, seed=14, L=120)
+    text, _ = to_fastq(reads, crlf=tail.startswith(b"\r"))
+    p = H.stats_params(lmax=150, read_quality_range="20,")
+    mask, ctr, _, n = parse_and_run(text + tail, p)
+    assert n == reads.n
+    m_o, _, c_o = O.run(p, reads)
+    np.testing.assert_array_equal(mask, m_o)
+    np.testing.assert_array_equal(ctr, c_o)
+    with H.Parser() as ps:
+        assert ps.parse(b"\n\n").num_reads == 0
+        with pytest.raises(H.HpgqError):
+            ps.parse(b"@r\nACGT\n+\nIIII\n\n@s\nAC\n+\nII\n")
