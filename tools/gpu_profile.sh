@@ -10,9 +10,10 @@ export TMPDIR=/tmp
 if [ -z "$SKIP_TESTS" ]; then
   timeout -k 10 600 python -m pytest tests -x -q -m gpu > gpurun_out/prof/pytest_gpu.log 2>&1 || exit 3
 fi
-[ -n "$SKIP_BENCH" ] || timeout -k 10 600 python bench.py > gpurun_out/prof/bench.json 2> gpurun_out/prof/bench.err || exit 3
-[ -n "$SKIP_BENCH" ] || timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/trace -o run --output-format csv -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/prof/bench_traced.json 2> gpurun_out/prof/trace.err || exit 3
-for spec in ${CFGS:-c2:c2:10000000:150 c3:pe:10000000:150 c4:edit:12500000:150 c5:cgr:5000000:250}; do
+# the driver's exact bench command under the kernel trace: its JSON line and
+# the trace's per-kernel averages come from the same run
+[ -n "$SKIP_BENCH" ] || timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/trace -o run --output-format csv -- python3 bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/prof/bench.json 2> gpurun_out/prof/trace.err || exit 3
+for spec in ${CFGS:-c2:c2:10000000:150 c3:pe:10000000:150 c4:edit:12500000:150 c5:cgr:5000000:250 c2_lr:lr:10000000:150 c2_250:c2:5000000:250}; do
   IFS=: read cfg mode n L <<< "$spec"
   A="python tools/prof_engine.py --mode $mode --reads $n --L $L --iters 3"
   timeout -k 10 300 python bench.py --config $cfg --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/prof/bench_$cfg.json 2> gpurun_out/prof/bench_$cfg.err || exit 3

@@ -3,8 +3,9 @@
   python tools/profile_report.py --round r01
 
 Writes
-  profiles/<round>_bench_kernel_stats.csv   rocprofv3 --stats of `bench.py --steps 5`
-  profiles/<round>_bench.json               the bench line of that round's profile run
+  profiles/<round>_bench_kernel_stats.csv   rocprofv3 --stats of `python3 bench.py --gpus 1
+                                            --steps 20 --warmup 5` (the driver's command)
+  profiles/<round>_bench.json               the bench line of that same traced run
   profiles/<round>_pmc_engine_c2.json        per-launch PMC summary (FETCH/WRITE/SQ)
   profiles/pmc_engine_c2.json                the latter, read by bench.py for `traffic`
 HBM bytes follow MI355X_MICROARCH.md (HBM section): FETCH_SIZE (KB) x 1024 x 2
@@ -27,7 +28,9 @@ OUT = os.path.join(ROOT, "profiles")
 KERNELS = {"c2": ("engine_tri_kernel", "engine_kernel", "trim_kernel"),
            "c3": ("engine_tri_kernel", "engine_kernel", "trim_kernel"),
            "c4": ("engine_tri_kernel", "engine_kernel", "trim_kernel"),
-           "c5": ("cgr_stream_kernel", "span_first_kernel")}
+           "c5": ("cgr_stream_kernel", "span_first_kernel"),
+           "c2_lr": ("engine_tri_x_kernel", "engine_kernel"),
+           "c2_250": ("engine_tri_kernel", "engine_kernel")}
 
 
 def counters(sub, kerns):
