@@ -48,6 +48,15 @@ namespace hpgq {
 
 constexpr int kTriSlack = 8;    // readable bytes past the data end the loads may touch
 
+// A/B build knobs (tools/probes/build_geo_ab.sh): the cache policy of the read
+// streams' loads, and an XCD-contiguous workgroup -> unit order
+#ifndef HPGQ_LOAD_AUX
+#define HPGQ_LOAD_AUX 0
+#endif
+#ifndef HPGQ_XCD_REMAP
+#define HPGQ_XCD_REMAP 0
+#endif
+
 constexpr int GEO_TRI = 0, GEO_HEX = 1, GEO_WIDE = 2;
 constexpr int X_NOOR = 1, X_LR = 2;   // extra filter scans (engine_tri_x_kernel)
 
@@ -298,6 +307,13 @@ template <int MINW, int NM, bool EDIT, int G, int XM, bool FOLLOW>
 __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   static_assert(!EDIT || NM == 1, "edit on the segmented kernel is single-end");
   constexpr bool NX = XM & X_NOOR, LR = XM & X_LR;
+  // PASS FIRST (single-end, no extra scans): each step decides its reads'
+  // pass/fail from the step's own scan (segment totals by two ds_bpermute)
+  // BEFORE accumulating, so failed reads are never added and never re-read to
+  // be taken out (that re-read missed L2: +8 % HBM traffic and +3.5 % time at
+  // C2's ~6 % failures).  Paired-end and the extra-scan variants still add
+  // every read and subtract the failed ones in the unit epilogue.
+  constexpr bool PF = NM == 1 && XM == 0 && !EDIT && !FOLLOW;   // (edit, follow-up: their registers would spill)
   static_assert(!(XM && EDIT), "the extra-scan filter variants do not edit");
   using GG = Geo<G>;
   constexpr int NW = GG::kNW, kSegs = GG::kSegs, kSegW = GG::kSegW, kBlock = GG::kBlock, kU = GG::kU;
@@ -403,7 +419,10 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
 
   const int ublock = FOLLOW ? A.unit_reads : kBlock;   // reads per unit
   UnitIter<FOLLOW, kBlock> it;
-  it.init(A, (int)blockIdx.x * kWaves + wave, (int)gridDim.x * kWaves);
+  int wg = (int)blockIdx.x;
+  if (HPGQ_XCD_REMAP && (gridDim.x & 7) == 0)   // workgroups of one XCD (b mod 8) take consecutive units
+    wg = (wg & 7) * (int)(gridDim.x >> 3) + (wg >> 3);
+  it.init(A, wg * kWaves + wave, (int)gridDim.x * kWaves);
 
   // a unit's read offsets (lane j: read j), fetched one unit ahead of the
   // prologue that describes it, so the prologue does not wait for them
@@ -474,12 +493,12 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     const v4u rec = *reinterpret_cast<const v4u *>(tab(m, tb) + 4 * src);
     pd.n = rec.z;
     if (NW == 2) {
-      const v2u a = __builtin_amdgcn_raw_buffer_load_b64(rs[m], rec.x + lane8, 0, 0);
-      const v2u b = __builtin_amdgcn_raw_buffer_load_b64(rq[m], rec.y + lane8, 0, 0);
+      const v2u a = __builtin_amdgcn_raw_buffer_load_b64(rs[m], rec.x + lane8, 0, HPGQ_LOAD_AUX);
+      const v2u b = __builtin_amdgcn_raw_buffer_load_b64(rq[m], rec.y + lane8, 0, HPGQ_LOAD_AUX);
       pd.s[0] = a.x; pd.s[1] = a.y; pd.q[0] = b.x; pd.q[1] = b.y;
     } else {
-      const v4u a = __builtin_amdgcn_raw_buffer_load_b128(rs[m], rec.x + lane8, 0, 0);
-      const v4u b = __builtin_amdgcn_raw_buffer_load_b128(rq[m], rec.y + lane8, 0, 0);
+      const v4u a = __builtin_amdgcn_raw_buffer_load_b128(rs[m], rec.x + lane8, 0, HPGQ_LOAD_AUX);
+      const v4u b = __builtin_amdgcn_raw_buffer_load_b128(rq[m], rec.y + lane8, 0, HPGQ_LOAD_AUX);
 #pragma unroll
       for (int w = 0; w < NW; ++w) {
         pd.s[w] = a[w & 3];
@@ -513,11 +532,17 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     }
   };
 
+  // a step's per-lane values kept between its sums and its accumulation (PF)
+  struct StepVals {
+    uint32_t cd[NW], qm[NW], cg[NW];
+    uint32_t bad;
+  };
   // one step: per-lane partial (biased quality | G+C << 18); adds (SUB = false)
-  // or removes (SUB = true) the lane's positions from mate m's counters;
-  // NX: x2 = N | out-of-range << 16; LR: x3 = left | right window sums
+  // or removes (SUB = true) the lane's positions from mate m's counters
+  // (count = false: sums only, the values left in sv); NX: x2 = N |
+  // out-of-range << 16; LR: x3 = left | right window sums
   auto account = [&](auto mtag, const TriPending<NW> &pd, bool count, auto sub_tag, uint32_t &x2,
-                     uint32_t &x3) __attribute__((always_inline)) -> uint32_t {
+                     uint32_t &x3, StepVals &sv) __attribute__((always_inline)) -> uint32_t {
     constexpr int m = decltype(mtag)::value;
     constexpr bool SUB = decltype(sub_tag)::value;
     uint32_t sw[NW], qw[NW];
@@ -547,6 +572,13 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     uint32_t cg[NW];
 #pragma unroll
     for (int w = 0; w < NW; ++w) cg[w] = __builtin_amdgcn_perm(kCGHi, kCGLo, cd[w]);
+    sv.bad = bad;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      sv.cd[w] = cd[w];
+      sv.qm[w] = qm[w];
+      sv.cg[w] = cg[w];
+    }
     if (count) {
       TriAcc<NW> &ac = acc[m];
 #pragma unroll
@@ -615,6 +647,18 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     return qs + (gc << 18);
   };
 
+  // PF: the accumulation of a step whose values account() left in sv
+  auto account_add = [&](auto mtag, const StepVals &sv) __attribute__((always_inline)) {
+    TriAcc<NW> &ac = acc[decltype(mtag)::value];
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      ac.n4[w][0] += sv.cg[w];
+      ac.n4[w][1] += __builtin_amdgcn_perm(kATHi, kATLo, sv.cd[w]);
+      ac.q02[w] += sv.qm[w] & 0x00FF00FFu;
+      ac.q13[w] += __builtin_amdgcn_perm(0u, sv.qm[w], 0x0C030C01u);   // bytes 1, 3
+    }
+  };
+
   uint32_t len[NM], lenn[NM];
   uint32_t tw = 0, twn = 0;   // EDIT: trim word of the lane's read
   uint64_t dm = 0, dmn = 0;   // deferred lanes of the current / next unit
@@ -655,10 +699,29 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
           const int t = g * kU + u;
-          // every read is added; failed ones are taken out in the unit epilogue
           uint32_t x2 = 0, x3 = 0;
-          const uint32_t x = account(MateTag<m>{}, grp[slot][u], stats, AddTag{}, x2, x3);
+          StepVals sv;
+          // PF: sums first, the decision, then only passing reads are added;
+          // else every read is added and failed ones are taken out in the unit epilogue
+          const uint32_t x = account(MateTag<m>{}, grp[slot][u], stats && !PF, AddTag{}, x2, x3, sv);
           const uint32_t P = wave_scan(x);
+          if (PF && stats) {
+            bool pass = true;
+            if (filter) {   // this read's total: the segment's last inclusive prefix minus its first exclusive one
+              const int sg = min(seg, kSegs - 1) * kSegW;
+              const uint32_t e = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * (sg + kSegW - 1), (int)P);
+              const uint32_t b = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * sg, (int)(P - x));
+              const int n = (int)(grp[slot][u].n & 0xFFFFu), sraw = (int)((e - b) & 0x3FFFFu);
+              pass = n >= A.min_len && n <= A.max_len && lo_r * n <= sraw && sraw <= hi_r * n;
+            }
+            if (__builtin_expect(__ballot(sv.bad != 0) != 0, 0)) {   // rare: non-ACGTN bytes ("other" counts)
+              uint32_t d2, d3;
+              StepVals d;
+              if (pass) (void)account(MateTag<m>{}, grp[slot][u], true, AddTag{}, d2, d3, d);
+            } else if (pass) {
+              account_add(MateTag<m>{}, sv);
+            }
+          }
           // segment ends (the last lane of each segment) -> wends[kSegs t + seg], no wait needed
           if (ls == kSegW - 1 && seg < kSegs && t < nt) wends(m)[kSegs * t + seg] = P;
           if (NX) {
@@ -764,7 +827,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
         }
       }
     }
-    if (stats && failed) {
+    if (!PF && stats && failed) {
       // take the failed reads (pairs: both mates) back out.  A read must leave
       // through the segment it entered by (its lanes' byte counters hold it;
       // another segment's could borrow), so the failed reads of each segment
@@ -786,14 +849,15 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
         if (c == seg) mycnt = n;
       }
       uint32_t sub_x2 = 0, sub_x3 = 0;   // (unused: failed reads leave the counters only)
+      StepVals sub_sv;
       for (int k = 0; k < nsub; ++k) {
         const int src = seg < kSegs && k < mycnt ? (int)flist[min(k * kSegs + seg, 63)] : 63;
         TriPending<NW> pd;
         gather(0, tb, src, pd);
-        (void)account(MateTag<0>{}, pd, true, SubTag{}, sub_x2, sub_x3);
+        (void)account(MateTag<0>{}, pd, true, SubTag{}, sub_x2, sub_x3, sub_sv);
         if (NM == 2) {
           gather(NM - 1, tb, src, pd);
-          (void)account(MateTag<NM - 1>{}, pd, true, SubTag{}, sub_x2, sub_x3);
+          (void)account(MateTag<NM - 1>{}, pd, true, SubTag{}, sub_x2, sub_x3, sub_sv);
         }
       }
     }

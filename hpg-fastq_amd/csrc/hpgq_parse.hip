@@ -229,15 +229,16 @@ static int64_t trim_blank_tail(const char *tail, int64_t nt, int64_t n, bool &mo
     if (n < 1 || tail[n - 1 - base] != '\n') break;
     int64_t b = n - 1;   // content end of the last line
     if (b > base && tail[b - 1 - base] == '\r') --b;
-    if (b == 0 || (b > base && tail[b - 1 - base] == '\n')) {
-      n = b;
-      if (n <= base) {   // the blank tail runs past the bytes fetched
-        more = n > 0;
-        break;
-      }
-    } else {
+    if (b == 0) {   // the text is blank lines only
+      n = 0;
       break;
     }
+    if (b - 1 < base) {   // the byte before lies past the fetched tail: fetch again, ending at n
+      more = true;
+      break;
+    }
+    if (tail[b - 1 - base] != '\n') break;   // the last line is not blank
+    n = b;
   }
   return n;
 }

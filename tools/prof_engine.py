@@ -50,6 +50,8 @@ if args.mode == "c2":
 elif args.mode == "lr":   # C2 plus a 5' window filter (the window-scan variant)
     p = H.stats_params(lmax=L, read_quality_range="20,", read_length_range="50,", left_length=10,
                        left_quality_range="20,")
+elif args.mode == "nofail":   # a filter every read passes (no failed-read subtraction)
+    p = H.stats_params(lmax=L, read_quality_range="0,", read_length_range="1,")
 elif args.mode == "stats":
     p = H.stats_params(lmax=L)
 elif args.mode == "edit":
