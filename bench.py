@@ -69,6 +69,9 @@ CONFIGS = {
     "c2_nofail": dict(metric="Mreads/s (150 bp) stats + a filter every read passes", unit="Mreads/s",
                       reads=100_000_000, batch=10_000_000, L=150, seed=2,
                       workload="stats + --read-quality-range 0, --read-length-range 1, (no failures)"),
+    "c2_noor": dict(metric="Mreads/s (150 bp) stats+filter with N / out-of-range limits",
+                    unit="Mreads/s", reads=100_000_000, batch=10_000_000, L=150, seed=2,
+                    workload="C2 flags + --max-N 2 --max-out-of-quality 20"),
     "c2_lr": dict(metric="Mreads/s (150 bp) stats+filter with a 5' window filter",
                   unit="Mreads/s", reads=100_000_000, batch=10_000_000, L=150, seed=2,
                   workload="C2 flags + --left-length 10 --left-quality-range 20,"),
@@ -106,6 +109,8 @@ def params_for(cfg, L):
     if cfg == "c2_nofail":
         return H.stats_params(lmax=lmax, read_quality_range="0,", read_length_range="1,")
     extra = dict(left_length=10, left_quality_range="20,") if cfg == "c2_lr" else {}
+    if cfg == "c2_noor":
+        extra = dict(max_N=2, max_out_of_quality=20)
     p = H.stats_params(lmax=lmax, read_quality_range="20,", read_length_range="50,", **extra)
     if cfg == "c3":
         p.paired = 1

@@ -56,6 +56,9 @@ constexpr int kTriSlack = 8;    // readable bytes past the data end the loads ma
 #ifndef HPGQ_XCD_REMAP
 #define HPGQ_XCD_REMAP 0
 #endif
+#ifndef HPGQ_NO_PF_X   // extra-scan variants without pass-first (A/B)
+#define HPGQ_NO_PF_X 0
+#endif
 
 constexpr int GEO_TRI = 0, GEO_HEX = 1, GEO_WIDE = 2;
 constexpr int X_NOOR = 1, X_LR = 2;   // extra filter scans (engine_tri_x_kernel)
@@ -311,9 +314,11 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   // pass/fail from the step's own scan (segment totals by two ds_bpermute)
   // BEFORE accumulating, so failed reads are never added and never re-read to
   // be taken out (that re-read missed L2: +8 % HBM traffic and +3.5 % time at
-  // C2's ~6 % failures).  Paired-end and the extra-scan variants still add
+  // C2's ~6 % failures).  Paired-end, edit and the follow-up stages still add
   // every read and subtract the failed ones in the unit epilogue.
-  constexpr bool PF = NM == 1 && XM == 0 && !EDIT && !FOLLOW;   // (edit, follow-up: their registers would spill)
+  // (edit, follow-up: their registers would spill; the window variant alone
+  // fails few reads and ran 4 % slower with it: 692 vs 665 us per 10 M reads)
+  constexpr bool PF = NM == 1 && !EDIT && !FOLLOW && XM != X_LR && !(HPGQ_NO_PF_X && XM);
   static_assert(!(XM && EDIT), "the extra-scan filter variants do not edit");
   using GG = Geo<G>;
   constexpr int NW = GG::kNW, kSegs = GG::kSegs, kSegW = GG::kSegW, kBlock = GG::kBlock, kU = GG::kU;
@@ -341,8 +346,15 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   const bool x_all = A.flags & F_OOR_ALL, x_lonone = A.flags & F_OOR_LO_NONE, x_hinone = A.flags & F_OOR_HI_NONE;
   // LR: the window filters, read once (see NX above); length 0 = off
   const int w_ll = LR ? max(uni(A.cold->left_len), 0) : 0, w_rl = LR ? max(uni(A.cold->right_len), 0) : 0;
-  const int w_lmin = LR ? uni(A.cold->min_left) : 0, w_lmax = LR ? uni(A.cold->max_left) : 0;
-  const int w_rmin = LR ? uni(A.cold->min_right) : 0, w_rmax = LR ? uni(A.cold->max_right) : 0;
+  // (window means lie in [-383, 127] Phred: bounds clamped to +-512 keep k * bound in int32)
+  auto clampq = [](int q) { return min(max(q, -512), 512); };
+  const int w_lmin = LR ? clampq(uni(A.cold->min_left)) : 0, w_lmax = LR ? clampq(uni(A.cold->max_left)) : 0;
+  const int w_rmin = LR ? clampq(uni(A.cold->min_right)) : 0, w_rmax = LR ? clampq(uni(A.cold->max_right)) : 0;
+  // mean-quality window test in 32-bit: min*k <= S - phred*k <= max*k (S < 2^16, k <= 252)
+  auto win_in = [&](int sb, int k, int lo, int hi) __attribute__((always_inline)) {
+    const int q = sb - A.phred * k;
+    return lo * k <= q && q <= hi * k;
+  };
   // a left window within a lane's positions and no right window: no scan (the
   // segment's first lane stores its sum)
   const bool w_direct = LR && w_rl == 0 && w_ll <= 4 * NW;
@@ -705,14 +717,42 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
           // else every read is added and failed ones are taken out in the unit epilogue
           const uint32_t x = account(MateTag<m>{}, grp[slot][u], stats && !PF, AddTag{}, x2, x3, sv);
           const uint32_t P = wave_scan(x);
+          // segment ends (the last lane of each segment) -> wends[kSegs t + seg], no wait needed
+          if (ls == kSegW - 1 && seg < kSegs && t < nt) wends(m)[kSegs * t + seg] = P;
+          uint32_t P2 = 0, P3 = 0;
+          if (NX) {
+            P2 = wave_scan(x2);
+            if (ls == kSegW - 1 && seg < kSegs && t < nt) wends2(m)[kSegs * t + seg] = P2;
+          }
+          if (LR) {
+            if (w_direct) {   // the segment's first lane holds the whole window sum
+              if (ls == 0 && seg < kSegs && t < nt) wends3(m)[kSegs * t + seg] = x3;
+            } else {
+              P3 = wave_scan(x3);
+              if (ls == kSegW - 1 && seg < kSegs && t < nt) wends3(m)[kSegs * t + seg] = P3;
+            }
+          }
           if (PF && stats) {
             bool pass = true;
-            if (filter) {   // this read's total: the segment's last inclusive prefix minus its first exclusive one
+            if (filter) {   // this read's totals: the segment's last inclusive prefix minus its first exclusive one
               const int sg = min(seg, kSegs - 1) * kSegW;
-              const uint32_t e = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * (sg + kSegW - 1), (int)P);
-              const uint32_t b = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * sg, (int)(P - x));
-              const int n = (int)(grp[slot][u].n & 0xFFFFu), sraw = (int)((e - b) & 0x3FFFFu);
+              auto seg_total = [&](uint32_t Pi, uint32_t xi) __attribute__((always_inline)) {
+                return (uint32_t)__builtin_amdgcn_ds_bpermute(4 * (sg + kSegW - 1), (int)Pi) -
+                       (uint32_t)__builtin_amdgcn_ds_bpermute(4 * sg, (int)(Pi - xi));
+              };
+              const int n = (int)(grp[slot][u].n & 0xFFFFu), sraw = (int)(seg_total(P, x) & 0x3FFFFu);
               pass = n >= A.min_len && n <= A.max_len && lo_r * n <= sraw && sraw <= hi_r * n;
+              if (NX) {
+                const uint32_t r2 = seg_total(P2, x2);
+                if (x_n && (int)(r2 & 0xFFFFu) > x_maxn) pass = false;
+                if (x_o && (int)(r2 >> 16) > x_maxo) pass = false;
+              }
+              if (LR) {
+                const uint32_t r3 = w_direct ? (uint32_t)__builtin_amdgcn_ds_bpermute(4 * sg, (int)x3) : seg_total(P3, x3);
+                const int kl = min(w_ll, n), kr = min(w_rl, n);
+                if (kl > 0 && !win_in((int)(r3 & 0xFFFFu), kl, w_lmin, w_lmax)) pass = false;
+                if (kr > 0 && !win_in((int)(r3 >> 16), kr, w_rmin, w_rmax)) pass = false;
+              }
             }
             if (__builtin_expect(__ballot(sv.bad != 0) != 0, 0)) {   // rare: non-ACGTN bytes ("other" counts)
               uint32_t d2, d3;
@@ -720,20 +760,6 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
               if (pass) (void)account(MateTag<m>{}, grp[slot][u], true, AddTag{}, d2, d3, d);
             } else if (pass) {
               account_add(MateTag<m>{}, sv);
-            }
-          }
-          // segment ends (the last lane of each segment) -> wends[kSegs t + seg], no wait needed
-          if (ls == kSegW - 1 && seg < kSegs && t < nt) wends(m)[kSegs * t + seg] = P;
-          if (NX) {
-            const uint32_t P2 = wave_scan(x2);
-            if (ls == kSegW - 1 && seg < kSegs && t < nt) wends2(m)[kSegs * t + seg] = P2;
-          }
-          if (LR) {
-            if (w_direct) {   // the segment's first lane holds the whole window sum
-              if (ls == 0 && seg < kSegs && t < nt) wends3(m)[kSegs * t + seg] = x3;
-            } else {
-              const uint32_t P3 = wave_scan(x3);
-              if (ls == kSegW - 1 && seg < kSegs && t < nt) wends3(m)[kSegs * t + seg] = P3;
             }
           }
         }
@@ -793,10 +819,8 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
         const uint32_t p3 = __builtin_amdgcn_mov_dpp(e3, 0x138, 0xF, 0xF, true);   // lane j-1
         const uint32_t r3 = w_direct ? e3 : e3 - (((not_seg_first >> lane) & 1u) ? p3 : 0u);
         const int kl = min(w_ll, n), kr = min(w_rl, n);
-        if (kl > 0 && !mean_in((int64_t)(r3 & 0xFFFFu), kl, A.phred, w_lmin, w_lmax))
-          pass = false;
-        if (kr > 0 && !mean_in((int64_t)(r3 >> 16), kr, A.phred, w_rmin, w_rmax))
-          pass = false;
+        if (kl > 0 && !win_in((int)(r3 & 0xFFFFu), kl, w_lmin, w_lmax)) pass = false;
+        if (kr > 0 && !win_in((int)(r3 >> 16), kr, w_rmin, w_rmax)) pass = false;
       }
     }
     if (valid && A.mask) A.mask[my_read] = (uint8_t)pass;
