@@ -56,6 +56,9 @@ constexpr int kTriSlack = 8;    // readable bytes past the data end the loads ma
 #ifndef HPGQ_XCD_REMAP
 #define HPGQ_XCD_REMAP 0
 #endif
+#ifndef HPGQ_EARLY_TRIMS   // edit: trims one unit ahead (round 1; A/B)
+#define HPGQ_EARLY_TRIMS 0
+#endif
 #ifndef HPGQ_NO_PF_X   // extra-scan variants without pass-first (A/B)
 #define HPGQ_NO_PF_X 0
 #endif
@@ -319,6 +322,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   // (edit, follow-up: their registers would spill; the window variant alone
   // fails few reads and ran 4 % slower with it: 692 vs 665 us per 10 M reads)
   constexpr bool PF = NM == 1 && !EDIT && !FOLLOW && XM != X_LR && !(HPGQ_NO_PF_X && XM);
+  constexpr bool LATE = EDIT && !HPGQ_EARLY_TRIMS;   // the unit prologue's place (see the unit loop)
   static_assert(!(XM && EDIT), "the extra-scan filter variants do not edit");
   using GG = Geo<G>;
   constexpr int NW = GG::kNW, kSegs = GG::kSegs, kSegW = GG::kSegW, kBlock = GG::kBlock, kU = GG::kU;
@@ -689,13 +693,20 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   while (cur.u >= 0) {
     const int nr = cur.nr;
     const int nt = steps_of(cur, dm);
-    // the next unit's prologue (offsets and, for edit, the trims, which read
-    // the quality ends), so the lines the trims touch are still in L2 when the
-    // next unit streams them
-    load_block(nxt, tb ^ 1, lenn, twn, dmn, ia, ie);
-    const Unit nn2 = it.next();
-    fetch_idx(nn2, ia, ie);
-    const int nnt = steps_of(nxt, dmn);
+    // the next unit's prologue (read table, deferral mask; for edit the trims,
+    // which read the quality ends).  LATE (edit): just before the next unit's
+    // first loads, so the lines the trims bring in are still in L2 when that
+    // unit streams them (one unit ahead they were evicted: HBM traffic 1.5x
+    // the algorithmic bytes); else at the unit start, a unit ahead.
+    Unit nn2 = Unit{-1, 0, 0};
+    int nnt = 0;
+    auto describe_next = [&]() __attribute__((always_inline)) {
+      load_block(nxt, tb ^ 1, lenn, twn, dmn, ia, ie);
+      nn2 = it.next();
+      fetch_idx(nn2, ia, ie);
+      nnt = steps_of(nxt, dmn);
+    };
+    if (!LATE) describe_next();
     if (stats && since_flush > kByteEvery - kBlock / kSegs) {   // keep every byte <= 255
 #pragma unroll
       for (int m = 0; m < NM; ++m) acc[m].flush(pos_acc(m), lmax, p0);
@@ -766,8 +777,12 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       };
       // after this mate's last group: the next mate's first group, or the next unit's
       auto load_next_unit = [&](int slot) __attribute__((always_inline)) {
-        if (m + 1 < NM) load_group(m + 1 < NM ? m + 1 : 0, tb, nt, 0, slot);
-        else load_group(0, tb ^ 1, nnt, 0, slot);
+        if (m + 1 < NM) {
+          load_group(m + 1 < NM ? m + 1 : 0, tb, nt, 0, slot);
+        } else {
+          if (LATE) describe_next();
+          load_group(0, tb ^ 1, nnt, 0, slot);
+        }
       };
       for (int g = 0; g < ngroups; g += 2) {
         load_group(m, tb, nt, g + 1, 1);
@@ -784,6 +799,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       run_mate(MateTag<0>{});
       if (NM == 2) run_mate(MateTag<NM - 1>{});
     } else {
+      if (LATE) describe_next();
       load_group(0, tb ^ 1, nnt, 0, 0);   // a wholly deferred unit: straight to the next
     }
     since_flush += nt;
