@@ -18,6 +18,10 @@ namespace {
 constexpr int G = HPGQ_GEO;
 constexpr int kSeW = G == GEO_TRI ? 5 : 4;   // single-end
 constexpr int kPeW = 3;                      // paired-end
+#ifndef HPGQ_EDIT_WAVES
+#define HPGQ_EDIT_WAVES kSeW
+#endif
+constexpr int kEdW = HPGQ_EDIT_WAVES;        // single-end edit
 constexpr const char *kGeoName = G == GEO_TRI ? "tri" : (G == GEO_HEX ? "hex" : "wide");
 
 template <bool F, int XM>
@@ -38,7 +42,10 @@ SegChoice pick(int nm, bool edit, int xm, char *name, size_t cap) {
   } else {
     if (edit && nm == 2) return SegChoice{nullptr, 0};
     if (nm == 2) fn = (const void *)engine_tri_kernel<kPeW, 2, false, G, F>;
-    else if (edit) fn = (const void *)engine_tri_kernel<kSe, 1, true, G, F>;
+    else if (edit) {
+      fn = (const void *)engine_tri_kernel<kEdW, 1, true, G, F>;
+      w = kEdW;
+    }
     else fn = (const void *)engine_tri_kernel<kSe, 1, false, G, F>;
     std::snprintf(name, cap, "hpgq::engine_tri_kernel<%d, %d, %s, %s%s>", w, nm, edit ? "edit" : "filter", kGeoName,
                   F ? ", follow" : "");

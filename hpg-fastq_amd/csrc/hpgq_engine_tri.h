@@ -203,61 +203,80 @@ using SubTag = TriTag<true>;
 // first min(edit_left_length, n) bases and the trailing run within the last
 // min(edit_right_length, n - ts) with the SWAR in_range
 // test, from three 16-byte loads issued together for windows up to 16 / 32
-// bytes (else 8 bytes at a time); quality bytes [off, off + n) of rq.  Returns
-// ts | te << 16, the edit output.  Called by the unit prologue (one lane per
-// read), so the lines it touches are still in L2 when the steps stream the read.
+// bytes (trim_issue + trim_finish; else 8 bytes at a time, trim_word); quality
+// bytes [off, off + n) of rq; ts | te << 16 is the edit output.  Run by the
+// unit prologue, one lane per read.
+
+// the trim windows' quality bytes for the usual windows (left <= 16, right <=
+// 32): three 16-byte loads issued together, the right ones at pb = n - 32 (or
+// 0 for a short read, so no load starts before the read's own offset)
+struct TrimLoads {
+  v4u wl, wr0, wr1;
+};
+
+__device__ __forceinline__ bool trim_usual(const ColdParams &C) { return C.e_left_len <= 16 && C.e_right_len <= 32; }
+
+__device__ __forceinline__ TrimLoads trim_issue(const ColdParams &C, __amdgpu_buffer_rsrc_t rq, int off, int n) {
+  const int pb = n >= 32 ? n - 32 : 0;
+  TrimLoads T;
+  T.wl = C.e_left_len > 0 ? __builtin_amdgcn_raw_buffer_load_b128(rq, (uint32_t)off, 0, 0) : v4u{0u, 0u, 0u, 0u};
+  T.wr0 = T.wr1 = v4u{0u, 0u, 0u, 0u};
+  if (C.e_right_len > 0) {
+    T.wr0 = __builtin_amdgcn_raw_buffer_load_b128(rq, (uint32_t)(off + pb), 0, 0);
+    T.wr1 = __builtin_amdgcn_raw_buffer_load_b128(rq, (uint32_t)(off + pb + 16), 0, 0);
+  }
+  return T;
+}
+
+// 0x80 per in-range byte of raw quality words x, y (biased here, as the thresholds)
+__device__ __forceinline__ uint64_t trim_ok(const ColdParams &C, uint32_t x, uint32_t y, bool right) {
+  uint32_t lo, hi;
+  if (!right) {
+    lo = in_range(x ^ kQFlip, C.el_lo4, C.el_hi4, C.el_lo_none, C.el_hi_none, C.el_none_in);
+    hi = in_range(y ^ kQFlip, C.el_lo4, C.el_hi4, C.el_lo_none, C.el_hi_none, C.el_none_in);
+  } else {
+    lo = in_range(x ^ kQFlip, C.er_lo4, C.er_hi4, C.er_lo_none, C.er_hi_none, C.er_none_in);
+    hi = in_range(y ^ kQFlip, C.er_lo4, C.er_hi4, C.er_lo_none, C.er_hi_none, C.er_none_in);
+  }
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+
+__device__ __forceinline__ uint64_t trim_low_bytes(int k) { return k >= 8 ? ~0ull : ((1ull << (8 * max(k, 0))) - 1); }
+
+// the trims of a read of length n from its usual-window loads: ts | te << 16
+__device__ __forceinline__ uint32_t trim_finish(const ColdParams &C, const TrimLoads &T, int n) {
+  int ts = 0, te = 0;
+  const int pb = n >= 32 ? n - 32 : 0;
+  if (C.e_left_len > 0) {
+    const int lim = min(C.e_left_len, n);
+    const uint64_t k0 = trim_ok(C, T.wl.x, T.wl.y, false) & trim_low_bytes(lim);
+    const uint64_t k1 = trim_ok(C, T.wl.z, T.wl.w, false) & trim_low_bytes(lim - 8);
+    ts = k0 ? (__builtin_ctzll(k0) >> 3) : k1 ? 8 + (__builtin_ctzll(k1) >> 3) : lim;
+  }
+  if (C.e_right_len > 0) {
+    const int lim = min(C.e_right_len, n - ts);
+    const int lo = n - lim - pb, hi = n - pb;   // positions [lo, hi) of the 32 loaded
+    te = lim;
+    const uint64_t ok[4] = {trim_ok(C, T.wr0.x, T.wr0.y, true), trim_ok(C, T.wr0.z, T.wr0.w, true),
+                            trim_ok(C, T.wr1.x, T.wr1.y, true), trim_ok(C, T.wr1.z, T.wr1.w, true)};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {   // the last in-range byte wins (highest k last)
+      const uint64_t m = ok[k] & trim_low_bytes(hi - 8 * k) & ~trim_low_bytes(lo - 8 * k);
+      if (m) te = n - 1 - (pb + 8 * k + ((63 - __builtin_clzll(m)) >> 3));
+    }
+  }
+  return (uint32_t)ts | ((uint32_t)te << 16);
+}
+
 __device__ __forceinline__ uint32_t trim_word(const ColdParams &C, __amdgpu_buffer_rsrc_t rq,
                                               int off, int n) {
-  // 0x80 per in-range byte of raw quality words x, y (biased here, as the thresholds)
-  auto ok_of = [&](uint32_t x, uint32_t y, bool right) __attribute__((always_inline)) -> uint64_t {
-    uint32_t lo, hi;
-    if (!right) {
-      lo = in_range(x ^ kQFlip, C.el_lo4, C.el_hi4, C.el_lo_none, C.el_hi_none, C.el_none_in);
-      hi = in_range(y ^ kQFlip, C.el_lo4, C.el_hi4, C.el_lo_none, C.el_hi_none, C.el_none_in);
-    } else {
-      lo = in_range(x ^ kQFlip, C.er_lo4, C.er_hi4, C.er_lo_none, C.er_hi_none, C.er_none_in);
-      hi = in_range(y ^ kQFlip, C.er_lo4, C.er_hi4, C.er_lo_none, C.er_hi_none, C.er_none_in);
-    }
-    return (uint64_t)lo | ((uint64_t)hi << 32);
-  };
   auto ok8 = [&](int pos, bool right) __attribute__((always_inline)) -> uint64_t {
     const v2u w = __builtin_amdgcn_raw_buffer_load_b64(rq, (uint32_t)(off + pos), 0, 0);
-    return ok_of(w.x, w.y, right);
+    return trim_ok(C, w.x, w.y, right);
   };
-  auto low_bytes = [](int k) -> uint64_t { return k >= 8 ? ~0ull : ((1ull << (8 * max(k, 0))) - 1); };
+  auto low_bytes = [](int k) -> uint64_t { return trim_low_bytes(k); };
+  if (trim_usual(C)) return trim_finish(C, trim_issue(C, rq, off, n), n);
   int ts = 0, te = 0;
-  if (C.e_left_len <= 16 && C.e_right_len <= 32) {
-    // the usual windows: all loads at once, the runs found in registers
-    // (right: [pb, pb + 32) with pb = n - 32, or 0 for a short read so no load
-    // starts before the read's own offset)
-    const int pb = n >= 32 ? n - 32 : 0;
-    const v4u wl = C.e_left_len > 0 ? __builtin_amdgcn_raw_buffer_load_b128(rq, (uint32_t)off, 0, 0)
-                                    : v4u{0u, 0u, 0u, 0u};
-    v4u wr0 = v4u{0u, 0u, 0u, 0u}, wr1 = wr0;
-    if (C.e_right_len > 0) {
-      wr0 = __builtin_amdgcn_raw_buffer_load_b128(rq, (uint32_t)(off + pb), 0, 0);
-      wr1 = __builtin_amdgcn_raw_buffer_load_b128(rq, (uint32_t)(off + pb + 16), 0, 0);
-    }
-    if (C.e_left_len > 0) {
-      const int lim = min(C.e_left_len, n);
-      const uint64_t k0 = ok_of(wl.x, wl.y, false) & low_bytes(lim);
-      const uint64_t k1 = ok_of(wl.z, wl.w, false) & low_bytes(lim - 8);
-      ts = k0 ? (__builtin_ctzll(k0) >> 3) : k1 ? 8 + (__builtin_ctzll(k1) >> 3) : lim;
-    }
-    if (C.e_right_len > 0) {
-      const int lim = min(C.e_right_len, n - ts);
-      const int lo = n - lim - pb, hi = n - pb;   // positions [lo, hi) of the 32 loaded
-      te = lim;
-      const uint64_t ok[4] = {ok_of(wr0.x, wr0.y, true), ok_of(wr0.z, wr0.w, true),
-                              ok_of(wr1.x, wr1.y, true), ok_of(wr1.z, wr1.w, true)};
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {   // the last in-range byte wins (highest k last)
-        const uint64_t m = ok[k] & low_bytes(hi - 8 * k) & ~low_bytes(lo - 8 * k);
-        if (m) te = n - 1 - (pb + 8 * k + ((63 - __builtin_clzll(m)) >> 3));
-      }
-    }
-    return (uint32_t)ts | ((uint32_t)te << 16);
-  }
   if (C.e_left_len > 0) {
     const int lim = min(C.e_left_len, n);
     ts = lim;
