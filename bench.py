@@ -69,6 +69,9 @@ CONFIGS = {
     "c2_nofail": dict(metric="Mreads/s (150 bp) stats + a filter every read passes", unit="Mreads/s",
                       reads=100_000_000, batch=10_000_000, L=150, seed=2,
                       workload="stats + --read-quality-range 0, --read-length-range 1, (no failures)"),
+    "c3_nofail": dict(metric="Mpairs/s (2x150 bp) paired-end, a filter every pair passes", unit="Mpairs/s",
+                      reads=100_000_000, batch=10_000_000, L=150, seed=3,
+                      workload="PE 2x150 stats + --read-quality-range 0, --read-length-range 1, (no failures)"),
     "c2_noor": dict(metric="Mreads/s (150 bp) stats+filter with N / out-of-range limits",
                     unit="Mreads/s", reads=100_000_000, batch=10_000_000, L=150, seed=2,
                     workload="C2 flags + --max-N 2 --max-out-of-quality 20"),
@@ -106,8 +109,10 @@ def params_for(cfg, L):
                              right_length=30, right_quality_range="20,")
     if cfg == "c1_gpu":
         return H.stats_params(lmax=lmax)
-    if cfg == "c2_nofail":
-        return H.stats_params(lmax=lmax, read_quality_range="0,", read_length_range="1,")
+    if cfg in ("c2_nofail", "c3_nofail"):
+        p = H.stats_params(lmax=lmax, read_quality_range="0,", read_length_range="1,")
+        p.paired = 1 if cfg == "c3_nofail" else 0
+        return p
     extra = dict(left_length=10, left_quality_range="20,") if cfg == "c2_lr" else {}
     if cfg == "c2_noor":
         extra = dict(max_N=2, max_out_of_quality=20)

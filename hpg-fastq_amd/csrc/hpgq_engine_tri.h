@@ -56,6 +56,9 @@ constexpr int kTriSlack = 8;    // readable bytes past the data end the loads ma
 #ifndef HPGQ_XCD_REMAP
 #define HPGQ_XCD_REMAP 0
 #endif
+#ifndef HPGQ_NO_PEU   // paired-end: subtract failed pairs in the unit epilogue (round 1; A/B)
+#define HPGQ_NO_PEU 0
+#endif
 #ifndef HPGQ_EARLY_TRIMS   // edit: trims one unit ahead (round 1; A/B)
 #define HPGQ_EARLY_TRIMS 0
 #endif
@@ -191,12 +194,13 @@ __device__ __forceinline__ uint32_t tri_fix(uint32_t s, uint32_t m, uint32_t cod
   return codes & ~ff;
 }
 
-template <bool B>
+template <int V>
 struct TriTag {
-  static constexpr bool value = B;
+  static constexpr int value = V;
 };
-using AddTag = TriTag<false>;
-using SubTag = TriTag<true>;
+using AddTag = TriTag<0>;    // add the step's reads
+using SubTag = TriTag<1>;    // take reads out of the widened byte counters (unit epilogue)
+using UndoTag = TriTag<2>;   // take back what the same step just added (nibble counters)
 
 // ---- edit (A6) on the segmented kernel ---------------------------------------
 // The trim of one read: the leading run of out-of-range qualities within the
@@ -342,6 +346,13 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   // fails few reads and ran 4 % slower with it: 692 vs 665 us per 10 M reads)
   constexpr bool PF = NM == 1 && !EDIT && !FOLLOW && XM != X_LR && !(HPGQ_NO_PF_X && XM);
   constexpr bool LATE = EDIT && !HPGQ_EARLY_TRIMS;   // the unit prologue's place (see the unit loop)
+  // PEU (paired-end): a group is ONE step of both mates (grp[slot][m]); both
+  // are added, the pair is decided from both scans at once (ds_bpermute), and
+  // a failed pair is taken back out of the nibble counters from the registers
+  // still holding it -- no re-read (the epilogue's re-gather of failed pairs
+  // missed L2 and cost 15 % of C3).  Holding both mates' step values for a
+  // pass-first decision instead needed 215 VGPRs (2 waves/SIMD: no faster).
+  constexpr bool PEU = NM == 2 && !EDIT && !FOLLOW && XM == 0 && Geo<G>::kU >= 2 && !HPGQ_NO_PEU;
   static_assert(!(XM && EDIT), "the extra-scan filter variants do not edit");
   using GG = Geo<G>;
   constexpr int NW = GG::kNW, kSegs = GG::kSegs, kSegW = GG::kSegW, kBlock = GG::kBlock, kU = GG::kU;
@@ -553,6 +564,12 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     }
   };
 
+  // PEU: group g = step g of both mates
+  auto load_group_pe = [&](int tbx, int ntx, int g, int slot) __attribute__((always_inline)) {
+#pragma unroll
+    for (int m = 0; m < NM; ++m) gather(m, tbx, g < ntx ? min(kSegs * g + seg, 63) : 63, grp[slot][m]);
+  };
+
   // byte masks of the lane's words for the positions < p0 + c (c clamped to [0, 4 NW])
   auto mask_row = [&](int c, uint32_t (&mk)[NW]) __attribute__((always_inline)) {
     c = min(max(c, 0), 4 * NW);
@@ -579,7 +596,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   auto account = [&](auto mtag, const TriPending<NW> &pd, bool count, auto sub_tag, uint32_t &x2,
                      uint32_t &x3, StepVals &sv) __attribute__((always_inline)) -> uint32_t {
     constexpr int m = decltype(mtag)::value;
-    constexpr bool SUB = decltype(sub_tag)::value;
+    constexpr bool SUB = decltype(sub_tag)::value != 0, UNDO = decltype(sub_tag)::value == 2;
     uint32_t sw[NW], qw[NW];
     {   // realign: word w = bytes [al, al+4) of raw words w, w+1 (the last from lane+1)
       const uint32_t als = (pd.n >> 16) & 3u, alq = (pd.n >> 20) & 3u;
@@ -620,7 +637,12 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       for (int w = 0; w < NW; ++w) {
         const uint32_t at = __builtin_amdgcn_perm(kATHi, kATLo, cd[w]);
         const uint32_t h = __builtin_amdgcn_perm(0u, qm[w], 0x0C030C01u);   // bytes 1, 3
-        if (SUB) {
+        if (UNDO) {   // the same values this step added: no nibble can underflow
+          ac.n4[w][0] -= cg[w];
+          ac.n4[w][1] -= at;
+          ac.q02[w] -= qm[w] & 0x00FF00FFu;
+          ac.q13[w] -= h;
+        } else if (SUB) {
           ac.c8[w][1] -= cg[w] & 0x0F0F0F0Fu;
           ac.c8[w][2] -= (cg[w] >> 4) & 0x0F0F0F0Fu;
           ac.c8[w][0] -= at & 0x0F0F0F0Fu;
@@ -706,7 +728,8 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     load_block(cur, tb, len, tw, dm, ia, ie);
     nxt = it.next();
     fetch_idx(nxt, ia, ie);
-    load_group(0, tb, steps_of(cur, dm), 0, 0);
+    if (PEU) load_group_pe(tb, steps_of(cur, dm), 0, 0);
+    else load_group(0, tb, steps_of(cur, dm), 0, 0);
   }
   constexpr uint64_t not_seg_first = not_seg_first_mask<G>();   // lanes j with j % kSegs != 0
   while (cur.u >= 0) {
@@ -814,9 +837,52 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       }
       if (stats) acc[m].widen();
     };
-    if (ngroups > 0) {
+    // PEU: step g of both mates added, the pair decided, a failed pair undone
+    auto process_pair = [&](int g, int slot) __attribute__((always_inline)) {
+      constexpr int m1 = NM - 1;
+      const int t = g;
+      StepVals dsv;
+      uint32_t d2 = 0, d3 = 0;
+      const bool dec = stats && filter;
+      const int sg = min(seg, kSegs - 1) * kSegW;
+      auto read_ok = [&](uint32_t Pi, uint32_t xi, uint32_t ni) __attribute__((always_inline)) {
+        const uint32_t tot = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * (sg + kSegW - 1), (int)Pi) -
+                             (uint32_t)__builtin_amdgcn_ds_bpermute(4 * sg, (int)(Pi - xi));
+        const int n = (int)(ni & 0xFFFFu), sraw = (int)(tot & 0x3FFFFu);
+        return n >= A.min_len && n <= A.max_len && lo_r * n <= sraw && sraw <= hi_r * n;
+      };
+      const uint32_t x0 = account(MateTag<0>{}, grp[slot][0], stats, AddTag{}, d2, d3, dsv);
+      const uint32_t P0 = wave_scan(x0);
+      if (ls == kSegW - 1 && seg < kSegs && t < nt) wends(0)[kSegs * t + seg] = P0;
+      const bool pass0 = !dec || read_ok(P0, x0, grp[slot][0].n);   // (only a bool lives on)
+      const uint32_t x1 = account(MateTag<m1>{}, grp[slot][m1], stats, AddTag{}, d2, d3, dsv);
+      const uint32_t P1 = wave_scan(x1);
+      if (ls == kSegW - 1 && seg < kSegs && t < nt) wends(m1)[kSegs * t + seg] = P1;
+      if (!dec) return;
+      const bool pass = pass0 && read_ok(P1, x1, grp[slot][m1].n);
+      if (__builtin_expect(__ballot(!pass) != 0, 0) && !pass) {   // (lanes of a failed pair only)
+        (void)account(MateTag<0>{}, grp[slot][0], true, UndoTag{}, d2, d3, dsv);
+        (void)account(MateTag<m1>{}, grp[slot][m1], true, UndoTag{}, d2, d3, dsv);
+      }
+    };
+    if (PEU && ngroups > 0) {
+      const int ng = (nt + 1) & ~1;   // one step per group, an even count
+      for (int g = 0; g < ng; g += 2) {
+        load_group_pe(tb, nt, g + 1, 1);
+        process_pair(g, 0);
+        if (g + 2 < ng) load_group_pe(tb, nt, g + 2, 0);
+        else load_group_pe(tb ^ 1, nnt, 0, 0);
+        process_pair(g + 1, 1);
+        if (stats && ((g + 2) & 7) == 0)   // nibbles hold at most 15 steps
+          for (int m = 0; m < NM; ++m) acc[m].widen();
+      }
+      if (stats)
+        for (int m = 0; m < NM; ++m) acc[m].widen();
+    } else if (ngroups > 0) {
       run_mate(MateTag<0>{});
       if (NM == 2) run_mate(MateTag<NM - 1>{});
+    } else if (PEU) {
+      load_group_pe(tb ^ 1, nnt, 0, 0);   // a wholly deferred unit: straight to the next
     } else {
       if (LATE) describe_next();
       load_group(0, tb ^ 1, nnt, 0, 0);   // a wholly deferred unit: straight to the next
@@ -886,7 +952,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
         }
       }
     }
-    if (!PF && stats && failed) {
+    if (!PF && !PEU && stats && failed) {
       // take the failed reads (pairs: both mates) back out.  A read must leave
       // through the segment it entered by (its lanes' byte counters hold it;
       // another segment's could borrow), so the failed reads of each segment
