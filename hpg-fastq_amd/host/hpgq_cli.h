@@ -43,7 +43,8 @@ typedef struct {
   int filter_on;
   /* MI355X build options */
   int device;               /* first GPU */
-  int num_gpus;             /* GPU workers (0: every visible device) */
+  int num_gpus;             /* devices (0: every visible one) */
+  int gpu_workers;          /* worker threads per device (2: copy-in beside compute) */
   int64_t cg_batch_size;    /* --cg: FASTQ text bytes per chaos-game call */
   int lmax;                 /* per-position arrays (longest read kept) */
   int chunk_mb;             /* FASTQ text per parse unit */
@@ -73,7 +74,7 @@ typedef struct {
   uint32_t *cg_seq, *cg_q;  /* --cg: table_seq / table_q [dim*dim] (malloc'd) */
   uint32_t cg_words;        /* fq_word_count */
   int cg_exact_calls;       /* chaos-game calls the exact simulation redid */
-  int num_gpus;             /* GPU workers that ran */
+  int num_gpus;             /* GPU worker threads that ran */
 } cli_result_t;
 
 int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, cli_result_t *res);

@@ -91,7 +91,8 @@ static void usage(const cli_options_t *o) {
   printf("  --max-out-of-quality=<int>      Maximum number of nucleotides out of the read quality range\n");
   printf("\n  MI355X build:\n");
   printf("  --gpu=<int>                     First HIP device (default 0)\n");
-  printf("  --gpus=<int>                    GPU workers, chunks round-robin (default: every visible device)\n");
+  printf("  --gpus=<int>                    GPUs, chunks round-robin (default: every visible device)\n");
+  printf("  --gpu-workers=<int>             Worker threads per GPU (default 2: copy-in beside compute)\n");
   printf("  --lmax=<int>                    Longest read kept per position (default %d)\n",
          HPGQ_LMAX_LIMIT);
   printf("  --chunk-mb=<int>                FastQ text per GPU parse unit (default 256)\n");
@@ -113,7 +114,7 @@ static int exists(const char *path) {
 enum {
   O_THREADS = 1000, O_BATCH, O_QENC, O_KMERS, O_LRANGE, O_QRANGE, O_LLEN, O_LQRANGE, O_RLEN,
   O_RQRANGE, O_MAXN, O_MAXOOQ, O_GPU, O_LMAX, O_CHUNK, O_PRINT, O_COUNTERS, O_QUIET,
-  O_KMERSOUT, O_CG, O_KCG, O_GS, O_GPUS, O_CGBATCH, O_CGOUT
+  O_KMERSOUT, O_CG, O_KCG, O_GS, O_GPUS, O_CGBATCH, O_CGOUT, O_GPUW
 };
 
 cli_options_t *cli_parse(int command, const char *exec_name, int argc, char **argv) {
@@ -133,6 +134,7 @@ cli_options_t *cli_parse(int command, const char *exec_name, int argc, char **ar
   o->chunk_mb = 256;
   o->k_cg = 7;   /* DEFAULT_K_IN_CHAOS_GAME */
   o->cg_batch_size = 64000000;   /* DEFAULT_BATCH_SIZE_MB * 1000000, old/main_hpg_fastq_old.c:116 */
+  o->gpu_workers = 2;
   static const struct option longopts[] = {
       {"help", no_argument, 0, 'h'},
       {"fastq-file", required_argument, 0, 'f'},
@@ -155,6 +157,7 @@ cli_options_t *cli_parse(int command, const char *exec_name, int argc, char **ar
       {"max-out-of-quality", required_argument, 0, O_MAXOOQ},
       {"gpu", required_argument, 0, O_GPU},
       {"gpus", required_argument, 0, O_GPUS},
+      {"gpu-workers", required_argument, 0, O_GPUW},
       {"cg-batch-size", required_argument, 0, O_CGBATCH},
       {"cg-out", required_argument, 0, O_CGOUT},
       {"lmax", required_argument, 0, O_LMAX},
@@ -195,6 +198,7 @@ cli_options_t *cli_parse(int command, const char *exec_name, int argc, char **ar
       case O_MAXOOQ: o->max_out_of_quality = atoi(optarg); break;
       case O_GPU: o->device = atoi(optarg); break;
       case O_GPUS: o->num_gpus = atoi(optarg); break;
+      case O_GPUW: o->gpu_workers = atoi(optarg); break;
       case O_CGBATCH: o->cg_batch_size = atoll(optarg); break;
       case O_LMAX: o->lmax = atoi(optarg); break;
       case O_CHUNK: o->chunk_mb = atoi(optarg); break;
@@ -248,6 +252,7 @@ cli_options_t *cli_parse(int command, const char *exec_name, int argc, char **ar
   }
   if (o->num_threads < 1) o->num_threads = 1;
   if (o->num_gpus < 0) o->num_gpus = 0;
+  if (o->gpu_workers < 1) o->gpu_workers = 1;
   /* the old tool's floor (old/main_hpg_fastq_old.c:474-477 takes 64 MB below 64) */
   if (o->cg_batch_size < 64) o->cg_batch_size = 64000000;
   if (o->cg_batch_size > ((int64_t)1536 << 20)) {
@@ -319,8 +324,8 @@ void cli_display(const cli_options_t *o) {
     printf("\tGenomic signature   : %s\n", o->gs_filename ? o->gs_filename : "(none)");
   }
   printf("\nArchitecture options\n");
-  printf("\tGPU                 : %d (gfx950), workers: %s\n", o->device,
-         o->num_gpus > 0 ? "--gpus" : "every visible device");
+  printf("\tGPU                 : %d (gfx950), %d worker%s per GPU on %s\n", o->device, o->gpu_workers,
+         o->gpu_workers == 1 ? "" : "s", o->num_gpus > 0 ? "--gpus GPUs" : "every visible GPU");
   printf("\tReader threads      : %d\n", o->num_threads);
   printf("\tChunk size          : %d MB of FastQ text\n", o->chunk_mb);
   printf("=================================================\n");

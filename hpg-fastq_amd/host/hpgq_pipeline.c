@@ -9,8 +9,9 @@
  *              --num-threads parallel pread()s, cut at the last whole record
  *              (hpgq_fastq_complete_prefix); the partial record is carried
  *              into the next chunk.
- *   GPU        one worker thread per GPU (--gpus; default every visible
- *              device), chunk k on worker k mod G: hpgq_parse_host (H2D +
+ *   GPU        --gpu-workers threads per GPU (default 2: one copies a chunk
+ *              in while the other's kernels run) on --gpus devices (default
+ *              every visible one), chunk k on worker k mod G: hpgq_parse_host (H2D +
  *              parse into a device batch) and hpgq_run_device (filter / edit /
  *              stats fused) on the worker's ctx stream; for filter / edit the
  *              mask, trims and record offsets come back.  At the end the
@@ -433,13 +434,15 @@ int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, 
   pthread_mutex_init(&P.mu, NULL);
   pthread_cond_init(&P.cv, NULL);
 
-  /* GPU workers: --gpus (0: every visible device), worker w on device (gpu + w) mod ndev */
+  /* GPU workers: --gpu-workers per device on --gpus devices (0: every visible
+   * one); worker w on device (gpu + w mod ngpus) mod ndev */
   const int ndev = hpgq_device_count();
   if (ndev <= 0) {
     close(P.fd);
     return HPGQ_E_NO_DEVICE;
   }
-  int G = o->num_gpus > 0 ? o->num_gpus : ndev;
+  const int ngpus = o->num_gpus > 0 ? o->num_gpus : ndev;
+  int G = ngpus * (o->gpu_workers > 0 ? o->gpu_workers : 1);
   if (G > MAX_WORKERS) G = MAX_WORKERS;
   P.nworkers = G;
   P.nslots = 2 * G + 1;   /* reader + G workers + writer, with room to run ahead */
@@ -451,7 +454,7 @@ int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, 
     W[w].P = &P;
     W[w].p = p;
     W[w].w = w;
-    W[w].device = (o->device + w) % ndev;
+    W[w].device = (o->device + w % ngpus) % ndev;
     rc = worker_open(&W[w]);
   }
   /* a chunk holds --chunk-mb of text (with --cg: one chaos-game batch) */

@@ -259,15 +259,17 @@ def test_cli_cg_batches_independent_of_chunks_and_workers(tmp_path, chunk_mb, gp
 
 @pytest.mark.parametrize("cmd", ["stats", "filter", "edit"])
 def test_cli_workers_merge(tmp_path, cmd):
-    """--gpus 3 (three workers; on a one-GPU box they share device 0) with small
-    chunks: counters, k-mer tables and output files equal one worker's."""
+    """--gpus 3 --gpu-workers 2 (six workers; on a one-GPU box they share device
+    0) with small chunks: counters, k-mer tables and output files equal one
+    worker's."""
     reads = O.synth(30000, seed=27, L=150, n_per_1024=6)
     fq = _write(tmp_path, reads)
     outs = []
     for g in (1, 3):
         d = tmp_path / f"g{g}"
         d.mkdir()
-        args = [cmd, "-f", fq, "-o", d, "--chunk-mb", 1, "--gpus", g, "--counters-out", d / "ctr.bin",
+        args = [cmd, "-f", fq, "-o", d, "--chunk-mb", 1, "--gpus", g, "--gpu-workers", 1 if g == 1 else 2,
+                "--counters-out", d / "ctr.bin",
                 "--quiet", "--read-quality-range", "20,", "--read-length-range", "50,"]
         if cmd == "stats":
             args += ["--kmers", "--kmers-out", d / "km.bin", "--lmax", 150]

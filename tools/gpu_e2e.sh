@@ -12,7 +12,7 @@ for t in ${THREADS:-16}; do
   for lm in default 150; do
     LM=""; [ "$lm" != default ] && LM="--lmax $lm"
     for rep in 1 2 3; do
-      timeout -k 10 300 hpg-fastq_amd/hpg-fastq stats -f /tmp/e2e.fq -o /tmp/e2e_out --read-quality-range 20, --read-length-range 50, $LM --num-threads $t --chunk-mb ${CHUNK:-256} > gpurun_out/e2e/stats_t${t}_lmax${lm}_r${rep}.log 2>&1 || exit 6
+      timeout -k 10 300 hpg-fastq_amd/hpg-fastq stats -f /tmp/e2e.fq -o /tmp/e2e_out --read-quality-range 20, --read-length-range 50, $LM --num-threads $t --chunk-mb ${CHUNK:-256} ${E2E_ARGS} > gpurun_out/e2e/stats_t${t}_lmax${lm}_r${rep}.log 2>&1 || exit 6
     done
   done
 done
