@@ -69,9 +69,10 @@ def assert_cgr(k, batches, **kw):
     return rep
 
 
-def test_cgr_kat():
+@pytest.mark.parametrize("case", ["cgr", "cgr_k2"])
+def test_cgr_kat(case):
     from fastq_io import read_fastq
-    kat = json.load(open(os.path.join(GOLD, "kat_expected.json")))["cgr"]
+    kat = json.load(open(os.path.join(GOLD, "kat_expected.json")))[case]
     reads = read_fastq(os.path.join(GOLD, kat["reads"]))
     ts, tq, wc, _ = gpu_cgr(kat["k"], [reads], base_quality=kat["base_quality"])
     np.testing.assert_array_equal(ts, kat["table_seq"])

@@ -93,8 +93,9 @@ def test_report_golden_files(case):
             assert f.read() == data, suffix
 
 
-def test_kat_cgr():
-    c = KAT["cgr"]
+@pytest.mark.parametrize("case", ["cgr", "cgr_k2"])
+def test_kat_cgr(case):
+    c = KAT[case]
     reads = read_fastq(os.path.join(GOLD, c["reads"]))
     ts, tq, wc = O.cgr(c["k"], reads, c["base_quality"])
     np.testing.assert_array_equal(ts, c["table_seq"])
