@@ -1,7 +1,7 @@
 # build libhpgq variants for A/B timing: tools/build_ab.sh NAME "-DFLAG=..." ...
 # -> hpg-fastq_amd/ab/libhpgq_NAME.so (not tracked; travels with gpurun)
 set -e
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 name=$1; shift
 out=hpg-fastq_amd/ab/build_$name
 mkdir -p $out

@@ -2,7 +2,7 @@
 # other objects of the main build.  tools/build_cgr_ab.sh NAME "-DFLAG=..." ...
 # -> hpg-fastq_amd/ab/libhpgq_NAME.so (not tracked; travels with gpurun)
 set -e
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 name=$1; shift
 out=hpg-fastq_amd/ab/build_$name
 mkdir -p $out

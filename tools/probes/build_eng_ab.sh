@@ -1,7 +1,7 @@
 # engine-only A/B variants: recompile hpgq_engine.hip with extra flags, link with
 # the other objects of the main build.  tools/build_eng_ab.sh NAME "-DFLAG=..." ...
 set -e
-cd "$(dirname "$0")/.."
+cd "$(dirname "$0")/../.."
 name=$1; shift
 out=hpg-fastq_amd/ab/build_$name
 mkdir -p $out
