@@ -17,7 +17,10 @@ namespace {
 
 constexpr int G = HPGQ_GEO;
 constexpr int kSeW = G == GEO_TRI ? 5 : 4;   // single-end
-constexpr int kPeW = 3;                      // paired-end
+#ifndef HPGQ_PE_WAVES
+#define HPGQ_PE_WAVES 3
+#endif
+constexpr int kPeW = HPGQ_PE_WAVES;          // paired-end
 #ifndef HPGQ_EDIT_WAVES
 #define HPGQ_EDIT_WAVES kSeW
 #endif
