@@ -2,13 +2,14 @@
 filter | edit -> counters / output files, against the oracle on the same
 reads.  Small --chunk-mb forces records to be carried across parse units."""
 import os
+import subprocess
 
 import numpy as np
 import pytest
 
 import hpgfastq as H
 import oracle_lib as O
-from cli_lib import run_cli
+from cli_lib import CLI, run_cli
 from fastq_io import to_fastq
 
 pytestmark = pytest.mark.gpu
@@ -287,3 +288,38 @@ def test_cli_workers_merge(tmp_path, cmd):
         p = H.stats_params(lmax=150, read_quality_range="20,", read_length_range="50,")
         _, _, want = O.run(p, reads)
         np.testing.assert_array_equal(np.fromfile(b / "ctr.bin", np.uint64), want)
+
+
+@pytest.mark.parametrize("cmd", ["stats", "filter", "edit"])
+def test_cli_threads_under_tsan(tmp_path, cmd):
+    """The threaded host pipeline (reader threads, 2 GPU x 2 worker threads,
+    writer; hpg-fastq_amd/host/hpgq_pipeline.c) built with ThreadSanitizer
+    (`make -C hpg-fastq_amd tsan`; libhpgq itself is not instrumented): no
+    race reported, and the outputs equal the plain build's."""
+    tsan = os.path.join(os.path.dirname(CLI), "hpg-fastq-tsan")
+    if not os.path.exists(tsan):
+        pytest.fail("hpg-fastq-tsan not built (make -C hpg-fastq_amd tsan; __graft_entry__.build())")
+    reads = O.synth(20000, seed=29, L=150, n_per_1024=6)
+    fq = _write(tmp_path, reads)
+    outs = []
+    for exe in (CLI, tsan):
+        d = tmp_path / os.path.basename(exe)
+        d.mkdir()
+        args = [cmd, "-f", fq, "-o", d, "--chunk-mb", 1, "--gpus", 2, "--gpu-workers", 2,
+                "--counters-out", d / "ctr.bin", "--quiet", "--read-quality-range", "20,",
+                "--read-length-range", "50,"]
+        if cmd == "edit":
+            args += ["--left-length", 10, "--left-quality-range", "20,"]
+        supp = os.path.join(os.path.dirname(os.path.abspath(__file__)), "sanitize", "tsan.supp")
+        env = dict(os.environ, TSAN_OPTIONS=f"halt_on_error=1:second_deadlock_stack=1:suppressions={supp}")
+        # (TSan's shadow layout needs the address-space randomisation off:
+        # setarch -R, a fresh process that execs the CLI before any GPU use)
+        pre = ["setarch", os.uname().machine, "-R"] if exe == tsan else []
+        r = subprocess.run(pre + [exe] + [str(a) for a in args], capture_output=True, text=True, timeout=300,
+                           env=env)
+        assert r.returncode == 0 and "ThreadSanitizer" not in r.stderr, r.stderr[-4000:]
+        outs.append(d)
+    a, b = outs
+    np.testing.assert_array_equal(np.fromfile(a / "ctr.bin", np.uint64), np.fromfile(b / "ctr.bin", np.uint64))
+    for n in sorted(os.listdir(a)):
+        assert (a / n).read_bytes() == (b / n).read_bytes(), n
