@@ -46,6 +46,7 @@
 #define MAX_WORKERS 16
 #define MAX_SLOTS (2 * MAX_WORKERS + 2)
 #define MAX_CARRY (64u << 20)   /* longest record the reader can carry over */
+#define TRACE_MAX 1024
 
 typedef struct {
   char *buf;          /* page-locked */
@@ -76,7 +77,20 @@ typedef struct {
   FILE *out_pass, *out_fail;
   uint64_t written_pass, written_fail;
   int64_t cg_batch;   /* --cg: bytes of FASTQ text per chaos-game call (0: off) */
+  /* HPGQ_TRACE=1: per chunk (the first TRACE_MAX) the reader's and the worker's
+   * start / end times, printed to stderr at the end (diagnostics only) */
+  int trace;
+  double t0;
+  double tr[TRACE_MAX][5];   /* read start, read end, worker start, sync start, worker end */
+  int tw[TRACE_MAX];
 } pipe_t;
+
+static double now_s(void);
+static void trace_at(pipe_t *P, int64_t k, int i, int w) {
+  if (!P->trace || k >= TRACE_MAX) return;
+  P->tr[k][i] = now_s() - P->t0;
+  if (w >= 0) P->tw[k] = w;
+}
 
 static double now_s(void) {
   struct timespec t;
@@ -154,6 +168,7 @@ static void *reader_main(void *arg) {
     const int err = P->error;
     pthread_mutex_unlock(&P->mu);
     if (err) break;
+    trace_at(P, k, 0, -1);
     memcpy(s->buf, P->carry, P->carry_len);
     s->len = P->carry_len;
     const off_t g0 = P->pos - (off_t)P->carry_len;   /* file offset of buf[0] */
@@ -206,6 +221,7 @@ static void *reader_main(void *arg) {
       break;
     }
     memcpy(P->carry, s->buf + s->use, P->carry_len);
+    trace_at(P, k, 1, -1);
     pthread_mutex_lock(&P->mu);
     s->chunk = k;
     s->state = 1;
@@ -383,6 +399,7 @@ static int worker_chunk(worker_t *W, slot_t *s) {
     }
     if (rc == 0) rc = hpgq_parse_records(W->ps, s->rec_start, s->seq_start, s->plus_start, s->qual_start);
   }
+  trace_at(W->P, s->chunk, 3, -1);
   if (rc == 0) rc = hpgq_sync(W->ctx);
   if (rc == 0 && W->cg) {   /* after the parse and the mask; settled before the next parse reuses b */
     rc = hpgq_cgr_fill_device(W->cg, &b, o->filter_on ? W->d_mask : NULL,
@@ -406,7 +423,9 @@ static void *worker_main(void *arg) {
     const int stop = P->error || !(s->state == 1 && s->chunk == k);
     pthread_mutex_unlock(&P->mu);
     if (stop) break;
+    trace_at(P, k, 2, W->w);
     const int rc = worker_chunk(W, s);
+    trace_at(P, k, 4, -1);
     W->fastq_bytes += (double)s->use;
     pthread_mutex_lock(&P->mu);
     if (rc && !P->error) P->error = rc;
@@ -424,6 +443,7 @@ static void *worker_main(void *arg) {
 int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, cli_result_t *res) {
   pipe_t P;
   memset(&P, 0, sizeof(P));
+  P.trace = getenv("HPGQ_TRACE") != NULL;
   P.o = o;
   memset(res, 0, sizeof(*res));
   P.fd = open(o->in_filename, O_RDONLY);
@@ -482,6 +502,7 @@ int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, 
   if (rc) goto done;
 
   const double t0 = now_s();
+  P.t0 = t0;
   pthread_t reader, writer;
   pthread_create(&reader, NULL, reader_main, &P);
   if (writes) pthread_create(&writer, NULL, writer_main, &P);
@@ -543,6 +564,9 @@ int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, 
   }
   res->seconds = now_s() - t0;
   res->num_gpus = G;
+  for (int64_t k = 0; P.trace && k < P.chunks && k < TRACE_MAX; ++k)
+    fprintf(stderr, "trace chunk %lld: read %.1f-%.1f ms, worker %d %.1f-%.1f (sync from %.1f) ms\n", (long long)k,
+            1e3 * P.tr[k][0], 1e3 * P.tr[k][1], P.tw[k], 1e3 * P.tr[k][2], 1e3 * P.tr[k][4], 1e3 * P.tr[k][3]);
   if (rc == 0) {
     res->num_passed = counters[HPGQ_S_NUM_PASSED];
     res->num_failed = counters[HPGQ_S_NUM_FAILED];
