@@ -16,7 +16,10 @@ namespace hpgq {
 namespace {
 
 constexpr int G = HPGQ_GEO;
-constexpr int kSeW = G == GEO_TRI ? 5 : 4;   // single-end
+#ifndef HPGQ_SE_WAVES
+#define HPGQ_SE_WAVES (G == GEO_TRI ? 5 : 4)
+#endif
+constexpr int kSeW = HPGQ_SE_WAVES;          // single-end
 #ifndef HPGQ_PE_WAVES
 #define HPGQ_PE_WAVES 3
 #endif
