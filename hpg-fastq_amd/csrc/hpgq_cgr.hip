@@ -841,7 +841,8 @@ int hpgq_cgr_fill_device(hpgq_cgr_t *c, const hpgq_batch_t *b, const uint8_t *st
   SA.words = c->d_words;
   void *sargs[] = {&SA};
   HPGQ_HIP_TRY(hipLaunchKernel((const void *)S::span_first_kernel,
-                               dim3((unsigned)((b->num_reads + 1 + 255) / 256)), dim3(256), sargs, 0, c->stream));
+                               dim3((unsigned)std::min<int64_t>((b->num_reads + 1 + 255) / 256, S::kSpanFirstGrid)),
+                               dim3(256), sargs, 0, c->stream));
   HPGQ_HIP_TRY(hipLaunchKernel(S::stream_for(c->k), dim3(c->s_grid), dim3(S::kWG), sargs, 0, c->stream));
   c->pending.push_back(*b);
   return HPGQ_OK;

@@ -75,6 +75,9 @@ constexpr int kSpan = 1 << kSpanLog;         // bytes per span (16 KB, 8 tiles)
 #ifndef HPGQ_CGR_XCHG
 #define HPGQ_CGR_XCHG 0   // 1: read and clear by one exchange (measured ~1% slower)
 #endif
+#ifndef HPGQ_SPAN_FIRST_GRID
+#define HPGQ_SPAN_FIRST_GRID 2048
+#endif
 #ifndef HPGQ_CGR_CHAINS
 #define HPGQ_CGR_CHAINS 1   // independent add chains per lane and tile (2: measured no faster)
 #endif
@@ -112,21 +115,25 @@ __device__ __forceinline__ int64_t nspans(int32_t a0, int32_t b1) {
 // span_first[s] = the first read r with idx[r] >= a0 + s*kSpan - 32: thread r
 // writes the spans whose (start - 32) lies in (idx[r-1], idx[r]]; thread 0
 // also clears this fill's gate and done slots
+// (grid-stride: a few thousand workgroups walk the whole idx array; one
+// thread per read made the launch dispatch-bound at ~17 us per 5 M reads)
+constexpr int kSpanFirstGrid = HPGQ_SPAN_FIRST_GRID;
 __global__ void __launch_bounds__(256) span_first_kernel(SArgs A) {
-  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (r == 0) {
-    *A.gate = 0u;
-    *A.done = 0u;
-  }
-  if (r > A.num_reads) return;
   const int32_t b0 = A.idx[0], b1 = A.idx[A.num_reads];
   const int32_t a0 = b0 & ~15;
   const int64_t ns = nspans(a0, b1);
-  const int64_t hi = (int64_t)A.idx[r] + 32 - a0;   // s*kSpan <= hi
-  const int64_t lo = r == 0 ? -1 : (int64_t)A.idx[r - 1] + 32 - a0;   // s*kSpan > lo
-  const int64_t s0 = lo < 0 ? 0 : (lo >> kSpanLog) + 1;
-  const int64_t s1 = r == A.num_reads ? ns - 1 : (hi >> kSpanLog);   // past the last start: the end sentinel
-  for (int64_t s = s0; s <= s1 && s < ns; ++s) A.span_first[s] = (int32_t)r;
+  const int64_t stride = (int64_t)gridDim.x * 256;
+  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r <= A.num_reads; r += stride) {
+    if (r == 0) {
+      *A.gate = 0u;
+      *A.done = 0u;
+    }
+    const int64_t hi = (int64_t)A.idx[r] + 32 - a0;   // s*kSpan <= hi
+    const int64_t lo = r == 0 ? -1 : (int64_t)A.idx[r - 1] + 32 - a0;   // s*kSpan > lo
+    const int64_t s0 = lo < 0 ? 0 : (lo >> kSpanLog) + 1;
+    const int64_t s1 = r == A.num_reads ? ns - 1 : (hi >> kSpanLog);   // past the last start: the end sentinel
+    for (int64_t s = s0; s <= s1 && s < ns; ++s) A.span_first[s] = (int32_t)r;
+  }
 }
 
 // a lane's word of a start bitmap, cleared for its next use in the same LDS op
