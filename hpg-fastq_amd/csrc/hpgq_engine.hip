@@ -179,9 +179,10 @@ static void catch_all(Stage &s, int nm, int lmax, bool gen, bool follow) {
                 follow ? " (follow-up)" : "");
 }
 
-static size_t seg_lds(const hpgq_params_t &p, int nm, int xm) {
-  const size_t hlen = (size_t)p.lmax + 1 + HPGQ_MEANQ_BINS + HPGQ_GC_BINS;
-  const size_t mate_words = (size_t)6 * p.lmax + ((hlen + 1) & ~(size_t)1) + 2 * HPGQ_NUM_SCALARS;
+static size_t seg_lds(const hpgq_params_t &p, int nm, int xm, int pos) {
+  const size_t lp = (size_t)std::min(p.lmax, pos);   // the kernel's on-chip positions (tri_body: lp)
+  const size_t hlen = lp + 1 + HPGQ_MEANQ_BINS + HPGQ_GC_BINS;
+  const size_t mate_words = (size_t)6 * lp + ((hlen + 1) & ~(size_t)1) + 2 * HPGQ_NUM_SCALARS;
   // per mate [6][lmax] + hist + scalars, 16 B alignment, the byte-mask table,
   // per wave and mate two read tables (2 x 1 KB) + segment ends (+ one list per
   // extra scan), per wave a compaction scratch and a deferral word
@@ -264,13 +265,13 @@ static int plan_chain(hpgq_ctx *c, Chain &ch, int cus, int geo_force) {
   // a merged read longer than lmax leaves the segmented kernels (the
   // catch-all counts it as a long read)
   ch.s1.defer_len = stats ? std::min(pos1, p.lmax) : pos1;
-  int rc = finish_stage(c, ch.s1, seg_lds(p, c->nm, xm), cus);
+  int rc = finish_stage(c, ch.s1, seg_lds(p, c->nm, xm, pos1), cus);
   if (rc) return rc;
   ch.has2 = geo != hpgq::GEO_WIDE && ch.s1.defer_len < posw && !(stats && p.lmax <= pos1);
   if (ch.has2) {
     if (!seg_stage(ch.s2, hpgq::GEO_WIDE, c->nm, edit, xm, true)) return HPGQ_E_INVALID;
     ch.s2.defer_len = stats ? std::min(posw, p.lmax) : posw;
-    rc = finish_stage(c, ch.s2, seg_lds(p, c->nm, xm), cus);
+    rc = finish_stage(c, ch.s2, seg_lds(p, c->nm, xm, posw), cus);
     if (rc) return rc;
   }
   ch.has3 = true;

@@ -702,6 +702,29 @@ __device__ __forceinline__ void add_partials(uint64_t *dst, const unsigned long 
                 i < lmax ? (unsigned long long)(long long)(int32_t)pos[i] : (unsigned long long)pos[i]);
 }
 
+// the same from an LDS set sized for lp <= lmax positions (the segmented
+// kernels: their reads are at most a geometry's kPos long): hist [lp + 1 +
+// MEANQ + GC], pos [6][lp], added at the global layout's lmax offsets
+__device__ __forceinline__ void add_partials_lp(uint64_t *dst, const unsigned long long *sc,
+                                                const uint32_t *hist, const uint32_t *pos, int lmax, int lp,
+                                                int tid, int nthreads) {
+  for (int i = tid; i < HPGQ_NUM_SCALARS; i += nthreads)
+    if (sc[i]) atomicAdd(reinterpret_cast<unsigned long long *>(dst + i), sc[i]);
+  const int hl = lp + 1 + HPGQ_MEANQ_BINS + HPGQ_GC_BINS;
+  for (int i = tid; i < hl; i += nthreads)
+    if (hist[i]) {
+      const int gi = i <= lp ? i : i + (lmax - lp);   // mean-Q / GC bins follow the lmax + 1 length bins
+      atomicAdd(reinterpret_cast<unsigned long long *>(dst + HPGQ_NUM_SCALARS + gi), (unsigned long long)hist[i]);
+    }
+  uint64_t *dp = dst + HPGQ_NUM_SCALARS + lmax + 1 + HPGQ_MEANQ_BINS + HPGQ_GC_BINS;
+  for (int i = tid; i < 6 * lp; i += nthreads)
+    if (pos[i]) {
+      const int r = i / lp, j = i - r * lp;
+      atomicAdd(reinterpret_cast<unsigned long long *>(dp + r * lmax + j),
+                r == 0 ? (unsigned long long)(long long)(int32_t)pos[i] : (unsigned long long)pos[i]);
+    }
+}
+
 template <int NM, int NCH, bool GEN, bool FOLLOW>
 __global__ void __launch_bounds__(kWG) engine_kernel(EngineArgs A) {
   if (FOLLOW && follow_up_idle(A)) return;

@@ -364,7 +364,11 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   const int lane = tid & 63;
   const int wave = uni(tid >> 6);
   const int lmax = A.lmax;
-  const int hlen = lmax + 1 + HPGQ_MEANQ_BINS + HPGQ_GC_BINS;
+  // the LDS partials cover lp positions: every read this kernel merges is at
+  // most min(lmax, kPos) long (longer ones are deferred), so the counter set
+  // on chip does not grow with lmax (at lmax 1024 it would cut the residency)
+  const int lp = min(lmax, Geo<G>::kPos);
+  const int hlen = lp + 1 + HPGQ_MEANQ_BINS + HPGQ_GC_BINS;
   const int seg = min(lane / kSegW, kSegs);     // kSegs: idle lanes
   const int ls = lane - seg * kSegW;
   const bool owner = seg < kSegs && ls < GG::kOwn;
@@ -406,13 +410,13 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   // disjoint from the scratch: no type-punned aliasing); then the byte-mask table.
   // (pos_acc row 5 holds "other" counts until the epilogue turns it into N)
   const int hist_words = (hlen + 1) & ~1;
-  const int mate_words = 6 * lmax + hist_words + 2 * HPGQ_NUM_SCALARS;   // even: sc 8-B aligned
+  const int mate_words = 6 * lp + hist_words + 2 * HPGQ_NUM_SCALARS;   // even: sc 8-B aligned
   uint32_t *base = reinterpret_cast<uint32_t *>(lds);
   auto pos_acc = [&](int m) __attribute__((always_inline)) { return base + m * mate_words; };
-  auto other = [&](int m) __attribute__((always_inline)) { return base + m * mate_words + 5 * lmax; };
-  auto hist = [&](int m) __attribute__((always_inline)) { return base + m * mate_words + 6 * lmax; };
+  auto other = [&](int m) __attribute__((always_inline)) { return base + m * mate_words + 5 * lp; };
+  auto hist = [&](int m) __attribute__((always_inline)) { return base + m * mate_words + 6 * lp; };
   auto sc = [&](int m) __attribute__((always_inline)) {
-    return reinterpret_cast<unsigned long long *>(base + m * mate_words + 6 * lmax + hist_words);
+    return reinterpret_cast<unsigned long long *>(base + m * mate_words + 6 * lp + hist_words);
   };
   constexpr int kMateWaveWords = 2 * 256 + 64 * (1 + (NX ? 1 : 0) + (LR ? 1 : 0));
   constexpr int kWaveWords = NM * kMateWaveWords + 64 + 4;   // (multiple of 4: 16 B tables)
@@ -619,7 +623,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     if (__builtin_expect(bad != 0, 0)) {
       const uint32_t sign = SUB ? 0xFFFFFFFFu : 1u;
 #pragma unroll
-      for (int w = 0; w < NW; ++w) cd[w] = tri_fix(sw[w], mk[w], cd[w], other(m), count ? lmax : 0, p0 + 4 * w, sign);
+      for (int w = 0; w < NW; ++w) cd[w] = tri_fix(sw[w], mk[w], cd[w], other(m), count ? lp : 0, p0 + 4 * w, sign);
     }
     uint32_t cg[NW];
 #pragma unroll
@@ -751,7 +755,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     if (!LATE) describe_next();
     if (stats && since_flush > kByteEvery - kBlock / kSegs) {   // keep every byte <= 255
 #pragma unroll
-      for (int m = 0; m < NM; ++m) acc[m].flush(pos_acc(m), lmax, p0);
+      for (int m = 0; m < NM; ++m) acc[m].flush(pos_acc(m), lp, p0);
       since_flush = 0;
     }
     // an even number of groups per mate, so every mate (and unit) starts in
@@ -945,8 +949,8 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
             uint32_t bin;
             uint64_t fx;
             meanq_terms(s, wn, bin, fx);
-            atomicAdd(&h[lmax + 1 + bin], 1u);
-            atomicAdd(&h[lmax + 1 + HPGQ_MEANQ_BINS + (100 * gc) / wn], 1u);
+            atomicAdd(&h[lp + 1 + bin], 1u);
+            atomicAdd(&h[lp + 1 + HPGQ_MEANQ_BINS + (100 * gc) / wn], 1u);
             fx16[m] += fx;
           }
         }
@@ -1000,7 +1004,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
 #pragma unroll
   for (int m = 0; m < NM; ++m) {
     acc[m].widen();
-    acc[m].flush(pos_acc(m), lmax, p0);
+    acc[m].flush(pos_acc(m), lp, p0);
     const uint64_t tot = wave_sum64(fx16[m]);
     if (lane == 0) {
       unsigned long long *s = sc(m);
@@ -1014,10 +1018,10 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   }
   __syncthreads();
 #pragma unroll
-  for (int m = 0; m < NM; ++m) pos_fix<true>(pos_acc(m), hist(m), lmax, tid, mtab);   // (mtab is free now)
+  for (int m = 0; m < NM; ++m) pos_fix<true>(pos_acc(m), hist(m), lp, tid, mtab);   // (mtab is free now)
 #pragma unroll
   for (int m = 0; m < NM; ++m)
-    add_partials(A.counters + (size_t)m * A.clen, sc(m), hist(m), hlen, pos_acc(m), lmax, tid, kWG);
+    add_partials_lp(A.counters + (size_t)m * A.clen, sc(m), hist(m), pos_acc(m), lmax, lp, tid, kWG);
 }
 
 template <int MINW, int NM, bool EDIT, int G, bool FOLLOW>
