@@ -20,7 +20,9 @@ def host_batch(seq, qual, idx):
     """hpgq_batch_t over host numpy arrays (uint8, uint8, int32 of n+1)."""
     assert seq.dtype == np.uint8 and qual.dtype == np.uint8 and idx.dtype == np.int32
     assert seq.flags.c_contiguous and qual.flags.c_contiguous and idx.flags.c_contiguous
-    return Batch(len(idx) - 1, seq.ctypes.data, qual.ctypes.data, idx.ctypes.data)
+    b = Batch(len(idx) - 1, seq.ctypes.data, qual.ctypes.data, idx.ctypes.data)
+    b._keep = (seq, qual, idx)   # the struct holds raw pointers: keep the arrays alive with it
+    return b
 
 
 def device_batch(num_reads, seq_ptr, qual_ptr, idx_ptr):

@@ -111,3 +111,14 @@ def test_open_fails_loudly_without_device():
     with pytest.raises(H.HpgqError) as e:
         H.Engine(H.stats_params(lmax=150))
     assert e.value.code == -5
+
+
+def test_host_batch_keeps_its_arrays_alive():
+    """hpgq_batch_t holds raw pointers: a batch built over temporaries (e.g. a
+    sliced idx copy) must keep them alive, or the ABI reads freed memory."""
+    import gc
+    seq = np.frombuffer(b"ACGTACGT", dtype=np.uint8).copy()
+    b = H.engine.host_batch(seq, seq.copy(), np.array([2, 5, 8], dtype=np.int32).copy())
+    gc.collect()
+    idx = (C.c_int32 * 3).from_address(b.data_indices)
+    assert list(idx) == [2, 5, 8] and b.num_reads == 2
