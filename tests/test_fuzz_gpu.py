@@ -10,7 +10,8 @@ IUPAC bytes and quality bytes >= 128 (signed char), split
 over two calls with absolute offsets so the counters accumulate.  Masks,
 trims and the packed u64 counter sets must equal oracle_run's
 (oracle/hpgq_oracle.c, restating src/stats_fastq.c:257-417 and the filter /
-edit spec of DESIGN §2) whichever kernel chain the options route to.
+edit spec of DESIGN §2) whichever kernel chain the options route to, with
+the first geometry forced to tri / wide or the catch-all alone on some cases.
 """
 import numpy as np
 import pytest
@@ -20,7 +21,9 @@ import oracle_lib as O
 
 pytestmark = pytest.mark.gpu
 
-NCASES = 48
+NCASES = 192
+# first stage per case: the default chain, or forced (HPGQ_TRI_GEO / HPGQ_KERNEL=single)
+ROUTES = ["auto", "auto", "tri", "wide", "auto", "auto", "tri", "single"]
 LMAX = [64, 150, 156, 157, 160, 200, 250, 252, 300, 1024]
 BASE_LEN = [1, 20, 63, 100, 149, 150, 151, 156, 157, 160, 161, 200, 250, 252, 253, 300]
 
@@ -99,6 +102,11 @@ def _params(rng):
 def test_random_option_combination(case, monkeypatch):
     monkeypatch.delenv("HPGQ_KERNEL", raising=False)
     monkeypatch.delenv("HPGQ_TRI_GEO", raising=False)
+    route = ROUTES[case % len(ROUTES)]
+    if route == "single":
+        monkeypatch.setenv("HPGQ_KERNEL", "single")
+    elif route != "auto":
+        monkeypatch.setenv("HPGQ_TRI_GEO", route)
     rng = np.random.default_rng(1000 + case)
     p, cmd, o = _params(rng)
     n = int(rng.integers(1, 6000))
@@ -130,7 +138,7 @@ def test_random_option_combination(case, monkeypatch):
                 trim[n + lo:n + hi] = t[hi - lo:]
         c_g = e.counters()
         chain = e.kernel_chain
-    info = f"case {case}: {cmd} paired={p.paired} lmax={p.lmax} n={n} cut={cut} {o} chain={chain}"
+    info = f"case {case} ({route}): {cmd} paired={p.paired} lmax={p.lmax} n={n} cut={cut} {o} chain={chain}"
     np.testing.assert_array_equal(mask, m_o, err_msg=info)
     if p.edit_on:
         np.testing.assert_array_equal(trim, t_o, err_msg=info)
