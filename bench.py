@@ -307,14 +307,16 @@ def main():
     ext = torch.cuda.ExternalStream(eng.stream, device=dev)
     hb = [[H.engine.device_batch(n, sq.data_ptr(), ql.data_ptr(), ix.data_ptr())
            for (sq, ql, ix) in mm] for (n, mm, _nb) in batches]
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in batches]
+    # HIP events around every launch of every timed step (read after the loop)
+    ev = [[(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in batches] for _ in range(args.steps)]
 
-    def step(timed):
+    def step(evs=None):
+        timed = evs is not None
         eng.reset()
         for i, b in enumerate(hb):
             if timed:
-                ev[i][0].record(ext)
+                evs[i][0].record(ext)
             if cgr:
                 eng.fill_device(b[0])
             else:
@@ -322,12 +324,12 @@ def main():
                                d_mask.data_ptr() + int(offs[i]),
                                d_trim.data_ptr() + 4 * int(offs[i]) if params.edit_on else None)
             if timed:
-                ev[i][1].record(ext)
+                evs[i][1].record(ext)
         if world > 1:   # the one exchange step: RCCL sum of the counters / u32 CGR tables
             eng.allreduce()
 
     for _ in range(args.warmup):
-        step(False)
+        step()
     eng.sync()
     torch.cuda.synchronize()
 
@@ -335,11 +337,13 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    kern_ms = []
-    for _ in range(args.steps):
-        step(True)
-        eng.sync()
-        kern_ms.extend(a.elapsed_time(b) for a, b in ev)
+    for s in range(args.steps):
+        step(ev[s])
+        if cgr:   # a gated CGR call is redone exactly inside the sync: once per step
+            eng.sync()
+    # the engine steps queue back to back on the stream (stream-ordered resets);
+    # one host sync after the K steps (it also returns the error flag)
+    eng.sync()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -348,6 +352,7 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t.item())
+    kern_ms = [a.elapsed_time(b) for evs in ev for a, b in evs]
 
     # sanity: every read accounted for
     if cgr:
