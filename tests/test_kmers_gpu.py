@@ -73,3 +73,20 @@ def test_kmers_large_synthetic():
 def test_kmers_small_lmax_is_empty():
     reads = O.Reads.from_pairs([(b"ACGTACGT", b"IIIIIIII")])
     assert gpu_kmers(4, [reads]).size == 0
+
+
+@pytest.mark.parametrize("case", range(24))
+def test_kmers_random_combinations(case):
+    """Seeded draws of lmax (5..1024), 1-3 batches, with or without a pass
+    mask, leading offsets and homopolymer-heavy or odd-byte alphabets."""
+    rng = np.random.default_rng(700 + case)
+    lmax = int(rng.choice([5, 9, 64, 150, 156, 157, 160, 250, 252, 300, 1024]))
+    alphabet = [b"ACGTACGTACGTNacgtRY", b"AAAAAAAAAAAAAAAACGTN", b"ACGT", b"ACGTN-*."][case % 4]
+    batches = [_random_reads(rng, int(rng.integers(1, 1500)), 0, lmax + int(rng.integers(1, 60)),
+                             alphabet) for _ in range(int(rng.integers(1, 4)))]
+    masks = [(rng.random(b.n) < 0.7).astype(np.uint8) for b in batches] if case % 3 else None
+    want = np.zeros((1024, max(lmax - 4, 0)), dtype=np.uint64)
+    for i, b in enumerate(batches):
+        O.kmers(b, lmax, masks[i] if masks else None, want)
+    got = gpu_kmers(lmax, batches, masks, offset=int(rng.integers(0, 40)))
+    np.testing.assert_array_equal(got, want)
