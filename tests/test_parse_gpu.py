@@ -86,3 +86,32 @@ def test_parse_trailing_blank_lines(tail):
         assert ps.parse(b"\n\n").num_reads == 0
         with pytest.raises(H.HpgqError):
             ps.parse(b"@r\nACGT\n+\nIIII\n\n@s\nAC\n+\nII\n")
+
+
+@pytest.mark.parametrize("case", range(16))
+def test_parse_random_records(case):
+    """Seeded record sets (lengths 0..1024, odd bytes, '@' / '+' as quality
+    characters, LF or CRLF, bare or repeated '+' headers) parse to the same
+    records and the same engine results as the oracle on the reads."""
+    rng = np.random.default_rng(900 + case)
+    n = int(rng.integers(1, 3000))
+    top = int(rng.choice([10, 150, 300, 1024]))   # lmax <= HPGQ_LMAX_LIMIT
+    pairs = []
+    for _ in range(n):
+        L = int(rng.integers(0, top + 1))
+        s = np.frombuffer(b"ACGTNacgtRY", np.uint8)[rng.integers(0, 11, L)].tobytes()
+        q = (33 + rng.integers(0, 60, L)).astype(np.uint8).tobytes()   # includes '@' (64)
+        pairs.append((s, q))
+    reads = O.Reads.from_pairs(pairs)
+    crlf, plus = bool(case & 1), bool(case & 2)
+    text, _ = to_fastq(reads, crlf=crlf, plus_header=plus, prefix=["r", "@r", "+r", "r:"][case % 4])
+    lmax = max(top, 8)
+    p = H.stats_params(lmax=lmax, read_quality_range="15,", read_length_range="3,")
+    mask, ctr, recs, got_n = parse_and_run(text, p)
+    assert got_n == reads.n
+    m_o, _, c_o = O.run(p, reads)
+    np.testing.assert_array_equal(mask, m_o)
+    np.testing.assert_array_equal(ctr, c_o)
+    ref = np.array(split_records(text), np.uint32)
+    np.testing.assert_array_equal(recs["start"], ref[:, 0])
+    np.testing.assert_array_equal(recs["qual"], ref[:, 3])
