@@ -93,6 +93,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--lmax", type=int, default=None, help="override the config's lmax")
     a = ap.parse_args()
+    if a.steps < 1 or a.warmup < 0:
+        ap.error("--steps must be >= 1 and --warmup >= 0")
     cfg = CONFIGS[a.config]
     a.reads = a.reads or cfg["reads"]
     a.batch_reads = a.batch_reads or cfg["batch"]
