@@ -309,26 +309,31 @@ def main():
     ext = torch.cuda.ExternalStream(eng.stream, device=dev)
     hb = [[H.engine.device_batch(n, sq.data_ptr(), ql.data_ptr(), ix.data_ptr())
            for (sq, ql, ix) in mm] for (n, mm, _nb) in batches]
-    # HIP events around every launch of the LAST timed step (read after the
-    # loop): each event pair between two launches costs a ~10 us gap on the
-    # stream, so events in every step would take ~2 % off the timed steps
+    # HIP events on the engine stream bracket the timed launches: ONE pair
+    # around all K steps' launches (the steps queue back to back; an event pair
+    # between two launches leaves a ~10 us gap, so none sit between launches),
+    # or per step when the steps are separated by a host sync (CGR) or by the
+    # RCCL all-reduce (N > 1), which the brackets leave out.
+    # avg launch = bracketed GPU time / launches (it includes the chain's idle
+    # follow-up stages and the resets: a slight overstatement of the kernel).
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in batches]
+          for _ in range(args.steps)]
+    nb = len(hb)
+    per_step = cgr or world > 1
 
-    def step(evs=None):
-        timed = evs is not None
+    def step(s=None):
         eng.reset()
         for i, b in enumerate(hb):
-            if timed:
-                evs[i][0].record(ext)
+            if s is not None and i == 0 and (per_step or s == 0):
+                ev[s][0].record(ext)
             if cgr:
                 eng.fill_device(b[0])
             else:
                 eng.run_device(b[0], b[1] if mates == 2 else None,
                                d_mask.data_ptr() + int(offs[i]),
                                d_trim.data_ptr() + 4 * int(offs[i]) if params.edit_on else None)
-            if timed:
-                evs[i][1].record(ext)
+            if s is not None and i == nb - 1 and (per_step or s == args.steps - 1):
+                ev[s][1].record(ext)
         if world > 1:   # the one exchange step: RCCL sum of the counters / u32 CGR tables
             eng.allreduce()
 
@@ -342,7 +347,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for s in range(args.steps):
-        step(ev if s == args.steps - 1 else None)
+        step(s)
         if cgr:   # a gated CGR call is redone exactly inside the sync: once per step
             eng.sync()
     # the engine steps queue back to back on the stream (stream-ordered resets);
@@ -356,7 +361,10 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t.item())
-    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    if per_step:
+        timed_ms = sum(a.elapsed_time(b) for a, b in ev)
+    else:
+        timed_ms = ev[0][0].elapsed_time(ev[-1][1])
 
     # sanity: every read accounted for
     if cgr:
@@ -369,7 +377,7 @@ def main():
 
     total = args.reads * world * args.steps
     value = total / el / 1e6
-    avg_launch_s = float(np.mean(kern_ms)) / 1e3
+    avg_launch_s = timed_ms / (args.steps * nb) / 1e3
     bytes_per_launch = float(np.mean(alg))
     achieved = bytes_per_launch / avg_launch_s / 1e9
 
