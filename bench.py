@@ -53,6 +53,10 @@ CONFIGS = {
     "c5": dict(metric="Mreads/s (250 bp) chaos game k=7 tables",
                unit="Mreads/s", reads=25_000_000, batch=5_000_000, L=250, seed=5,
                workload="C5: chaos game k=7 feature tables (200 M x 250 bp over 8 GPUs)"),
+    "c5_valid": dict(metric="Mreads/s (250 bp) chaos game k=7 tables, ONLY_VALID_READS",
+                     unit="Mreads/s", reads=25_000_000, batch=5_000_000, L=250, seed=5,
+                     workload="C5 with a read_status array marking a random 5 % of reads invalid "
+                              "(ONLY_VALID_READS, old/chaos_game.c:188; the CLI's `stats --cg` with a filter)"),
     # routing / geometry cases, not BASELINE configs
     "c2_1024": dict(metric="Mreads/s (150 bp) stats+filter, lmax 1024 (drop-in default)",
                     unit="Mreads/s", reads=100_000_000, batch=10_000_000, L=150, seed=2, lmax=1024,
@@ -142,34 +146,52 @@ def native_oracle():
     import subprocess
     import tempfile
     src = os.path.join(ROOT, "oracle", "hpgq_oracle.c")
-    out = os.path.join(tempfile.gettempdir(), f"hpgq_oracle_native_{os.getpid()}.so")
+    tmp = tempfile.mkdtemp(prefix="hpgq_oracle_")
+    out = os.path.join(tmp, "liboracle_native.so")
     cmd = ["gcc", "-O3", "-march=native", "-std=c99", "-fopenmp", "-fPIC", "-ffp-contract=off",
            "-shared", "-o", out, src]
     try:
         subprocess.run(cmd, check=True, capture_output=True, timeout=120)
-        return out, "gcc -O3 -march=native -fopenmp (built on this host)"
+        lib = C.CDLL(out)
+        build = "gcc -O3 -march=native -fopenmp (built on this host)"
     except (OSError, subprocess.SubprocessError):
-        return os.path.join(ROOT, "oracle", "liboracle.so"), "gcc -O3 -march=x86-64-v2 -fopenmp (portable)"
+        lib = C.CDLL(os.path.join(ROOT, "oracle", "liboracle.so"))
+        build = "gcc -O3 -march=x86-64-v2 -fopenmp (portable)"
+    # the loaded library stays mapped; its file and directory can go
+    for f in (out, tmp):
+        try:
+            os.remove(f) if f == out else os.rmdir(f)
+        except OSError:
+            pass
+    return lib, build
+
+
+def omp_threads(default):
+    """This job's CPU share from OMP_NUM_THREADS (its first field: nested
+    OpenMP lists such as '16,1' are valid), else `default`."""
+    try:
+        return max(1, int(os.environ.get("OMP_NUM_THREADS", "").split(",")[0]))
+    except ValueError:
+        return default
 
 
 def cpu_baseline(args, params):
-    so, build = native_oracle()
-    lib = C.CDLL(so)
+    lib, build = native_oracle()
     lib.oracle_run.restype = C.c_int
     lib.oracle_run.argtypes = [C.POINTER(H.Params), C.POINTER(H.Batch), C.POINTER(H.Batch),
                                C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
     lib.oracle_synth.argtypes = [C.POINTER(H.Synth), C.c_int64, C.c_int64, C.c_void_p,
                                  C.c_void_p, C.c_void_p]
     lib.oracle_cgr_fill_batches.restype = C.c_int
-    lib.oracle_cgr_fill_batches.argtypes = [C.c_int, C.c_int, C.POINTER(H.Batch), C.c_int,
-                                            C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+    lib.oracle_cgr_fill_batches.argtypes = [C.c_int, C.c_int, C.POINTER(H.Batch), C.c_void_p, C.c_int,
+                                            C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
     ncores = len(os.sched_getaffinity(0))
     # the GPU box gives one GPU's job a share of the host's cores and says so in
     # OMP_NUM_THREADS (16 there); sched_getaffinity shows the whole host
-    share = int(os.environ.get("OMP_NUM_THREADS") or ncores)
-    threads = max(1, min(share, ncores))
+    threads = max(1, min(omp_threads(ncores), ncores))
     L = args.read_length
-    n = 2_000_000 if args.config != "c5" else 400_000
+    cgr = args.config in ("c5", "c5_valid")
+    n = 400_000 if cgr else 2_000_000
     mates = 2 if args.config == "c3" else 1
     bufs = []
     for m in range(mates):
@@ -181,7 +203,7 @@ def cpu_baseline(args, params):
         bufs.append((seq, qual, idx))
     bs = [H.Batch(n, sq.ctypes.data, ql.ctypes.data, ix.ctypes.data) for sq, ql, ix in bufs]
     nt = [threads]
-    if args.config == "c5":
+    if cgr:
         # independent fill calls (one per batch of 20 k reads) spread over the threads
         nb = 20
         per = n // nb
@@ -192,9 +214,14 @@ def cpu_baseline(args, params):
         ts = np.zeros(128 * 128, np.uint32)
         tq = np.zeros(128 * 128, np.uint32)
         wc = np.zeros(1, np.uint32)
-        run = lambda p=None: lib.oracle_cgr_fill_batches(7, 33, sub, nb, ts.ctypes.data,  # noqa: E731
-                                                         tq.ctypes.data, wc.ctypes.data, nt[0])
-        what = f"oracle_cgr_fill_batches (old/chaos_game.c restated), {nb} fill calls"
+        valid = args.config == "c5_valid"
+        status = read_status(n, args.seed)
+        sp = (C.c_void_p * nb)(*[status.ctypes.data + i * per for i in range(nb)])
+        run = lambda p=None: lib.oracle_cgr_fill_batches(  # noqa: E731
+            7, 33, sub, sp if valid else None, 1 if valid else 0, nb, ts.ctypes.data,
+            tq.ctypes.data, wc.ctypes.data, nt[0])
+        what = (f"oracle_cgr_fill_batches (old/chaos_game.c restated), {nb} fill calls"
+                + (", ONLY_VALID_READS with the same 5 % invalid status" if valid else ""))
     else:
         mask = np.zeros(n, np.uint8)
         trim = np.zeros(n * mates, np.uint32)
@@ -237,6 +264,18 @@ def cpu_baseline(args, params):
                      f"{el:.1f} s; {what}, {threads} OpenMP threads (this GPU's CPU share; "
                      f"{ncores} visible); value_1thread: one pass on 1 thread ({el1:.1f} s){c1}")
     return out
+
+
+def read_status(n, seed, first=0):
+    """c5_valid's read_status[]: 1 (VALID_READ) except a random 5 % (0),
+    counter-based per read index so any shard regenerates its slice."""
+    i = np.arange(first, first + n, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        x = (i + np.uint64(seed) * np.uint64(0x9E3779B97F4A7C15)) * np.uint64(0xBF58476D1CE4E5B9)
+        x ^= x >> np.uint64(31)
+        x *= np.uint64(0x94D049BB133111EB)
+        x ^= x >> np.uint64(29)
+    return ((x % np.uint64(100)) >= np.uint64(5)).astype(np.uint8)
 
 
 # ---- resident synthetic shard ----------------------------------------------
@@ -283,7 +322,8 @@ def main():
     dev = torch.device("cuda", local)
 
     L = args.read_length
-    cgr = args.config == "c5"
+    cgr = args.config in ("c5", "c5_valid")
+    valid = args.config == "c5_valid"
     params = params_for(args.config, L)
     mates = 2 if params.paired else 1
     batches = make_batches(args, rank, dev, mates)
@@ -291,11 +331,19 @@ def main():
     d_trim = torch.empty(args.reads * mates, dtype=torch.int32, device=dev)
     offs = np.cumsum([0] + [b[0] for b in batches])
 
+    statuses = []
     if cgr:
         eng = H.ChaosGame(7, 33, device=local)
-        kernel_name = "hpgq::cgr::stream::cgr_stream_kernel<7> (+span_first)"
+        kernel_name = f"hpgq::cgr::stream::cgr_stream_kernel<7, {'true' if valid else 'false'}> (+span_first)"
         # algorithmic bytes per read: seq + quality + offset (tables stay in LDS)
-        alg = [nb for (_n, _m, nb) in batches]
+        # (+ 1 status byte per read; the skipped reads' bytes are streamed too)
+        alg = [nb + (n if valid else 0) for (n, _m, nb) in batches]
+        if valid:
+            lo = 0
+            for (n, _m, _nb) in batches:
+                statuses.append(torch.from_numpy(read_status(n, args.seed, rank * args.reads + lo)).to(dev))
+                lo += n
+            torch.cuda.synchronize()
     else:
         eng = H.Engine(params, device=local)
         kernel_name = eng.kernel_name
@@ -327,7 +375,10 @@ def main():
             if s is not None and i == 0 and (per_step or s == 0):
                 ev[s][0].record(ext)
             if cgr:
-                eng.fill_device(b[0])
+                if valid:
+                    eng.fill_device(b[0], statuses[i].data_ptr(), H.CGR_ONLY_VALID_READS)
+                else:
+                    eng.fill_device(b[0])
             else:
                 eng.run_device(b[0], b[1] if mates == 2 else None,
                                d_mask.data_ptr() + int(offs[i]),

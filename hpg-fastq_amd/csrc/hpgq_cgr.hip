@@ -189,9 +189,6 @@ __device__ __forceinline__ void step(uint32_t fl, uint32_t qb, uint32_t qold, St
     if (UNCOND) {
       const uint32_t cell = word ? (uint32_t)(cx * dim + cy) : (uint32_t)(dim * dim);
       const uint64_t inc = ((uint64_t)acc << 32) | 1u;
-#if HPGQ_CGR_ABL == 1   // timing probe only: the table add skipped
-      if (__builtin_expect(sub == 0xDEADBEEFu, 0))
-#endif
       atomicAdd(reinterpret_cast<unsigned long long *>(ts) + cell, (unsigned long long)inc);
     } else if (word) {
       const int cell = cx * dim + cy;
@@ -426,9 +423,6 @@ __device__ State guess_entry(const Args &A, const Src &S, const uint8_t *cls, in
   constexpr double half = (double)(1 << K) * 0.5;   // :107-108
   State st = {half, half};
   if (r == 0) return st;
-#if HPGQ_CGR_ABL == 2   // timing probe only: no context replay
-  if (A.num_reads > 0) return st;
-#endif
   if (A.mode != HPGQ_CGR_ONLY_VALID_READS) return warm_contiguous<K>(A, S, cls, r);
   // common case: the previous read alone holds kWarm bytes
   const int ap = A.idx[r - 1], ar = A.idx[r];
@@ -637,16 +631,22 @@ namespace hpgq {
 namespace cgr {
 namespace stream {
 
-static const void *stream_for(int k) {
+template <bool VALID>
+static const void *stream_for_mode(int k) {
   switch (k) {
-    case 1: return (const void *)cgr_stream_kernel<1>;
-    case 2: return (const void *)cgr_stream_kernel<2>;
-    case 3: return (const void *)cgr_stream_kernel<3>;
-    case 4: return (const void *)cgr_stream_kernel<4>;
-    case 5: return (const void *)cgr_stream_kernel<5>;
-    case 6: return (const void *)cgr_stream_kernel<6>;
-    default: return (const void *)cgr_stream_kernel<7>;
+    case 1: return (const void *)cgr_stream_kernel<1, VALID>;
+    case 2: return (const void *)cgr_stream_kernel<2, VALID>;
+    case 3: return (const void *)cgr_stream_kernel<3, VALID>;
+    case 4: return (const void *)cgr_stream_kernel<4, VALID>;
+    case 5: return (const void *)cgr_stream_kernel<5, VALID>;
+    case 6: return (const void *)cgr_stream_kernel<6, VALID>;
+    default: return (const void *)cgr_stream_kernel<7, VALID>;
   }
+}
+
+// valid: the ONLY_VALID_READS instance (reads with status != 1 skipped, :188)
+static const void *stream_for(int k, bool valid) {
+  return valid ? stream_for_mode<true>(k) : stream_for_mode<false>(k);
 }
 
 }  // namespace stream
@@ -665,18 +665,23 @@ struct hpgq_cgr {
   size_t lds = 0;
   int grid = 0;
   int64_t last_replays = 0;
-  // stream path (k <= 7, all reads; hpgq_cgr_stream.h).  Each streamed fill
+  // stream path (k <= 7, either mode; hpgq_cgr_stream.h).  Each streamed fill
   // gets a gate/done slot; the exact simulation of a fill whose gate is set
-  // runs at the next sync (the batch must stay valid until then, as for any
-  // asynchronous fill).
+  // runs at the next sync (the batch and its status array must stay valid
+  // until then, as for any asynchronous fill).
   int path = HPGQ_CGR_PATH_AUTO;
   int32_t *d_span_first = nullptr;
   unsigned long long *d_scratch = nullptr;
   uint32_t *d_slots = nullptr;            // [kSlots][2]: gate, done
-  std::vector<hpgq_batch_t> pending;      // streamed fills not synced yet (slot = index)
+  struct Fill {
+    hpgq_batch_t b;
+    const uint8_t *status;
+    int mode;
+  };
+  std::vector<Fill> pending;              // streamed fills not synced yet (slot = index)
   bool ran_exact = false;                 // an exact simulation ran since the last sync
   int last_exact = 0;
-  int s_grid = 0;
+  int s_grid[2] = {0, 0};   // stream grid: all reads, ONLY_VALID_READS
   // RCCL (hpgq_cgr_allreduce): [table_seq | table_q | word count] u32, packed
   // and summed out of place; reads return the sum until the next fill / reset
   ncclComm_t comm = nullptr;
@@ -779,9 +784,11 @@ int hpgq_cgr_open(hpgq_cgr_t **cg, int device, int k, int base_quality) {
     HPGQ_HIP_TRY(hipMemsetAsync(c->d_scratch, 0, cells * 8, c->stream));
     HPGQ_HIP_TRY(hipMalloc(&c->d_slots, S::kSlots * 2 * sizeof(uint32_t)));
     HPGQ_HIP_TRY(hipMemsetAsync(c->d_slots, 0, S::kSlots * 2 * sizeof(uint32_t), c->stream));
-    int spc = 0;
-    HPGQ_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&spc, S::stream_for(k), S::kWG, 0));
-    c->s_grid = std::max(1, spc) * cus;
+    for (int v = 0; v < 2; ++v) {
+      int spc = 0;
+      HPGQ_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&spc, S::stream_for(k, v != 0), S::kWG, 0));
+      c->s_grid[v] = std::max(1, spc) * cus;
+    }
     c->pending.reserve(S::kSlots);
   }
   *cg = c;
@@ -817,8 +824,9 @@ int hpgq_cgr_fill_device(hpgq_cgr_t *c, const hpgq_batch_t *b, const uint8_t *st
   if (!b->seq || !b->quality || !b->data_indices) return HPGQ_E_INVALID;
   HPGQ_HIP_TRY(hipSetDevice(c->device));
   c->reduced = false;
-  const bool streamed = c->path == HPGQ_CGR_PATH_AUTO && mode == HPGQ_CGR_ALL_READS &&
-                        c->k <= hpgq::cgr::stream::kMaxK;
+  const bool valid = mode == HPGQ_CGR_ONLY_VALID_READS;
+  if (valid && !status) return HPGQ_OK;   // no status array: every read is skipped (:188)
+  const bool streamed = c->path == HPGQ_CGR_PATH_AUTO && c->k <= hpgq::cgr::stream::kMaxK;
   if (!streamed) return cgr_exact(c, b, status, mode);
   namespace S = hpgq::cgr::stream;
   if ((int)c->pending.size() == S::kSlots) {   // out of slots: settle the ones in flight
@@ -830,6 +838,7 @@ int hpgq_cgr_fill_device(hpgq_cgr_t *c, const hpgq_batch_t *b, const uint8_t *st
   SA.seq = b->seq;
   SA.qual = b->quality;
   SA.idx = b->data_indices;
+  SA.status = valid ? status : nullptr;
   SA.num_reads = b->num_reads;
   SA.base_quality = c->base_quality;
   SA.span_first = c->d_span_first;
@@ -843,8 +852,8 @@ int hpgq_cgr_fill_device(hpgq_cgr_t *c, const hpgq_batch_t *b, const uint8_t *st
   HPGQ_HIP_TRY(hipLaunchKernel((const void *)S::span_first_kernel,
                                dim3((unsigned)std::min<int64_t>((b->num_reads + 1 + 255) / 256, S::kSpanFirstGrid)),
                                dim3(256), sargs, 0, c->stream));
-  HPGQ_HIP_TRY(hipLaunchKernel(S::stream_for(c->k), dim3(c->s_grid), dim3(S::kWG), sargs, 0, c->stream));
-  c->pending.push_back(*b);
+  HPGQ_HIP_TRY(hipLaunchKernel(S::stream_for(c->k, valid), dim3(c->s_grid[valid ? 1 : 0]), dim3(S::kWG), sargs, 0, c->stream));
+  c->pending.push_back(hpgq_cgr::Fill{*b, status, mode});
   return HPGQ_OK;
 }
 
@@ -856,11 +865,11 @@ int hpgq_cgr_sync(hpgq_cgr_t *c) {
     // streamed fills whose gate is set: the exact simulation, in fill order
     std::vector<uint32_t> slots(2 * c->pending.size());
     HPGQ_HIP_TRY(hipMemcpy(slots.data(), c->d_slots, slots.size() * 4, hipMemcpyDeviceToHost));
-    std::vector<hpgq_batch_t> todo;
+    std::vector<hpgq_cgr::Fill> todo;
     todo.swap(c->pending);
     for (size_t i = 0; i < todo.size(); ++i)
       if (slots[2 * i] & hpgq::cgr::stream::GATE_EXACT) {
-        int rc = cgr_exact(c, &todo[i], nullptr, HPGQ_CGR_ALL_READS);
+        int rc = cgr_exact(c, &todo[i].b, todo[i].status, todo[i].mode);
         if (rc) return rc;
       }
     HPGQ_HIP_TRY(hipStreamSynchronize(c->stream));

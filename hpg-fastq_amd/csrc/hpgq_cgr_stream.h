@@ -35,6 +35,18 @@
 // never violate this; a batch that does (poly-A/T/G runs, lowercase, IUPAC)
 // sets the gate and the exact kernels redo the whole call.
 //
+// ONLY_VALID_READS (VALID): a read whose status is not VALID_READ is skipped
+// before any state update (:188), so f passes through it unchanged and it
+// emits no word: its bytes act exactly like 'N' bytes (no move, no word) and
+// its quality bytes like zeros, and that is how the kernel treats them.  Read
+// starts whose validity differs from the read before are scattered into a
+// second per-wave bitmap (XOR, so empty reads at one offset cancel); a
+// byte's "skipped" bit is the tile's entry state XOR a prefix parity of those
+// toggles (within the lane by shifts, across lanes by one ballot), and a tile
+// holding skipped bytes masks them before anything else looks at its bytes.
+// The run bound and the exact run scan then see the moves of the valid reads
+// only, across skipped reads, as the reference's carried f does.
+//
 // Layout: the bytes [idx[0], idx[n]) are cut into spans of kSpan bytes; wave
 // g takes spans g, g + W, ... (W waves in the grid) as one stream of 2 KB
 // tiles, a lane 32 contiguous bytes of seq and of quality per tile (16-byte
@@ -49,10 +61,12 @@
 // << 32, one ds_add_u64 per byte; a byte that ends no word adds to its lane's
 // spare cell), flushed to a global u64 scratch table; the last workgroup to
 // finish moves it into the reference layout (or discards it when the gate is
-// set).  A run of >= kRun (>= 41) D-moves covers a whole aligned 16-byte
-// chunk with no Z on that axis; a tile whose chunks all hold a Z on both axes
-// can only hold runs of <= 30, so only tiles with a Z-free chunk (or entered
-// with a long open run) are scanned exactly, lane by lane.
+// set).  A run of >= kRun (>= 41) D-moves spans at least three aligned 16-byte
+// chunks, and a chunk wholly inside it holds no Z on that axis; so only tiles
+// with a Z-free chunk (VALID: a Z-free chunk that holds a D move -- a run's
+// interior chunks hold >= 9 of its D moves, so one of them does, while wholly
+// skipped stretches do not trigger) or entered with a long open run are
+// scanned exactly, lane by lane.
 #pragma once
 
 namespace hpgq {
@@ -61,26 +75,12 @@ namespace stream {
 
 constexpr int kWaves = 16;
 constexpr int kWG = kWaves * 64;
-#ifndef HPGQ_CGR_LANE_BYTES
-#define HPGQ_CGR_LANE_BYTES 32
-#endif
-constexpr int kLaneBytes = HPGQ_CGR_LANE_BYTES;   // 32 (the packed code stream assumes it)
+constexpr int kLaneBytes = 32;               // the packed code stream assumes it
 constexpr int kNdw = kLaneBytes / 4;
 constexpr int kTile = 64 * kLaneBytes;       // bytes per wave tile (2 KB)
-#ifndef HPGQ_CGR_SPAN_LOG
-#define HPGQ_CGR_SPAN_LOG 14
-#endif
-constexpr int kSpanLog = HPGQ_CGR_SPAN_LOG;
+constexpr int kSpanLog = 14;
 constexpr int kSpan = 1 << kSpanLog;         // bytes per span (16 KB, 8 tiles)
-#ifndef HPGQ_CGR_XCHG
-#define HPGQ_CGR_XCHG 0   // 1: read and clear by one exchange (measured ~1% slower)
-#endif
-#ifndef HPGQ_SPAN_FIRST_GRID
-#define HPGQ_SPAN_FIRST_GRID 2048
-#endif
-#ifndef HPGQ_CGR_CHAINS
-#define HPGQ_CGR_CHAINS 1   // independent add chains per lane and tile (2: measured no faster)
-#endif
+constexpr int kSpanFirstGrid = 2048;
 constexpr int kMaxK = 7;                     // 4^7 u64 cells = 128 KB of LDS
 constexpr int64_t kMaxSpans = ((int64_t)1 << 31) / kSpan + 2;
 constexpr int kSlots = 256;                  // fills in flight between two syncs
@@ -93,10 +93,13 @@ constexpr uint32_t kCdHi = 0x02030003u;   //                    T 3, G 2, N 3 (N
                                           // as 3 it has no Z bit in ~code below)
 constexpr uint32_t kV1Lo = 0x01000100u;   // 1 for A/C/G/T, 0 for N
 constexpr uint32_t kV1Hi = 0x01000001u;
+constexpr uint32_t kDLo = 0x00000100u;    // D moves x | y << 1: A 1, C 0
+constexpr uint32_t kDHi = 0x02000003u;    //                     T 3, G 2, N 0
 
 struct SArgs {
   const char *seq, *qual;
   const int32_t *idx;
+  const uint8_t *status;            // VALID: read_status[] (1 = VALID_READ)
   int64_t num_reads;
   uint32_t base_quality;
   int32_t *span_first;              // [kMaxSpans] first read with idx[r] >= span start - 32
@@ -117,7 +120,6 @@ __device__ __forceinline__ int64_t nspans(int32_t a0, int32_t b1) {
 // also clears this fill's gate and done slots
 // (grid-stride: a few thousand workgroups walk the whole idx array; one
 // thread per read made the launch dispatch-bound at ~17 us per 5 M reads)
-constexpr int kSpanFirstGrid = HPGQ_SPAN_FIRST_GRID;
 __global__ void __launch_bounds__(256) span_first_kernel(SArgs A) {
   const int32_t b0 = A.idx[0], b1 = A.idx[A.num_reads];
   const int32_t a0 = b0 & ~15;
@@ -136,16 +138,11 @@ __global__ void __launch_bounds__(256) span_first_kernel(SArgs A) {
   }
 }
 
-// a lane's word of a start bitmap, cleared for its next use in the same LDS op
-// (ds_wrxchg_rtn_b32: one LDS instruction instead of a read and a write)
+// a lane's word of a bitmap, cleared for its next use
 __device__ __forceinline__ uint32_t take_bits(uint32_t *p) {
-#if HPGQ_CGR_XCHG
-  return atomicExch(p, 0u);
-#else
   const uint32_t v = *p;
   *p = 0u;
   return v;
-#endif
 }
 
 __device__ __forceinline__ uint32_t dpp_ror1(uint32_t v) {   // lane l <- lane l-1, lane 0 <- lane 63
@@ -162,13 +159,15 @@ struct Cls {
   uint32_t p0, p1;     // the 32 codes packed, byte j at bits 2j of the 64-bit p1:p0
   uint32_t v;          // bit j: byte j is A/C/G/T
   uint32_t zlo, zhi;   // OR of per-byte Z bits (bit0 x, bit1 y) over the first / last 16 bytes
+  uint32_t dlo, dhi;   // VALID: the same for D moves
   uint32_t bad;        // nonzero: a byte that is not exactly A/C/G/T/N
 };
 
+template <bool VALID>
 __device__ __forceinline__ Cls classify(const uint32_t s[kNdw]) {
   static_assert(kNdw == 8, "the packed code stream assumes 32 bytes per lane");
   Cls c;
-  uint32_t bad = 0, zl = 0, zh = 0, vp[kNdw / 2], g[kNdw];
+  uint32_t bad = 0, zl = 0, zh = 0, dl = 0, dh = 0, vp[kNdw / 2], g[kNdw];
 #pragma unroll
   for (int d = 0; d < kNdw; ++d) {
     const uint32_t code = s[d] & 0x07070707u;
@@ -179,6 +178,11 @@ __device__ __forceinline__ Cls classify(const uint32_t s[kNdw]) {
     // Z bits: a Z move on x is x = 0 (C/G), on y is y = 0 (A/C): ~code & 3
     if (d < 4) zl = __builtin_amdgcn_bitop3_b32(zl, c.cd[d], 0x03030303u, 0xF2);   // zl | (~cd & 3s)
     if (d >= kNdw - 4) zh = __builtin_amdgcn_bitop3_b32(zh, c.cd[d], 0x03030303u, 0xF2);
+    if (VALID) {
+      const uint32_t dm = __builtin_amdgcn_perm(kDHi, kDLo, code);
+      if (d < 4) dl |= dm;
+      else dh |= dm;
+    }
     // the V bit of byte j to bit j: byte weights 1,2,4,8 (<< 4 for odd dwords) by v_dot4
     const uint32_t v1 = __builtin_amdgcn_perm(kV1Hi, kV1Lo, code);
     vp[d >> 1] = (d & 1) ? __builtin_amdgcn_udot4(v1, 0x80402010u, vp[d >> 1], false)
@@ -191,6 +195,8 @@ __device__ __forceinline__ Cls classify(const uint32_t s[kNdw]) {
   for (int d = 0; d < kNdw / 2; ++d) c.v |= vp[d] << (8 * d);
   c.zlo = zl;
   c.zhi = zh;
+  c.dlo = dl;
+  c.dhi = dh;
   c.bad = bad;
   return c;
 }
@@ -241,6 +247,13 @@ __device__ uint32_t scan_tile(const Cls &c, uint32_t ein, uint32_t run_max, bool
   return run;
 }
 
+__device__ __forceinline__ bool moving_byte(uint8_t ch) { return ch == 'A' || ch == 'C' || ch == 'G' || ch == 'T'; }
+
+template <int AX>
+__device__ __forceinline__ bool d_move(uint8_t ch) {
+  return AX == 0 ? (ch == 'A' || ch == 'T') : (ch == 'G' || ch == 'T');
+}
+
 // the run open at byte `at` on axis AX (capped at run_max), walking back from
 // it; rare: only for tiles that need the exact scan
 template <int AX>
@@ -248,48 +261,81 @@ __device__ uint32_t run_before(const SArgs &A, int32_t b0, int32_t at, uint32_t 
   uint32_t run = 0;
   for (int32_t p = at - 1; p >= b0 && run < run_max; --p) {
     const uint8_t ch = (uint8_t)A.seq[p];
-    const bool mv = ch == 'A' || ch == 'C' || ch == 'G' || ch == 'T';
-    if (!mv) continue;   // N (other bytes set the gate in their own tile)
-    const bool d = AX == 0 ? (ch == 'A' || ch == 'T') : (ch == 'G' || ch == 'T');
-    if (!d) break;
+    if (!moving_byte(ch)) continue;   // N (other bytes set the gate in their own tile)
+    if (!d_move<AX>(ch)) break;
     ++run;
+  }
+  return run;
+}
+
+// VALID: the same, skipping the reads that are not valid; t is the read that
+// holds byte at - 1 (-1: none)
+template <int AX>
+__device__ uint32_t run_before_valid(const SArgs &A, int32_t at, int64_t t, uint32_t run_max) {
+  uint32_t run = 0;
+  int32_t p = at - 1;
+  for (; t >= 0 && run < run_max; --t) {
+    const int32_t lo = A.idx[t];
+    if (A.status[t] == 1) {
+      for (; p >= lo && run < run_max; --p) {
+        const uint8_t ch = (uint8_t)A.seq[p];
+        if (!moving_byte(ch)) continue;
+        if (!d_move<AX>(ch)) return run;
+        ++run;
+      }
+    }
+    p = lo - 1;
   }
   return run;
 }
 
 // the idx window a wave walks: lane j holds idx[r + j] (0x7FFFFFFF past the
 // end); the load is unconditional (clamped index) so that no branch splits the
-// compiler's view of the loads in flight
-__device__ __forceinline__ int32_t idx_window(const SArgs &A, int64_t r, int lane) {
-  const int64_t j = r + lane;
-  const int32_t v = A.idx[j <= A.num_reads ? j : A.num_reads];
-  return j <= A.num_reads ? v : 0x7FFFFFFF;
+// compiler's view of the loads in flight.  VALID: tg = 1 when read r + j's
+// validity differs from read r + j - 1's (the state before read 0 is valid).
+template <bool VALID>
+__device__ __forceinline__ int32_t idx_window(const SArgs &A, int64_t r, int lane, uint32_t &tg) {
+  const int64_t j = r + lane, n = A.num_reads;
+  const int32_t v = A.idx[j <= n ? j : n];
+  if (VALID) {
+    const int64_t ja = j < n ? j : n - 1, jb = j >= 1 && j <= n ? j - 1 : 0;
+    const bool va = A.status[ja] == 1, vb = j == 0 || A.status[jb] == 1;
+    tg = j < n && va != vb ? 1u : 0u;
+  }
+  return j <= n ? v : 0x7FFFFFFF;
 }
 
 // read starts in [base, limit) (limit - base <= 64 * kLaneBytes): bits into
-// the wave's LDS bitmap sc[64], advancing the cursor r past them.  iw is the
-// window at r (loaded ahead by the caller); it comes back as the window at
-// the new r, its load in flight.  hop: the tile is its span's last, so the
-// cursor moves on to rn (the next span's first read) instead.
-__device__ __forceinline__ void scatter_starts(const SArgs &A, uint32_t *sc, int64_t &r, int32_t &iw,
-                                               int32_t base, int32_t limit, int lane, bool hop = false,
+// the wave's LDS bitmap sc[64] (TOG: the validity toggles into tc[64]),
+// advancing the cursor r past them.  iw / itg are the window at r (loaded
+// ahead by the caller); they come back as the window at the new r, its load
+// in flight.  hop: the tile is its span's last, so the cursor moves on to rn
+// (the next span's first read) instead.
+template <bool VALID, bool TOG>
+__device__ __forceinline__ void scatter_starts(const SArgs &A, uint32_t *sc, uint32_t *tc, int64_t &r, int32_t &iw,
+                                               uint32_t &itg, int32_t base, int32_t limit, int lane, bool hop = false,
                                                int64_t rn = 0) {
-  auto put = [&](int32_t x) {
+  auto put = [&](int32_t x, uint32_t tg) {
     const bool in = x < limit;
     const uint32_t o = (uint32_t)(x - base);
-    if (in && o < 64u * kLaneBytes) atomicOr(&sc[o / kLaneBytes], 1u << (o % kLaneBytes));   // o in range unless idx is unsorted
+    if (in && o < 64u * kLaneBytes) {   // o in range unless idx is unsorted
+      atomicOr(&sc[o / kLaneBytes], 1u << (o % kLaneBytes));
+      if (TOG && tg) atomicXor(&tc[o / kLaneBytes], 1u << (o % kLaneBytes));
+    }
     const int c = __popcll(__ballot(in));
     r += c;
     return c;
   };
-  if (__builtin_expect(put(iw) == 64, 0)) {   // rare: more than 64 starts in the tile
+  if (__builtin_expect(put(iw, itg) == 64, 0)) {   // rare: more than 64 starts in the tile
     int c;
     do {
-      c = put(idx_window(A, r, lane));
+      uint32_t tg = 0;
+      const int32_t x = idx_window<VALID>(A, r, lane, tg);
+      c = put(x, tg);
     } while (c == 64);
   }
   if (hop) r = rn;
-  iw = idx_window(A, r, lane);
+  iw = idx_window<VALID>(A, r, lane, itg);
 }
 
 // a lane's bytes at o (o >= 0) from a buffer descriptor; bytes past the end read 0
@@ -313,7 +359,25 @@ __device__ __forceinline__ void mask_range(int32_t o, int32_t lo, int32_t hi, ui
   }
 }
 
-template <int K>
+// VALID: bytes whose bit is set in skip (bit j = byte j) -> 'N' and quality 0
+__device__ __forceinline__ void mask_skipped(uint32_t skip, uint32_t sw[kNdw], uint32_t qw[kNdw]) {
+#pragma unroll
+  for (int d = 0; d < kNdw; ++d) {
+    // 4 bits -> 4 byte masks (the products land on distinct bits: no carries)
+    const uint32_t bm = ((((skip >> (4 * d)) & 0xFu) * 0x00204081u) & 0x01010101u) * 0xFFu;
+    sw[d] = __builtin_amdgcn_bitop3_b32(sw[d], bm, 0x4E4E4E4Eu, 0xB8);   // bm ? 'N' : sw
+    qw[d] &= ~bm;
+  }
+}
+
+// the chunk-and-axis pairs (4 bits: chunk 0 x, y, chunk 1 x, y) of a lane
+// whose bytes hold a bit of u (per byte bits 0-1, lo: bytes 0..15, hi: 16..31)
+__device__ __forceinline__ uint32_t chunk_bits(uint32_t lo, uint32_t hi) {
+  const uint32_t u = lo | (hi << 2);
+  return (u | (u >> 8) | (u >> 16) | (u >> 24)) & 0xFu;
+}
+
+template <int K, bool VALID>
 __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
   static_assert(K >= 1 && K <= kMaxK, "LDS table");
   constexpr int cells = 1 << (2 * K);
@@ -321,17 +385,19 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
   constexpr uint32_t SPARE = (uint32_t)cells << 3;      // the spare cells (one per lane: bytes
                                                         // that end no word do not collide)
   constexpr uint32_t kRun = 48 - K;
+  // per wave: start bitmaps of two tiles (this, next) + context; VALID: the
+  // validity toggles of the two tiles
+  constexpr int kBm = VALID ? 5 : 3;
   __shared__ unsigned long long tab[cells + 64];
-  __shared__ uint32_t scb[kWaves * 3 * 64];   // per wave: two start bitmaps (this tile, next tile) + context
+  __shared__ uint32_t scb[kWaves * kBm * 64];
   __shared__ uint32_t last;
   for (int i = threadIdx.x; i < cells + 64; i += kWG) tab[i] = 0ull;
   const int lane = threadIdx.x & 63;
   const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: spans, tiles and buffer descriptors stay scalar
   const uint32_t spare = SPARE + 8u * (uint32_t)lane;
-  uint32_t *sc = scb + 192 * wid;
-  sc[lane] = 0u;
-  sc[64 + lane] = 0u;
-  sc[128 + lane] = 0u;
+  uint32_t *sc = scb + kBm * 64 * wid;
+#pragma unroll
+  for (int b = 0; b < kBm; ++b) sc[64 * b + lane] = 0u;
   __syncthreads();
 
   const int32_t b0 = __builtin_amdgcn_readfirstlane(A.idx[0]);
@@ -340,9 +406,6 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
   const int64_t ns = nspans(a0, b1);
   const int64_t gw = (int64_t)blockIdx.x * kWaves + wid, nwav = (int64_t)gridDim.x * kWaves;
   bool risky = false;
-#if HPGQ_CGR_ABL == 6
-  uint32_t sink = 0;
-#endif
 
   // one descriptor pair per call: offsets past b1 + slack read zeros without
   // memory traffic (the context loads of tiles that enter no span, the
@@ -357,6 +420,7 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
   const __attribute__((address_space(4))) int32_t *sfirst =
       (const __attribute__((address_space(4))) int32_t *)A.span_first;
   uint32_t *scx = sc + 128;   // the context bitmap: starts in the 32 bytes before a span
+  uint32_t *tcb = sc + 192;   // VALID: the toggle bitmaps of the two tiles
 
   // The wave's spans s = gw, gw + nwav, ... form one tile stream: the next
   // tile's bytes, read-start bits and (entering a span) context are fetched
@@ -374,12 +438,14 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
     uint32_t einx = 15, einy = 15;
     bool eknown = false;
     // span entry: the 16 bytes before t0 (all 'N' before the batch) and the
-    // read starts among the 32 before it
-    auto enter = [&](const uint32_t (&cs)[4], const uint32_t (&cq)[2], const uint32_t ps, const int32_t t0) {
+    // read starts among the 32 before it; VALID: rv = the read holding byte
+    // t0 - 1 (-1: none), the entry state skip_in (1: that read is skipped)
+    auto enter = [&](const uint32_t (&cs)[4], const uint32_t (&cq)[2], const uint32_t ps, const int32_t t0,
+                     const int64_t rv, uint32_t &skip_in) {
       uint32_t sw[kNdw];
 #pragma unroll
       for (int d = 0; d < kNdw; ++d) sw[d] = d < kNdw - 4 ? 0x4E4E4E4Eu : cs[d - (kNdw - 4)];
-      const Cls c = classify(sw);
+      const Cls c = classify<false>(sw);
       pp1 = __builtin_amdgcn_readfirstlane(c.p1);
       pq6 = __builtin_amdgcn_readfirstlane(cq[0]);
       pq7 = __builtin_amdgcn_readfirstlane(cq[1]);
@@ -387,14 +453,36 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
       pS = ps;
       einx = einy = 15;
       eknown = false;
-      if (!(c.zhi & 0x01010101u) || !(c.zhi & 0x02020202u)) {
-        einx = run_before<0>(A, b0, t0, kRun);
-        einy = run_before<1>(A, b0, t0, kRun);
+      if (!VALID) {
+        if (!(c.zhi & 0x01010101u) || !(c.zhi & 0x02020202u)) {
+          einx = run_before<0>(A, b0, t0, kRun);
+          einy = run_before<1>(A, b0, t0, kRun);
+          eknown = true;
+        }
+        return;
+      }
+      // VALID: the bound of 15 holds when read rv is valid and its bytes among
+      // the 16 hold a Z on both axes (they are the bytes after its start)
+      const bool vrd = rv >= 0 && __builtin_amdgcn_readfirstlane(A.status[rv]) == 1;
+      skip_in = rv >= 0 && !vrd ? 1u : 0u;
+      const uint32_t st = ps >> 16;   // starts among the 16 bytes
+      const uint32_t own = st ? (0xFFFFu << (31 - __builtin_clz(st))) & 0xFFFFu : 0xFFFFu;
+      uint32_t zx = 0, zy = 0;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const uint32_t b = (c.cd[4 + (i >> 2)] >> (8 * (i & 3))) & 3u;
+        const uint32_t vv = (c.v >> (16 + i)) & 1u;
+        zx |= (vv & ~b & 1u) << i;
+        zy |= (vv & (~b >> 1) & 1u) << i;
+      }
+      if (!vrd || !(zx & own) || !(zy & own)) {
+        einx = run_before_valid<0>(A, t0, rv, kRun);
+        einy = run_before_valid<1>(A, t0, rv, kRun);
         eknown = true;
       }
     };
-    auto ctx_starts = [&](int64_t &r, int32_t &iw, const int32_t t0) {
-      scatter_starts(A, scx, r, iw, t0 - kLaneBytes, t0, lane);
+    auto ctx_starts = [&](int64_t &r, int32_t &iw, uint32_t &itg, const int32_t t0) {
+      scatter_starts<VALID, false>(A, scx, nullptr, r, iw, itg, t0 - kLaneBytes, t0, lane);
       __builtin_amdgcn_wave_barrier();
       const uint32_t ps = __builtin_amdgcn_readfirstlane(scx[0]);
       __builtin_amdgcn_wave_barrier();
@@ -403,36 +491,49 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
     };
     // mid: runs between the tile's set-up and its table adds (the next tile's
     // start scatter: its LDS read then waits behind the previous tile's adds,
-    // long drained, rather than behind this one's)
+    // long drained, rather than behind this one's).  VALID: sk = the skip
+    // state at the tile start, tg = the lane's toggle word, rf = the first read
+    // starting in the tile; returns the toggles' parity (the next tile's state
+    // is sk ^ parity).
     auto tile = [&](const int32_t t, const int32_t tend, uint32_t (&sw)[kNdw], uint32_t (&qw)[kNdw],
-                    const uint32_t so, auto &&mid) {
+                    const uint32_t so, const uint32_t sk, const uint32_t tg, const int64_t rf, auto &&mid) {
       const int32_t o = t + kLaneBytes * lane;
-#if HPGQ_CGR_ABL == 4   // timing probe only: loads and start bitmaps, no counting
-      {
-        uint32_t x = so;
-#pragma unroll
-        for (int d = 0; d < kNdw; ++d) x ^= sw[d] ^ qw[d];
-        if (__builtin_expect(x == 0x12345678u, 0)) risky = true;
-        mid();
-        return;
-      }
-#endif
       if (t < b0 || t + kTile > tend) mask_range(o, b0, tend, sw, qw);   // edge tiles
-      const Cls c = classify(sw);
+      uint32_t par = 0;
+      if (VALID) {
+        // skip bit of byte j = sk ^ (toggles of the lanes below) ^ (toggles of bytes <= j)
+        uint32_t px = tg;
+        px ^= px << 1;
+        px ^= px << 2;
+        px ^= px << 4;
+        px ^= px << 8;
+        px ^= px << 16;
+        const uint64_t bal = __ballot(__builtin_popcount(tg) & 1);
+        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+        const uint32_t skip = px ^ (0u - ((below ^ sk) & 1u));
+        par = (uint32_t)__popcll(bal) & 1u;
+        if (__ballot(skip != 0u)) mask_skipped(skip, sw, qw);
+      }
+      const Cls c = classify<VALID>(sw);
       uint32_t qor = 0;
 #pragma unroll
       for (int d = 0; d < kNdw; ++d) qor |= qw[d];
       // flags: unsupported bytes
       if (__ballot(c.bad != 0u || (qor & 0x80808080u) != 0u)) risky = true;
-      // runs: a 16-byte chunk without a Z on an axis, or a long run entering the tile
-      // (zlo: x/y Z bits per byte offset over bytes 0..15, zhi over 16..31;
-      // gathered to 4 bits: the chunk-and-axis pairs that hold a Z)
-      const uint32_t zu = c.zlo | (c.zhi << 2);
-      const bool zfree = ((zu | (zu >> 8) | (zu >> 16) | (zu >> 24)) & 0xFu) != 0xFu;
+      // runs: a 16-byte chunk without a Z on an axis (VALID: that holds a D
+      // move there), or a long run entering the tile
+      const uint32_t zc = chunk_bits(c.zlo, c.zhi);
+      const bool zfree = VALID ? (chunk_bits(c.dlo, c.dhi) & ~zc) != 0u : zc != 0xFu;
       if (__builtin_expect(__ballot(zfree) != 0ull || einx > 16 || einy > 16, 0)) {
         if (!eknown) {
-          einx = run_before<0>(A, b0, t, kRun);
-          einy = run_before<1>(A, b0, t, kRun);
+          if (VALID) {
+            einx = run_before_valid<0>(A, t, rf - 1, kRun);
+            einy = run_before_valid<1>(A, t, rf - 1, kRun);
+          } else {
+            einx = run_before<0>(A, b0, t, kRun);
+            einy = run_before<1>(A, b0, t, kRun);
+          }
         }
         einx = scan_tile<0>(c, einx, kRun, risky);
         einy = scan_tile<1>(c, einy, kRun, risky);
@@ -469,7 +570,8 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
       // the word ending at byte j: codes of bytes j-K+1..j (oldest at bits 0-1)
       // from the 96-bit stream np1:p0:p1 (byte i at bit 2(i + 16)), cut out by
       // one v_alignbit at the cell's byte offset (x 8), then masked
-      auto step = [&](const int j, uint32_t &acc) {
+#pragma unroll
+      for (int j = 0; j < kLaneBytes; ++j) {
         const int sh = 2 * j + 29 - 2 * (K - 1);   // stream bit of byte j-K+1, less 3
         const uint32_t win = sh < 32 ? __builtin_amdgcn_alignbit(c.p0, np1, sh)
                            : sh < 64 ? __builtin_amdgcn_alignbit(c.p1, c.p0, sh - 32)
@@ -481,40 +583,11 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
         acc = acc + __builtin_amdgcn_ubfe(qw[j >> 2], 8 * (j & 3), 8) - qold;
         // addr = E bit j ? w : spare (v_bfe_i32 + v_bitop3; left to itself the
         // compiler spends three instructions on it)
-        uint32_t e, addr;
-#if HPGQ_CGR_ABL == 5   // timing probe only: no emission select
-        addr = w;
-        (void)e;
-#else
-        e = (uint32_t)__builtin_amdgcn_sbfe((int)E, j, 1);
-        addr = __builtin_amdgcn_bitop3_b32(e, w, spare, 0xCA);   // e ? w : spare
-#endif
+        const uint32_t e = (uint32_t)__builtin_amdgcn_sbfe((int)E, j, 1);
+        const uint32_t addr = __builtin_amdgcn_bitop3_b32(e, w, spare, 0xCA);   // e ? w : spare
         const unsigned long long inc = ((unsigned long long)acc << 32) | 1ull;
-#if HPGQ_CGR_ABL == 6   // timing probe only: the adds replaced by one VALU op
-        sink += addr ^ (uint32_t)(inc >> 32);
-#else
-#if HPGQ_CGR_ABL == 3   // timing probe only: no table adds
-        if (__builtin_expect(addr == 0xFFFFFFFFu, 0))
-#endif
         atomicAdd(reinterpret_cast<unsigned long long *>(reinterpret_cast<char *>(tab) + addr), inc);
-#endif
-      };
-#if HPGQ_CGR_CHAINS == 2
-      // two independent quality chains (bytes [0,16) and [16,32)) interleaved:
-      // the second's sum starts from bytes 9..15 of this lane
-      constexpr int kH = kLaneBytes / 2;
-      uint32_t acc2 = 0;
-#pragma unroll
-      for (int j = kH - K; j < kH; ++j) acc2 += __builtin_amdgcn_ubfe(qw[j >> 2], 8 * (j & 3), 8);
-#pragma unroll
-      for (int j = 0; j < kH; ++j) {
-        step(j, acc);
-        step(j + kH, acc2);
       }
-#else
-#pragma unroll
-      for (int j = 0; j < kLaneBytes; ++j) step(j, acc);
-#endif
       // carry the last lane to the next tile's lane 0
       // (rotated by one lane: lane 0 holds lane 63's, the "old" operand of
       // the next tile's wave_shr:1)
@@ -523,12 +596,15 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
       pq7 = dpp_ror1(qw[kNdw - 1]);
       pv = dpp_ror1(c.v);
       pS = dpp_ror1(so);
+      return par;
     };
     int32_t tA = a0 + (int32_t)(s << kSpanLog), tB;
     int32_t eA = (int32_t)min((int64_t)tA + kSpan, (int64_t)b1), eB;
     int64_t r = sfirst[s];
     int64_t rn = sfirst[min(s + nwav, ns - 1)];
-    int32_t iw = idx_window(A, r, lane);
+    uint32_t itg = 0;
+    int32_t iw = idx_window<VALID>(A, r, lane, itg);
+    uint32_t skA = 0, skB = 0;   // VALID: skip state at the tile starts
     {
       uint32_t cs[4] = {0x4E4E4E4Eu, 0x4E4E4E4Eu, 0x4E4E4E4Eu, 0x4E4E4E4Eu}, cq[2] = {0u, 0u};
       if (s != 0) {   // spans after the first start >= 16 KB past b0
@@ -537,19 +613,23 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
         cs[0] = a[0]; cs[1] = a[1]; cs[2] = a[2]; cs[3] = a[3];
         cq[0] = q[0]; cq[1] = q[1];
       }
-      enter(cs, cq, ctx_starts(r, iw, tA), tA);
+      const uint32_t ps = ctx_starts(r, iw, itg, tA);
+      enter(cs, cq, ps, tA, r - 1, skA);
     }
-    uint32_t sA[kNdw], qA[kNdw], sB[kNdw], qB[kNdw], soA, soB;
-    scatter_starts(A, sc, r, iw, tA, tA + kTile, lane, tA + kTile >= eA, rn);
+    uint32_t sA[kNdw], qA[kNdw], sB[kNdw], qB[kNdw], soA, soB, tgA = 0, tgB = 0;
+    int64_t rfA = r, rfB = 0;   // VALID: the first read starting in the tile
+    scatter_starts<VALID, VALID>(A, sc, tcb, r, iw, itg, tA, tA + kTile, lane, tA + kTile >= eA, rn);
     soA = take_bits(&sc[lane]);
+    if (VALID) tgA = take_bits(&tcb[lane]);
     load32(rs, (uint32_t)(tA + kLaneBytes * lane), sA);
     load32(rq, (uint32_t)(tA + kLaneBytes * lane), qA);
     // count tile x while fetching tile y (straight-line: the loads are
     // unconditional, so the compiler counts the loads in flight exactly and
     // a tile waits only for its own bytes); false past the wave's last tile
     auto half = [&](const int32_t tx, const int32_t ex, uint32_t (&sx)[kNdw], uint32_t (&qx)[kNdw], const uint32_t sox,
-                    uint32_t *scpx, int32_t &ty, int32_t &ey, uint32_t (&sy)[kNdw], uint32_t (&qy)[kNdw],
-                    uint32_t &soy, uint32_t *scpy) {
+                    const uint32_t skx, const uint32_t tgx, const int64_t rfx, uint32_t *scpy, uint32_t *tcpy,
+                    int32_t &ty, int32_t &ey, uint32_t (&sy)[kNdw], uint32_t (&qy)[kNdw], uint32_t &soy,
+                    uint32_t &sky, uint32_t &tgy, int64_t &rfy) {
       ty = tx + kTile;
       ey = ex;
       bool entering = false, fin = false;
@@ -561,38 +641,37 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
           ey = (int32_t)min((int64_t)ty + kSpan, (int64_t)b1);
           entering = true;
           rn = sfirst[min(s + nwav, ns - 1)];
-          psn = ctx_starts(r, iw, ty);
+          psn = ctx_starts(r, iw, itg, ty);
         } else {
           fin = true;
         }
       }
+      const int64_t rv = r - 1;   // entering: the read holding byte ty - 1
       const v4u a = __builtin_amdgcn_raw_buffer_load_b128(rs, entering ? (uint32_t)ty - 16u : kPast, 0, 0);
       const v2u q = __builtin_amdgcn_raw_buffer_load_b64(rq, entering ? (uint32_t)ty - 8u : kPast, 0, 0);
       const uint32_t oy = fin ? kPast : (uint32_t)(ty + kLaneBytes * lane);
       load32(rs, oy, sy);
       load32(rq, oy, qy);
-      (void)scpx;   // (cleared when read: take_bits)
-      tile(tx, ex, sx, qx, sox, [&] {
-        scatter_starts(A, scpy, r, iw, ty, fin ? INT32_MIN : ty + kTile, lane, ty + kTile >= ey, rn);
+      const uint32_t par = tile(tx, ex, sx, qx, sox, skx, tgx, rfx, [&] {
+        rfy = r;
+        scatter_starts<VALID, VALID>(A, scpy, tcpy, r, iw, itg, ty, fin ? INT32_MIN : ty + kTile, lane,
+                                     ty + kTile >= ey, rn);
         soy = take_bits(&scpy[lane]);
+        if (VALID) tgy = take_bits(&tcpy[lane]);
       });
       if (fin) return false;
+      sky = skx ^ par;
       if (entering) {
         const uint32_t cs[4] = {a[0], a[1], a[2], a[3]}, cq[2] = {q[0], q[1]};
-        enter(cs, cq, psn, ty);
+        enter(cs, cq, psn, ty, rv, sky);
       }
       return true;
     };
     for (;;) {
-      if (!half(tA, eA, sA, qA, soA, sc, tB, eB, sB, qB, soB, sc + 64)) break;
-      if (!half(tB, eB, sB, qB, soB, sc + 64, tA, eA, sA, qA, soA, sc)) break;
+      if (!half(tA, eA, sA, qA, soA, skA, tgA, rfA, sc + 64, tcb + 64, tB, eB, sB, qB, soB, skB, tgB, rfB)) break;
+      if (!half(tB, eB, sB, qB, soB, skB, tgB, rfB, sc, tcb, tA, eA, sA, qA, soA, skA, tgA, rfA)) break;
     }
-    sc[lane] = 0u;
-    sc[64 + lane] = 0u;
   }
-#if HPGQ_CGR_ABL == 6
-  if (sink == 0x12345678u) risky = true;
-#endif
   if (__ballot(risky) && lane == 0) atomicOr(A.gate, GATE_EXACT);
   __syncthreads();
   for (int i = threadIdx.x; i < cells; i += kWG) {

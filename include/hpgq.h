@@ -303,13 +303,14 @@ int  hpgq_cgr_allreduce(hpgq_cgr_t *cg);
 uint32_t *hpgq_cgr_global_device(hpgq_cgr_t *cg);
 
 /*
- * Path selection.  AUTO (default): for k <= 7 and ALL_READS a coalesced
+ * Path selection.  AUTO (default): for k <= 7 (either mode) a coalesced
  * integer pass computes each word's cell from its own k bases, which is
  * provably the reference's (int)f cell unless some axis sees a run of
- * >= 48-k toward-dim moves or the batch holds bytes other than A/C/G/T/N or
- * qualities >= 128; such a call is redone by the exact double simulation on
- * the device.  EXACT: always the exact simulation.  Both are bit-identical
- * to old/chaos_game.c:165-267.
+ * >= 48-k toward-dim moves or a counted read holds bytes other than A/C/G/T/N
+ * or qualities >= 128; such a call is redone by the exact double simulation
+ * on the device.  In ONLY_VALID_READS mode the skipped reads' bytes count as
+ * absent (they move nothing, :188).  EXACT: always the exact simulation.
+ * Both are bit-identical to old/chaos_game.c:165-267.
  */
 #define HPGQ_CGR_PATH_AUTO  0
 #define HPGQ_CGR_PATH_EXACT 1

@@ -372,8 +372,11 @@ int oracle_cgr_fill(int k, int base_quality, const hpgq_batch_t *b, const uint8_
 
 /* independent batches (each its own fill call) in parallel: the CPU baseline
  * for config C5 (state resets per call, so batches are independent). */
-int oracle_cgr_fill_batches(int k, int base_quality, const hpgq_batch_t *bs, int nb,
-                            uint32_t *table_seq, uint32_t *table_q, uint32_t *word_count,
+/* nb independent fill calls spread over nthreads (bench.py's CPU baseline);
+ * status (may be NULL): one read_status[] per call, with mode as in
+ * oracle_cgr_fill */
+int oracle_cgr_fill_batches(int k, int base_quality, const hpgq_batch_t *bs, const uint8_t *const *status,
+                            int mode, int nb, uint32_t *table_seq, uint32_t *table_q, uint32_t *word_count,
                             int nthreads) {
   int dim = 1 << k;
   size_t cells = (size_t)dim * dim;
@@ -385,7 +388,7 @@ int oracle_cgr_fill_batches(int k, int base_quality, const hpgq_batch_t *bs, int
 #pragma omp parallel for num_threads(nt) schedule(dynamic, 1)
   for (int i = 0; i < nb; i++) {
     int t = omp_get_thread_num();
-    int e = oracle_cgr_fill(k, base_quality, &bs[i], NULL, HPGQ_CGR_ALL_READS,
+    int e = oracle_cgr_fill(k, base_quality, &bs[i], status ? status[i] : NULL, mode,
                             ts + (size_t)t * cells * 2, ts + (size_t)t * cells * 2 + cells, wc + t);
     if (e) err = e;
   }

@@ -3,20 +3,21 @@ old/chaos_game.c:165-267, bit for bit (GPU).
 
 Each seeded case draws k (1..12: the stream pass up to 7, the exact kernels
 above), the base quality, ALL_READS or ONLY_VALID_READS with a random status
-array, and 1-3 fill calls (the double state restarts per call, :180-181, and
+array (40 % of cases), and 1-3 fill calls (the double state restarts per call, :180-181, and
 is carried across the reads of one call, :263-264) over ragged reads that mix
 uniform random bases with N stretches, homopolymer / two-base runs of random
 length (around the stream pass's exactness threshold of 48-k D moves,
 DESIGN §4.5), lowercase / IUPAC bytes and quality bytes >= 128 -- so the gate
 between the stream pass and the exact simulation is hit from both sides.
-Tables and the u32 word count must equal the oracle's.
+Tables and the u32 word count must equal the oracle's, and each call must
+have taken the stream pass exactly when `stream_gate` says it is exact.
 """
 import numpy as np
 import pytest
 
 import hpgfastq as H
 import oracle_lib as O
-from test_cgr_gpu import assert_cgr
+from test_cgr_gpu import assert_cgr, stream_gate
 
 pytestmark = pytest.mark.gpu
 
@@ -64,7 +65,11 @@ def test_random_cgr_fills(case):
     wild_q = rng.random() < 0.2
     batches = [_batch(rng, base_q, odd, wild_q) for _ in range(int(rng.integers(1, 4)))]
     kw = dict(base_quality=base_q)
-    if rng.random() < 0.25:
+    if rng.random() < 0.4:
         kw["mode"] = H.CGR_ONLY_VALID_READS
-        kw["statuses"] = [(rng.random(b.n) < 0.8).astype(np.uint8) for b in batches]
-    assert_cgr(k, batches, **kw)
+        kw["statuses"] = [(rng.random(b.n) < rng.choice([0.5, 0.8, 0.95])).astype(np.uint8) for b in batches]
+    log = []
+    assert_cgr(k, batches, exact_log=log, **kw)
+    # the stream pass ran wherever it is exact, the exact kernels elsewhere
+    st = kw.get("statuses", [None] * len(batches))
+    assert log == [int(stream_gate(k, b, s, kw.get("mode", H.CGR_ALL_READS))) for b, s in zip(batches, st)]

@@ -58,6 +58,32 @@ def oracle_cgr(k, batches, statuses=None, mode=0, base_quality=33, path=None, ex
     return tables[0], tables[1], int(tables[2][0])
 
 
+def stream_gate(k, reads, status=None, mode=H.CGR_ALL_READS):
+    """Whether a streamed fill hands the call to the exact simulation
+    (hpgq_cgr_stream.h): over the COUNTED reads (ONLY_VALID_READS: status 1,
+    old/chaos_game.c:188) in order, a run of >= 48-k D moves on an axis (A/T on
+    x, G/T on y; N and skipped reads move nothing, so runs pass through them),
+    a byte other than A/C/G/T/N, or a quality byte >= 128.  The kernel's gate
+    is exactly this predicate (the exact run scan runs wherever a run could
+    reach the bound).  k > 7: always the exact kernels."""
+    if k > 7:
+        return True
+    a, b = int(reads.idx[0]), int(reads.idx[-1])
+    seq, qual = reads.seq[a:b], reads.qual[a:b]
+    if mode == H.CGR_ONLY_VALID_READS:
+        keep = np.repeat(np.asarray(status) == 1, np.diff(reads.idx))
+        seq, qual = seq[keep], qual[keep]
+    if (qual >= 128).any() or (~np.isin(seq, np.frombuffer(b"ACGTN", np.uint8))).any():
+        return True
+    mv = seq[np.isin(seq, np.frombuffer(b"ACGT", np.uint8))]
+    for dset in (b"AT", b"GT"):
+        d = np.concatenate([[0], np.isin(mv, np.frombuffer(dset, np.uint8)).astype(np.int8), [0]])
+        e = np.diff(d)
+        if len(mv) and (np.nonzero(e == -1)[0] - np.nonzero(e == 1)[0]).max(initial=0) >= 48 - k:
+            return True
+    return False
+
+
 def assert_cgr(k, batches, **kw):
     ts, tq, wc, rep = gpu_cgr(k, batches, **kw)
     os_, oq, ow = oracle_cgr(k, batches, **kw)
@@ -233,11 +259,117 @@ def test_cgr_edge_bytes_and_lengths():
         assert log == [1]   # lowercase / IUPAC / qualities >= 128: exact path
 
 
-def test_cgr_only_valid_reads():
+@pytest.mark.parametrize("skipped", [0.0, 0.05, 0.2, 0.9, 1.0])
+@pytest.mark.parametrize("k", [3, 7])
+def test_cgr_only_valid_reads(k, skipped):
+    """ONLY_VALID_READS (old/chaos_game.c:188) on the stream pass: random
+    reads stay on it whatever the share of skipped reads; status values other
+    than 1 (VALID_READ) all skip."""
+    reads = O.synth(20000, seed=9, L=250)
+    rng = np.random.default_rng(9)
+    status = np.where(rng.random(reads.n) < skipped, rng.choice([0, 2, 255], reads.n), 1).astype(np.uint8)
+    log = []
+    assert_cgr(k, [reads], statuses=[status], mode=H.CGR_ONLY_VALID_READS, exact_log=log)
+    assert log == [0]
+
+
+def test_cgr_only_valid_reads_exact_path():
     reads = O.synth(5000, seed=9, L=250)
     rng = np.random.default_rng(9)
     status = (rng.random(reads.n) < 0.8).astype(np.uint8)
-    assert_cgr(7, [reads], statuses=[status], mode=H.CGR_ONLY_VALID_READS)
+    log = []
+    assert_cgr(7, [reads], statuses=[status], mode=H.CGR_ONLY_VALID_READS, path=H.CGR_PATH_EXACT,
+               exact_log=log)
+    assert log == [1]
+
+
+def _skip_batch(rng, k, run_len, n=900):
+    """Reads with D-move runs of run_len split by 1-3 SKIPPED reads (status 0)
+    that hold Z moves, long D runs, lowercase / IUPAC bytes and qualities
+    >= 128 -- none of which may count -- plus skipped reads elsewhere."""
+    alph = {0: b"AT", 1: b"GT", 2: b"T"}
+    pairs, status = [], []
+
+    def junk():
+        L = int(rng.integers(0, 200))
+        s = bytearray(np.array(rng.choice(list(b"ACGTNacgtRYK"), L), np.uint8).tobytes())
+        if L > 80 and rng.random() < 0.5:
+            a = int(rng.integers(0, L - 70))
+            s[a:a + 70] = bytes([b"AGT"[int(rng.integers(0, 3))]]) * 70
+        q = rng.integers(33, 256, L).astype(np.uint8).tobytes()
+        return bytes(s), q
+
+    i = 0
+    while len(pairs) < n:
+        L = int(rng.integers(30, 300))
+        mix = np.array(rng.choice(list(b"ACGT"), L), np.uint8).tobytes()
+        if i % 4 == 0:
+            ax = (i // 4) % 3
+            run = bytes(rng.choice(list(alph[ax]), run_len).astype(np.uint8))
+            z = {0: b"C", 1: b"A", 2: b"C"}[ax]
+            cut = int(rng.integers(1, len(run)))
+            a = mix[: L // 2] + z + run[:cut]
+            b = run[cut:] + z + mix[L // 2:]
+            pairs.append((a, rng.integers(33, 75, len(a)).astype(np.uint8).tobytes()))
+            status.append(1)
+            for _ in range(int(rng.integers(1, 4))):
+                pairs.append(junk())
+                status.append(int(rng.choice([0, 2])))
+            pairs.append((b, rng.integers(33, 75, len(b)).astype(np.uint8).tobytes()))
+            status.append(1)
+        elif i % 7 == 3:
+            pairs.append(junk())
+            status.append(0)
+        else:
+            pairs.append((mix, rng.integers(33, 75, L).astype(np.uint8).tobytes()))
+            status.append(1)
+        i += 1
+    return O.Reads.from_pairs(pairs), np.array(status, np.uint8)
+
+
+@pytest.mark.parametrize("k", [1, 2, 4, 7])
+def test_cgr_valid_threshold_runs_across_skipped_reads(k):
+    """Runs of 47-k / 48-k D moves split by skipped reads: f passes through a
+    skipped read unchanged (:188), so the halves form one run -- 47-k stays on
+    the stream pass and 48-k sets the gate, whatever the skipped reads hold."""
+    rng = np.random.default_rng(300 + k)
+    for run_len, gate in ((47 - k, 0), (48 - k, 1)):
+        reads, status = _skip_batch(rng, k, run_len)
+        assert stream_gate(k, reads, status, H.CGR_ONLY_VALID_READS) == bool(gate)
+        log = []
+        assert_cgr(k, [reads], statuses=[status], mode=H.CGR_ONLY_VALID_READS, exact_log=log)
+        assert log == [gate]
+
+
+@pytest.mark.parametrize("k", [4, 7])
+def test_cgr_valid_stream_many_spans(k):
+    """150 MB in one ONLY_VALID_READS call with 5 % skipped reads (and 2 %
+    skipped runs of 1-40 reads, so skipped stretches cover whole tiles and
+    spans): the stream pass equals the exact GPU kernels."""
+    reads = O.synth(600_000, seed=12, L=250)
+    rng = np.random.default_rng(12)
+    status = (rng.random(reads.n) >= 0.05).astype(np.uint8)
+    for s0 in rng.integers(0, reads.n - 40, reads.n // 2000):
+        status[s0:s0 + int(rng.integers(1, 41))] = 0
+    log = []
+    ts, tq, wc, _ = gpu_cgr(k, [reads], statuses=[status], mode=H.CGR_ONLY_VALID_READS, exact_log=log)
+    assert log == [0]
+    es, eq, ew, _ = gpu_cgr(k, [reads], statuses=[status], mode=H.CGR_ONLY_VALID_READS,
+                            path=H.CGR_PATH_EXACT)
+    assert wc == ew and wc > 0
+    np.testing.assert_array_equal(ts, es)
+    np.testing.assert_array_equal(tq, eq)
+
+
+def test_cgr_valid_without_status_counts_nothing():
+    reads = O.synth(1000, seed=3, L=150)
+    cg = H.ChaosGame(7, 33)
+    t = _dev(reads)
+    cg.fill_device(H.engine.device_batch(reads.n, t["seq"].data_ptr(), t["qual"].data_ptr(),
+                                         t["idx"].data_ptr()), None, H.CGR_ONLY_VALID_READS)
+    ts, tq, wc = cg.tables()
+    cg.close()
+    assert wc == 0 and not ts.any() and not tq.any()
 
 
 @pytest.mark.parametrize("off", [37, 16384 - 5, 3 * 16384 + 9])

@@ -1,7 +1,7 @@
 """Profiling driver: the C2 engine kernel on one resident 10M-read batch.
 
 Run under rocprofv3 (kernel trace or --pmc passes); no timing of its own.
-  python tools/prof_engine.py [--reads N] [--iters K] [--mode c2|stats|edit|edit0|editL|editR|maxn|pe|cgr]
+  python tools/prof_engine.py [--reads N] [--iters K] [--mode c2|stats|edit|edit0|editL|editR|maxn|pe|cgr|cgrv]
 """
 import argparse
 import ctypes as C
@@ -25,7 +25,7 @@ args = ap.parse_args()
 
 dev = torch.device("cuda", 0)
 n, L = args.reads, args.L
-if args.mode == "cgr":
+if args.mode in ("cgr", "cgrv"):
     s = H.Synth(5, L, 5, 5, 1, 33, 0)
     idx = np.zeros(n + 1, np.int32)
     H.check(H.lib.hpgq_synth_indices_host(C.byref(s), 0, n, idx.ctypes.data), "idx")
@@ -39,8 +39,17 @@ if args.mode == "cgr":
     torch.cuda.synchronize()
     cg = H.ChaosGame(args.k)
     b = H.engine.device_batch(n, sq.data_ptr(), ql.data_ptr(), ix.data_ptr())
+    st = None
+    if args.mode == "cgrv":   # ONLY_VALID_READS with bench.py's 5 % invalid status
+        sys.path.insert(0, ROOT)
+        from bench import read_status
+        st = torch.from_numpy(read_status(n, 5)).to(dev)
+        torch.cuda.synchronize()
     for _ in range(args.iters):
-        cg.fill_device(b)
+        if st is not None:
+            cg.fill_device(b, st.data_ptr(), H.CGR_ONLY_VALID_READS)
+        else:
+            cg.fill_device(b)
     cg.sync()
     print("cgr reads", n, "replays", cg.last_replays(), "words", cg.tables()[2])
     cg.close()
