@@ -79,6 +79,13 @@ CONFIGS = {
     "c2_noor": dict(metric="Mreads/s (150 bp) stats+filter with N / out-of-range limits",
                     unit="Mreads/s", reads=100_000_000, batch=10_000_000, L=150, seed=2,
                     workload="C2 flags + --max-N 2 --max-out-of-quality 20"),
+    "c4_noor": dict(metric="Mreads/s (150 bp) edit Q20 trim + --max-N 2 + stats",
+                    unit="Mreads/s", reads=62_500_000, batch=12_500_000, L=150, seed=4,
+                    workload="C4 flags + --max-N 2 (the post-trim filter, src/edit_fastq.c:159-164)"),
+    "c4_pe": dict(metric="Mpairs/s (2x150 bp) paired-end edit Q20 trim + stats",
+                  unit="Mpairs/s", reads=50_000_000, batch=10_000_000, L=150, seed=4,
+                  workload="C4 trims on paired-end 2x150 + --read-quality-range 20, "
+                           "(pair kept iff both mates pass; old/main_hpg_fastq_old.c:728)"),
     "c2_lr": dict(metric="Mreads/s (150 bp) stats+filter with a 5' window filter",
                   unit="Mreads/s", reads=100_000_000, batch=10_000_000, L=150, seed=2,
                   workload="C2 flags + --left-length 10 --left-quality-range 20,"),
@@ -110,9 +117,14 @@ def parse():
 
 def params_for(cfg, L):
     lmax = CONFIGS[cfg].get("lmax", L)
-    if cfg == "c4":
-        return H.edit_params(lmax=lmax, stats=True, left_length=10, left_quality_range="20,",
-                             right_length=30, right_quality_range="20,")
+    if cfg in ("c4", "c4_noor", "c4_pe"):
+        extra = dict(max_N=2) if cfg == "c4_noor" else {}
+        if cfg == "c4_pe":
+            extra = dict(read_quality_range="20,")
+        p = H.edit_params(lmax=lmax, stats=True, left_length=10, left_quality_range="20,",
+                          right_length=30, right_quality_range="20,", **extra)
+        p.paired = 1 if cfg == "c4_pe" else 0
+        return p
     if cfg == "c1_gpu":
         return H.stats_params(lmax=lmax)
     if cfg in ("c2_nofail", "c3_nofail"):
@@ -192,7 +204,7 @@ def cpu_baseline(args, params):
     L = args.read_length
     cgr = args.config in ("c5", "c5_valid")
     n = 400_000 if cgr else 2_000_000
-    mates = 2 if args.config == "c3" else 1
+    mates = 2 if params.paired else 1
     bufs = []
     for m in range(mates):
         s = H.Synth(args.seed, L, 5, 5, 1, 33, m)

@@ -250,7 +250,7 @@ static int plan_chain(hpgq_ctx *c, Chain &ch, int cus, int geo_force) {
   const int xm = (nx ? hpgq::X_NOOR : 0) | (lr ? hpgq::X_LR : 0);
   const bool edit = fl & hpgq::F_EDIT;
   const char *force = std::getenv("HPGQ_KERNEL");   // "single": the catch-all alone (tests)
-  const bool seg = !(xm && edit) && !(edit && c->nm == 2) && !(force && std::strcmp(force, "single") == 0);
+  const bool seg = !(force && std::strcmp(force, "single") == 0);
   if (!seg) {
     catch_all(ch.s1, c->nm, p.lmax, needs_generic(fl), false);
     return finish_stage(c, ch.s1, catch_all_lds(p, c->nm), cus);

@@ -2,7 +2,8 @@
 // (built once per geometry with -DHPGQ_GEO=0|1|2, so the three compile in
 // parallel).  Occupancy per variant (MINW, waves per SIMD) is the highest at
 // which the variant's registers fit without spills: single-end 4 (tri 5),
-// paired-end 3 (two mates' accumulators), see DESIGN.md §4.1.
+// paired-end 3 (two mates' accumulators), see DESIGN.md §4.1.  Every
+// combination of paired-end, edit and the extra filter scans has an instance.
 #include <cstdio>
 
 #include "hpgq_engine_tri.h"
@@ -30,29 +31,32 @@ constexpr int kPeW = HPGQ_PE_WAVES;          // paired-end
 constexpr int kEdW = HPGQ_EDIT_WAVES;        // single-end edit
 constexpr const char *kGeoName = G == GEO_TRI ? "tri" : (G == GEO_HEX ? "hex" : "wide");
 
-template <bool F, int XM>
+template <bool F, int XM, bool EDIT>
 const void *x_kernel(int nm) {
-  return nm == 2 ? (const void *)engine_tri_x_kernel<kPeW, 2, G, F, XM> : (const void *)engine_tri_x_kernel<kSeW, 1, G, F, XM>;
+  return nm == 2 ? (const void *)engine_tri_x_kernel<kPeW, 2, G, F, XM, EDIT>
+                 : (const void *)engine_tri_x_kernel<EDIT ? kEdW : kSeW, 1, G, F, XM, EDIT>;
+}
+
+template <bool F, bool EDIT>
+const void *x_kernel_for(int nm, int xm) {
+  return xm == X_NOOR ? x_kernel<F, X_NOOR, EDIT>(nm) : xm == X_LR ? x_kernel<F, X_LR, EDIT>(nm)
+                                                            : x_kernel<F, X_NOOR | X_LR, EDIT>(nm);
 }
 
 template <bool F>
 SegChoice pick(int nm, bool edit, int xm, char *name, size_t cap) {
-  constexpr int kSe = kSeW;
   const void *fn = nullptr;
-  int w = nm == 2 ? kPeW : kSe;
+  const int w = nm == 2 ? kPeW : (edit ? kEdW : kSeW);
   if (xm) {
-    if (edit) return SegChoice{nullptr, 0};
-    fn = xm == X_NOOR ? x_kernel<F, X_NOOR>(nm) : xm == X_LR ? x_kernel<F, X_LR>(nm) : x_kernel<F, X_NOOR | X_LR>(nm);
-    std::snprintf(name, cap, "hpgq::engine_tri_x_kernel<%d, %d, %s%s%s%s>", w, nm, kGeoName, F ? ", follow" : "",
-                  (xm & X_NOOR) ? ", noor" : "", (xm & X_LR) ? ", window" : "");
+    fn = edit ? x_kernel_for<F, true>(nm, xm) : x_kernel_for<F, false>(nm, xm);
+    std::snprintf(name, cap, "hpgq::engine_tri_x_kernel<%d, %d, %s%s%s%s%s>", w, nm, kGeoName,
+                  edit ? ", edit" : "", F ? ", follow" : "", (xm & X_NOOR) ? ", noor" : "",
+                  (xm & X_LR) ? ", window" : "");
   } else {
-    if (edit && nm == 2) return SegChoice{nullptr, 0};
-    if (nm == 2) fn = (const void *)engine_tri_kernel<kPeW, 2, false, G, F>;
-    else if (edit) {
-      fn = (const void *)engine_tri_kernel<kEdW, 1, true, G, F>;
-      w = kEdW;
-    }
-    else fn = (const void *)engine_tri_kernel<kSe, 1, false, G, F>;
+    if (nm == 2) fn = edit ? (const void *)engine_tri_kernel<kPeW, 2, true, G, F>
+                           : (const void *)engine_tri_kernel<kPeW, 2, false, G, F>;
+    else if (edit) fn = (const void *)engine_tri_kernel<kEdW, 1, true, G, F>;
+    else fn = (const void *)engine_tri_kernel<kSeW, 1, false, G, F>;
     std::snprintf(name, cap, "hpgq::engine_tri_kernel<%d, %d, %s, %s%s>", w, nm, edit ? "edit" : "filter", kGeoName,
                   F ? ", follow" : "");
   }

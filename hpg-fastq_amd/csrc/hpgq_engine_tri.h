@@ -48,24 +48,6 @@ namespace hpgq {
 
 constexpr int kTriSlack = 8;    // readable bytes past the data end the loads may touch
 
-// A/B build knobs (tools/probes/build_geo_ab.sh): the cache policy of the read
-// streams' loads, and an XCD-contiguous workgroup -> unit order
-#ifndef HPGQ_LOAD_AUX
-#define HPGQ_LOAD_AUX 0
-#endif
-#ifndef HPGQ_XCD_REMAP
-#define HPGQ_XCD_REMAP 0
-#endif
-#ifndef HPGQ_NO_PEU   // paired-end: subtract failed pairs in the unit epilogue (round 1; A/B)
-#define HPGQ_NO_PEU 0
-#endif
-#ifndef HPGQ_EARLY_TRIMS   // edit: trims one unit ahead (round 1; A/B)
-#define HPGQ_EARLY_TRIMS 0
-#endif
-#ifndef HPGQ_NO_PF_X   // extra-scan variants without pass-first (A/B)
-#define HPGQ_NO_PF_X 0
-#endif
-
 constexpr int GEO_TRI = 0, GEO_HEX = 1, GEO_WIDE = 2;
 constexpr int X_NOOR = 1, X_LR = 2;   // extra filter scans (engine_tri_x_kernel)
 
@@ -318,9 +300,10 @@ struct MateTag {
 // mate 1's steps, then mate 2's, each mate with its own accumulators / LDS
 // partials / counter set; the epilogue takes the pair decision (both mates
 // pass) and subtracts failed pairs from both sets.
-// EDIT (NM = 1): the unit prologue trims each read (trim_word, written to
-// A.trim when the caller wants it) and describes it by its window [ts, n - te)
-// (offset + ts, length n - ts - te): stats and filter see the trimmed read.
+// EDIT: the unit prologue trims each read (each mate; trim_word, written to
+// A.trim when the caller wants it: mate 2 at num_reads + i) and describes it
+// by its window [ts, n - te) (offset + ts, length n - ts - te): stats and the
+// filter (with any extra scans) see the trimmed read.
 // XM (extra filter scans; the plain kernels have none):
 //   X_NOOR: the filter also counts N bases and out-of-range qualities per read
 //     (max_N, max_out_of_quality; src/filter_fastq.c:140-145): a second
@@ -334,7 +317,6 @@ struct MateTag {
 // FOLLOW: a follow-up stage (reads deferred by the stage before, by unit masks).
 template <int MINW, int NM, bool EDIT, int G, int XM, bool FOLLOW>
 __device__ __forceinline__ void tri_body(const EngineArgs &A) {
-  static_assert(!EDIT || NM == 1, "edit on the segmented kernel is single-end");
   constexpr bool NX = XM & X_NOOR, LR = XM & X_LR;
   // PASS FIRST (single-end, no extra scans): each step decides its reads'
   // pass/fail from the step's own scan (segment totals by two ds_bpermute)
@@ -344,16 +326,15 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   // every read and subtract the failed ones in the unit epilogue.
   // (edit, follow-up: their registers would spill; the window variant alone
   // fails few reads and ran 4 % slower with it: 692 vs 665 us per 10 M reads)
-  constexpr bool PF = NM == 1 && !EDIT && !FOLLOW && XM != X_LR && !(HPGQ_NO_PF_X && XM);
-  constexpr bool LATE = EDIT && !HPGQ_EARLY_TRIMS;   // the unit prologue's place (see the unit loop)
+  constexpr bool PF = NM == 1 && !EDIT && !FOLLOW && XM != X_LR;
+  constexpr bool LATE = EDIT;   // the unit prologue's place (see the unit loop)
   // PEU (paired-end): a group is ONE step of both mates (grp[slot][m]); both
   // are added, the pair is decided from both scans at once (ds_bpermute), and
   // a failed pair is taken back out of the nibble counters from the registers
   // still holding it -- no re-read (the epilogue's re-gather of failed pairs
   // missed L2 and cost 15 % of C3).  Holding both mates' step values for a
   // pass-first decision instead needed 215 VGPRs (2 waves/SIMD: no faster).
-  constexpr bool PEU = NM == 2 && !EDIT && !FOLLOW && XM == 0 && Geo<G>::kU >= 2 && !HPGQ_NO_PEU;
-  static_assert(!(XM && EDIT), "the extra-scan filter variants do not edit");
+  constexpr bool PEU = NM == 2 && !FOLLOW && XM == 0 && Geo<G>::kU >= 2;
   using GG = Geo<G>;
   constexpr int NW = GG::kNW, kSegs = GG::kSegs, kSegW = GG::kSegW, kBlock = GG::kBlock, kU = GG::kU;
   static_assert(4 * kU <= kNibbleEvery && kBlock / kSegs - 4 * kU <= kNibbleEvery, "nibble widening");
@@ -469,10 +450,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
 
   const int ublock = FOLLOW ? A.unit_reads : kBlock;   // reads per unit
   UnitIter<FOLLOW, kBlock> it;
-  int wg = (int)blockIdx.x;
-  if (HPGQ_XCD_REMAP && (gridDim.x & 7) == 0)   // workgroups of one XCD (b mod 8) take consecutive units
-    wg = (wg & 7) * (int)(gridDim.x >> 3) + (wg >> 3);
-  it.init(A, wg * kWaves + wave, (int)gridDim.x * kWaves);
+  it.init(A, (int)blockIdx.x * kWaves + wave, (int)gridDim.x * kWaves);
 
   // a unit's read offsets (lane j: read j), fetched one unit ahead of the
   // prologue that describes it, so the prologue does not wait for them
@@ -490,7 +468,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   // unit prologue: lane j describes read (pair) j in read table `tb`; absent
   // and deferred reads get length 0 and out-of-range offsets.  Returns this
   // lane's lengths (the epilogue needs them) and the deferred-lane mask.
-  auto load_block = [&](const Unit &U, int tb, uint32_t (&len)[NM], uint32_t &tw, uint64_t &dm,
+  auto load_block = [&](const Unit &U, int tb, uint32_t (&len)[NM], uint32_t (&tw)[NM], uint64_t &dm,
                         const int32_t (&ia)[NM], const int32_t (&ie)[NM]) __attribute__((always_inline)) {
     const bool on = lane < U.nr;
     const uint32_t rid = (uint32_t)(U.u * ublock) + (FOLLOW ? scratch[lane] : (uint32_t)lane);
@@ -513,15 +491,15 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       if (lane == 0) A.defer_bits[U.u] = pbits;
       ndefer += (uint32_t)__builtin_popcountll(dm);
     }
-    tw = 0;
 #pragma unroll
     for (int m = 0; m < NM; ++m) {
       int a = ia[m], e = ie[m];
+      tw[m] = 0;
       if (EDIT) {   // trim here, then describe the trimmed window
-        tw = live ? trim_word(cold, rq[m], bq[m] + a, e - a) : 0u;
-        if (A.trim && live) A.trim[rid] = tw;
-        a += (int)(tw & 0xFFFFu);
-        e -= (int)(tw >> 16);
+        tw[m] = live ? trim_word(cold, rq[m], bq[m] + a, e - a) : 0u;
+        if (A.trim && live) A.trim[(size_t)m * (size_t)A.num_reads + rid] = tw[m];
+        a += (int)(tw[m] & 0xFFFFu);
+        e -= (int)(tw[m] >> 16);
         if (e < a) e = a;
       }
       const uint32_t n = live ? (uint32_t)(e - a) : 0u;
@@ -543,12 +521,12 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     const v4u rec = *reinterpret_cast<const v4u *>(tab(m, tb) + 4 * src);
     pd.n = rec.z;
     if (NW == 2) {
-      const v2u a = __builtin_amdgcn_raw_buffer_load_b64(rs[m], rec.x + lane8, 0, HPGQ_LOAD_AUX);
-      const v2u b = __builtin_amdgcn_raw_buffer_load_b64(rq[m], rec.y + lane8, 0, HPGQ_LOAD_AUX);
+      const v2u a = __builtin_amdgcn_raw_buffer_load_b64(rs[m], rec.x + lane8, 0, 0);
+      const v2u b = __builtin_amdgcn_raw_buffer_load_b64(rq[m], rec.y + lane8, 0, 0);
       pd.s[0] = a.x; pd.s[1] = a.y; pd.q[0] = b.x; pd.q[1] = b.y;
     } else {
-      const v4u a = __builtin_amdgcn_raw_buffer_load_b128(rs[m], rec.x + lane8, 0, HPGQ_LOAD_AUX);
-      const v4u b = __builtin_amdgcn_raw_buffer_load_b128(rq[m], rec.y + lane8, 0, HPGQ_LOAD_AUX);
+      const v4u a = __builtin_amdgcn_raw_buffer_load_b128(rs[m], rec.x + lane8, 0, 0);
+      const v4u b = __builtin_amdgcn_raw_buffer_load_b128(rq[m], rec.y + lane8, 0, 0);
 #pragma unroll
       for (int w = 0; w < NW; ++w) {
         pd.s[w] = a[w & 3];
@@ -721,12 +699,12 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   };
 
   uint32_t len[NM], lenn[NM];
-  uint32_t tw = 0, twn = 0;   // EDIT: trim word of the lane's read
+  uint32_t tw[NM], twn[NM];   // EDIT: trim words of the lane's read (pair)
   uint64_t dm = 0, dmn = 0;   // deferred lanes of the current / next unit
   int tb = 0;   // read table of the current unit
   int32_t ia[NM], ie[NM];   // offsets of the unit after the next one to be described
   Unit cur = it.next(), nxt = Unit{-1, 0, 0};
-  for (int m = 0; m < NM; ++m) len[m] = lenn[m] = 0;
+  for (int m = 0; m < NM; ++m) len[m] = lenn[m] = tw[m] = twn[m] = 0;
   if (cur.u >= 0) {
     fetch_idx(cur, ia, ie);
     load_block(cur, tb, len, tw, dm, ia, ie);
@@ -874,8 +852,12 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       for (int g = 0; g < ng; g += 2) {
         load_group_pe(tb, nt, g + 1, 1);
         process_pair(g, 0);
-        if (g + 2 < ng) load_group_pe(tb, nt, g + 2, 0);
-        else load_group_pe(tb ^ 1, nnt, 0, 0);
+        if (g + 2 < ng) {
+          load_group_pe(tb, nt, g + 2, 0);
+        } else {
+          if (LATE) describe_next();
+          load_group_pe(tb ^ 1, nnt, 0, 0);
+        }
         process_pair(g + 1, 1);
         if (stats && ((g + 2) & 7) == 0)   // nibbles hold at most 15 steps
           for (int m = 0; m < NM; ++m) acc[m].widen();
@@ -886,6 +868,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       run_mate(MateTag<0>{});
       if (NM == 2) run_mate(MateTag<NM - 1>{});
     } else if (PEU) {
+      if (LATE) describe_next();
       load_group_pe(tb ^ 1, nnt, 0, 0);   // a wholly deferred unit: straight to the next
     } else {
       if (LATE) describe_next();
@@ -932,10 +915,10 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     const uint64_t failed = __ballot(valid && !pass);
     const uint32_t npass = (uint32_t)__builtin_popcountll(__ballot(pass));
     const uint32_t nvalid = (uint32_t)(nr - __builtin_popcountll(dm));
-    if (EDIT) cnt[0][3] += (uint32_t)__builtin_popcountll(__ballot(valid && tw != 0u));
 #pragma unroll
     for (int m = 0; m < NM; ++m) {
       const int n = (int)len[m];
+      if (EDIT) cnt[m][3] += (uint32_t)__builtin_popcountll(__ballot(valid && tw[m] != 0u));
       cnt[m][0] += nvalid;
       cnt[m][1] += npass;
       cnt[m][2] += (uint32_t)__builtin_popcountll(failed);
@@ -991,8 +974,10 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       }
     }
 #pragma unroll
-    for (int m = 0; m < NM; ++m) len[m] = lenn[m];
-    tw = twn;
+    for (int m = 0; m < NM; ++m) {
+      len[m] = lenn[m];
+      tw[m] = twn[m];
+    }
     dm = dmn;
     tb ^= 1;
     cur = nxt;
@@ -1029,10 +1014,10 @@ __global__ void __launch_bounds__(kWG, MINW) engine_tri_kernel(EngineArgs A) {
   tri_body<MINW, NM, EDIT, G, 0, FOLLOW>(A);
 }
 
-// the segmented kernel with extra filter scans (XM: X_NOOR | X_LR; no edit)
-template <int MINW, int NM, int G, bool FOLLOW, int XM>
+// the segmented kernel with extra filter scans (XM: X_NOOR | X_LR)
+template <int MINW, int NM, int G, bool FOLLOW, int XM, bool EDIT>
 __global__ void __launch_bounds__(kWG, MINW) engine_tri_x_kernel(EngineArgs A) {
-  tri_body<MINW, NM, false, G, XM, FOLLOW>(A);
+  tri_body<MINW, NM, EDIT, G, XM, FOLLOW>(A);
 }
 
 // kernel selection (one translation unit per geometry, hpgq_engine_geo.hip):

@@ -413,6 +413,66 @@ def test_window_filters_paired(geo_choice):
     assert_same(p, r1, r2)
 
 
+# ---- edit with the extra filter scans / paired-end edit (segmented) ---------
+C4_TRIMS = dict(left_length=10, left_quality_range="20,", right_length=30, right_quality_range="20,")
+EDIT_X_CASES = {
+    "c4_noor": dict(max_N=2),
+    "maxn_oor": dict(read_quality_range="22,38", max_N=0, max_out_of_quality=5),
+    "oor_len": dict(read_length_range="40,140", read_quality_range="15,", max_out_of_quality=12),
+    "plain": dict(read_quality_range="25,"),
+}
+
+
+@pytest.mark.parametrize("paired", [0, 1])
+@pytest.mark.parametrize("name", sorted(EDIT_X_CASES))
+def test_edit_filters_route_to_segmented_kernel(name, paired, geo_choice):
+    """edit with --max-N / --max-out-of-quality (the post-trim filter,
+    src/edit_fastq.c:159-164) and paired-end edit (old/main_hpg_fastq_old.c:728)
+    run on the segmented kernels -- no catch-all -- bit-identical to the
+    oracle (masks, trims of both mates, both counter sets), at a size that
+    gives every wave several blocks."""
+    p = H.edit_params(lmax=150, stats=True, **C4_TRIMS, **EDIT_X_CASES[name])
+    p.paired = paired
+    with H.Engine(p) as e:
+        nx = name != "plain"
+        assert ("engine_tri_x_kernel" if nx else "engine_tri_kernel") in e.kernel_name, e.kernel_chain
+        assert "edit" in e.kernel_name and ("noor" in e.kernel_name) == nx, e.kernel_chain
+        assert f", {1 + paired}, " in e.kernel_name, e.kernel_chain
+        assert ("hex" if geo_choice == "auto" else geo_choice) in e.kernel_name
+    n = 300_000 if paired else 600_000
+    r1 = O.synth(n, seed=26, L=150, trunc_pct=10, n_per_1024=12, mate=0)
+    r2 = O.synth(n, seed=26, L=150, trunc_pct=10, n_per_1024=12, mate=1) if paired else None
+    c = assert_same(p, r1, r2)
+    assert c[H.S_NUM_EDITED] > 0 and c[H.S_NUM_FAILED] > 0
+
+
+@pytest.mark.parametrize("paired", [0, 1])
+def test_edit_with_window_filters_abi(paired, geo_choice):
+    """Through the C-ABI a caller may combine edit with the 5'/3' window
+    filters (the CLI's edit disables them, src/edit_fastq.c:159-164): the
+    windows apply to the trimmed read, on the segmented window-scan variant."""
+    p = H.edit_params(lmax=150, stats=True, **C4_TRIMS, read_quality_range="18,")
+    p.filter_on = 1
+    p.left_length, p.min_left_quality, p.max_left_quality = 12, 24, H.MAX_VALUE
+    p.right_length, p.min_right_quality, p.max_right_quality = 20, 10, 38
+    p.paired = paired
+    with H.Engine(p) as e:
+        assert "edit" in e.kernel_name and "window" in e.kernel_name, e.kernel_chain
+    r1 = O.synth(100_000, seed=27, L=150, trunc_pct=10, mate=0)
+    r2 = O.synth(100_000, seed=27, L=150, trunc_pct=10, mate=1) if paired else None
+    assert_same(p, r1, r2)
+
+
+def test_paired_edit_mixed_lengths(geo_choice):
+    """Paired-end edit across the chain: pairs with a mate past the first
+    geometry go to the wide follow-up or the catch-all, trimmed there."""
+    r1 = _mixed(2000, 9, [60, 150, 158, 240, 400], [20, 40, 20, 15, 5])
+    r2 = _mixed(2000, 10, [60, 150, 158, 240, 400], [20, 40, 20, 15, 5])
+    p = H.edit_params(lmax=512, stats=True, **C4_TRIMS, max_N=1)
+    p.paired = 1
+    assert_same(p, r1, r2)
+
+
 # ---- routing by the reads' actual lengths (DESIGN §4.0) ---------------------
 C2 = dict(read_quality_range="20,", read_length_range="50,")
 

@@ -65,8 +65,9 @@ def _run_gpu(params, batches, split=False):
             for a, b in zip(cuts[:-1], cuts[1:]):   # absolute offsets: idx + a
                 bs = [H.engine.device_batch(b - a, sq.data_ptr(), ql.data_ptr(), ix.data_ptr() + 4 * a)
                       for sq, ql, ix in mm]
+                # (paired trims: mate 2 at num_reads + i of each call, so only whole-batch calls)
                 e.run_device(bs[0], bs[1] if nsets == 2 else None, mask.data_ptr() + a,
-                             trim.data_ptr() + 4 * a if params.edit_on and nsets == 1 else None)
+                             trim.data_ptr() + 4 * a if params.edit_on and (nsets == 1 or not split) else None)
             e.sync()
             masks.append(mask.cpu().numpy())
             trims.append(trim.cpu().numpy().view(np.uint32) if params.edit_on else None)
@@ -87,7 +88,10 @@ def _oracle_range(params, seed, L, lo, n, pool):
     ctr = np.zeros(H.counters_len(params.lmax) * nsets, np.uint64)
     for _m, _t, c in res:
         ctr += c   # u64: wraps like the device counters
-    return np.concatenate([m for m, _t, _c in res]), np.concatenate([t for _m, t, _c in res]), ctr
+    # trims: [mate 1 | mate 2] per part -> [mate 1 of the range | mate 2 of the range]
+    trim = np.concatenate([t[: len(t) // nsets * (mt + 1)][len(t) // nsets * mt:]
+                           for mt in range(nsets) for _m, t, _c in res])
+    return np.concatenate([m for m, _t, _c in res]), trim, ctr
 
 
 def _check_config(params, seed, L, reads, batch):
@@ -134,6 +138,30 @@ def test_c4_full_size():
     assert int(c[H.S_NUM_EDITED]) > 0
 
 
+def test_c4_noor_full_size():
+    """C4 flags + --max-N 2 (the post-trim N filter, src/edit_fastq.c:159-164) on the
+    segmented edit kernel's N / out-of-range variant (bench --config c4_noor)."""
+    p = H.edit_params(lmax=150, stats=True, left_length=10, left_quality_range="20,",
+                      right_length=30, right_quality_range="20,", max_N=2)
+    with H.Engine(p) as e:
+        assert "edit" in e.kernel_name and "noor" in e.kernel_name, e.kernel_chain
+    c = _check_config(p, seed=4, L=150, reads=62_500_000, batch=12_500_000)
+    assert int(c[H.S_NUM_EDITED]) > 0 and int(c[H.S_NUM_FAILED]) > 0
+
+
+def test_c4_pe_full_size():
+    """C4 trims on paired-end 2 x 150: 50 M pairs in 10 M-pair batches, each mate
+    trimmed, a pair kept iff both mates pass (bench --config c4_pe)."""
+    p = H.edit_params(lmax=150, stats=True, left_length=10, left_quality_range="20,",
+                      right_length=30, right_quality_range="20,", read_quality_range="20,")
+    p.paired = 1
+    with H.Engine(p) as e:
+        assert "engine_tri_kernel" in e.kernel_name and "edit" in e.kernel_name, e.kernel_chain
+    c = _check_config(p, seed=4, L=150, reads=50_000_000, batch=10_000_000)
+    ln = H.counters_len(150)
+    assert int(c[H.S_NUM_EDITED]) > 0 and int(c[ln + H.S_NUM_EDITED]) > 0
+
+
 def test_c5_full_size():
     """C5: chaos game k = 7 over 25 M x 250 bp, one fill call per 5 M-read batch (bench
     --config c5): device tables == the oracle's chaos_game_fill_tables restatement summed
@@ -165,6 +193,49 @@ def test_c5_full_size():
         want_s += s
         want_q += q
         want_w = (want_w + int(w[0])) & 0xFFFFFFFF   # fq_word_count is u32
+    np.testing.assert_array_equal(ts.reshape(-1), want_s)
+    np.testing.assert_array_equal(tq.reshape(-1), want_q)
+    assert wc == want_w
+
+
+def test_c5_valid_full_size():
+    """C5 in ONLY_VALID_READS mode with bench.py's 5 % invalid read_status
+    (bench --config c5_valid): every call on the stream pass, tables equal the
+    oracle's over the same calls and statuses (old/chaos_game.c:188)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import read_status
+    k, seed, L, reads, batch = 7, 5, 250, 25_000_000, 5_000_000
+    batches = _device_batches(seed, L, reads, batch, 1)
+    cg = H.ChaosGame(k, 33)
+    keep = []
+    try:
+        for lo, n, mm in batches:
+            sq, ql, ix = mm[0]
+            st = torch.from_numpy(read_status(n, seed, lo)).to(torch.device("cuda", 0))
+            keep.append(st)
+            cg.fill_device(H.engine.device_batch(n, sq.data_ptr(), ql.data_ptr(), ix.data_ptr()),
+                           st.data_ptr(), H.CGR_ONLY_VALID_READS)
+            cg.sync()
+            assert cg.last_exact() == 0
+        ts, tq, wc = cg.tables()
+    finally:
+        cg.close()
+    del batches, keep
+
+    def call(lo):
+        r = O.synth(batch, seed=seed, L=L, first=lo)
+        return O.cgr(k, r, status=read_status(batch, seed, lo), mode=H.CGR_ONLY_VALID_READS)
+
+    with ThreadPoolExecutor(min(POOL, reads // batch)) as pool:
+        res = list(pool.map(call, range(0, reads, batch)))
+    want_s = np.zeros(1 << (2 * k), np.uint32)
+    want_q = np.zeros(1 << (2 * k), np.uint32)
+    want_w = 0
+    for s_, q, w in res:
+        want_s += s_
+        want_q += q
+        want_w = (want_w + int(w[0])) & 0xFFFFFFFF
     np.testing.assert_array_equal(ts.reshape(-1), want_s)
     np.testing.assert_array_equal(tq.reshape(-1), want_q)
     assert wc == want_w
