@@ -67,12 +67,25 @@ struct hpgq_ctx {
   int parity = 0;
   uint64_t *d_bits1 = nullptr, *d_bits2 = nullptr;   // deferred reads per s1 unit
   size_t bits_cap = 0;
-  // host-path device staging
-  char *d_buf = nullptr;
-  size_t d_buf_cap = 0;
-  uint8_t *d_mask = nullptr;
-  uint32_t *d_trim = nullptr;
-  size_t d_out_cap = 0;
+  // host path (hpgq_run_host): two staging slots, each a pinned host buffer
+  // and a device buffer for one batch and its outputs.  The caller's batch is
+  // copied into the slot's pinned buffer in chunks, each chunk's H2D queued on
+  // the copy stream as soon as it is filled; the engine stream waits for the
+  // slot's copies only, so one batch's H2D overlaps the previous batch's
+  // kernels.  Outputs come back into the slot's pinned buffer and reach the
+  // caller's arrays in hpgq_sync (or when the slot is reused).
+  hipStream_t cstream = nullptr;
+  struct Slot {
+    char *h = nullptr, *d = nullptr;   // [seq | qual | idx] per mate, then mask | trim
+    size_t cap = 0;
+    hipEvent_t copied = nullptr, used = nullptr;   // H2D done / the slot's kernels + D2H done
+    bool busy = false;
+    uint8_t *mask_dst = nullptr;   // caller outputs waiting for this slot's D2H
+    uint32_t *trim_dst = nullptr;
+    size_t mask_off = 0, trim_off = 0, nreads = 0, ntrim = 0;   // ntrim: reads x mates
+  } slot[2];
+  int cur_slot = 0;
+  int32_t *h_err = nullptr;   // pinned: the error flag, copied back by hpgq_sync
   ncclComm_t comm = nullptr;
 };
 
@@ -415,6 +428,13 @@ int hpgq_open(hpgq_ctx_t **out, int device, const hpgq_params_t *p) {
   c->d_flags = reinterpret_cast<uint32_t *>(c->d_state + c->clen * c->nm);
   HPGQ_HIP_TRY(hipMalloc(&c->d_global, c->clen * c->nm * sizeof(uint64_t)));
   HPGQ_HIP_TRY(hipMemsetAsync(c->d_state, 0, state_bytes(c), c->stream));
+  HPGQ_HIP_TRY(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
+  HPGQ_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&c->h_err), 64, hipHostMallocDefault));
+  *c->h_err = 0;
+  for (auto &sl : c->slot) {
+    HPGQ_HIP_TRY(hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming));
+    HPGQ_HIP_TRY(hipEventCreateWithFlags(&sl.used, hipEventDisableTiming));
+  }
   int cus = 0;
   HPGQ_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
   rc = plan(c, cus);
@@ -441,12 +461,18 @@ void hpgq_close(hpgq_ctx_t *c) {
   (void)hipFree(c->d_state);
   (void)hipFree(c->d_global);
   (void)hipFree(c->d_cold);
+  if (c->cstream) (void)hipStreamSynchronize(c->cstream);
   (void)hipFree(c->d_bits1);
   (void)hipFree(c->d_bits2);
-  (void)hipFree(c->d_buf);
-  (void)hipFree(c->d_mask);
-  (void)hipFree(c->d_trim);
+  for (auto &sl : c->slot) {
+    (void)hipFree(sl.d);
+    if (sl.h) (void)hipHostFree(sl.h);
+    if (sl.copied) (void)hipEventDestroy(sl.copied);
+    if (sl.used) (void)hipEventDestroy(sl.used);
+  }
+  if (c->h_err) (void)hipHostFree(c->h_err);
   if (c->h_report) (void)hipHostFree(c->h_report);
+  if (c->cstream) (void)hipStreamDestroy(c->cstream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }
@@ -563,23 +589,51 @@ int hpgq_run_device(hpgq_ctx_t *c, const hpgq_batch_t *b, const hpgq_batch_t *b2
   return launch(c, A);
 }
 
-static int ensure_dev(hpgq_ctx *c, size_t bytes, size_t nreads) {
-  if (bytes > c->d_buf_cap) {
-    HPGQ_HIP_TRY(hipStreamSynchronize(c->stream));
-    (void)hipFree(c->d_buf);
-    c->d_buf = nullptr;
-    size_t cap = bytes + bytes / 4 + 4096;
-    if (hipMalloc(&c->d_buf, cap) != hipSuccess) { c->d_buf_cap = 0; return HPGQ_E_NOMEM; }
-    c->d_buf_cap = cap;
+// hand a slot's finished outputs to the caller's arrays (its D2H is done)
+static void slot_deliver(hpgq_ctx::Slot &sl) {
+  if (sl.mask_dst) std::memcpy(sl.mask_dst, sl.h + sl.mask_off, sl.nreads);
+  if (sl.trim_dst) std::memcpy(sl.trim_dst, sl.h + sl.trim_off, sl.ntrim * sizeof(uint32_t));
+  sl.mask_dst = nullptr;
+  sl.trim_dst = nullptr;
+  sl.busy = false;
+}
+
+// a slot for the next batch: its previous batch finished (outputs delivered)
+// and room for `bytes` in both of its buffers
+static int slot_acquire(hpgq_ctx *c, size_t bytes, hpgq_ctx::Slot *&out) {
+  c->cur_slot ^= 1;
+  hpgq_ctx::Slot &sl = c->slot[c->cur_slot];
+  if (sl.busy) {
+    HPGQ_HIP_TRY(hipEventSynchronize(sl.used));
+    slot_deliver(sl);
   }
-  if (nreads > c->d_out_cap) {
-    HPGQ_HIP_TRY(hipStreamSynchronize(c->stream));
-    (void)hipFree(c->d_mask);
-    (void)hipFree(c->d_trim);
-    size_t cap = nreads + nreads / 4 + 64;
-    if (hipMalloc(&c->d_mask, cap) != hipSuccess) return HPGQ_E_NOMEM;
-    if (hipMalloc(&c->d_trim, cap * 2 * sizeof(uint32_t)) != hipSuccess) return HPGQ_E_NOMEM;
-    c->d_out_cap = cap;
+  if (bytes > sl.cap) {
+    (void)hipFree(sl.d);
+    if (sl.h) (void)hipHostFree(sl.h);
+    sl.d = nullptr;
+    sl.h = nullptr;
+    sl.cap = 0;
+    const size_t cap = bytes + bytes / 4 + 4096;
+    if (hipMalloc(&sl.d, cap) != hipSuccess) return HPGQ_E_NOMEM;
+    if (hipHostMalloc(reinterpret_cast<void **>(&sl.h), cap, hipHostMallocDefault) != hipSuccess) {
+      sl.h = nullptr;
+      return HPGQ_E_NOMEM;
+    }
+    sl.cap = cap;
+  }
+  out = &sl;
+  return HPGQ_OK;
+}
+
+// the caller's bytes into the slot's pinned buffer, each kChunk piece's H2D
+// queued on the copy stream as soon as it is filled (the DMA of one piece
+// overlaps the memcpy of the next)
+static int stage_copy(hpgq_ctx *c, hpgq_ctx::Slot &sl, size_t off, const void *src, size_t bytes) {
+  constexpr size_t kChunk = (size_t)1 << 20;
+  for (size_t o = 0; o < bytes; o += kChunk) {
+    const size_t n = std::min(kChunk, bytes - o);
+    std::memcpy(sl.h + off + o, static_cast<const char *>(src) + o, n);
+    HPGQ_HIP_TRY(hipMemcpyAsync(sl.d + off + o, sl.h + off + o, n, hipMemcpyHostToDevice, c->cstream));
   }
   return HPGQ_OK;
 }
@@ -594,50 +648,70 @@ int hpgq_run_host(hpgq_ctx_t *c, const hpgq_batch_t *b, const hpgq_batch_t *b2,
   if (n == 0) return HPGQ_OK;
   HPGQ_HIP_TRY(hipSetDevice(c->device));
   const hpgq_batch_t *bs[2] = {b, b2};
-  size_t bytes[2] = {0, 0}, off[2][4];
+  size_t bytes[2] = {0, 0}, off[2][3];
   size_t total = 0;
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
   for (int m = 0; m < c->nm; ++m) {
     const int32_t *ix = bs[m]->data_indices;
     bytes[m] = (size_t)(ix[n] - ix[0]);
-    off[m][0] = total; total += (bytes[m] + HPGQ_DEVICE_SLACK + 255) & ~(size_t)255;   // seq
-    off[m][1] = total; total += (bytes[m] + HPGQ_DEVICE_SLACK + 255) & ~(size_t)255;   // quality
-    off[m][2] = total; total += ((size_t)(n + 1) * 4 + 255) & ~(size_t)255;
+    off[m][0] = total; total += al(bytes[m] + HPGQ_DEVICE_SLACK);   // seq
+    off[m][1] = total; total += al(bytes[m] + HPGQ_DEVICE_SLACK);   // quality
+    off[m][2] = total; total += al((size_t)(n + 1) * 4);            // data_indices
   }
-  int rc = ensure_dev(c, total, (size_t)n);
+  const size_t mask_off = total;
+  total += al((size_t)n);
+  const size_t trim_off = total;
+  total += al((size_t)n * c->nm * 4);
+  hpgq_ctx::Slot *sp = nullptr;
+  int rc = slot_acquire(c, total, sp);
   if (rc) return rc;
+  hpgq_ctx::Slot &sl = *sp;
   hpgq::EngineArgs A{};
   fill_args(c, A);
   A.num_reads = n;
   for (int m = 0; m < c->nm; ++m) {
     const int32_t *ix = bs[m]->data_indices;
-    char *ds = c->d_buf + off[m][0], *dq = c->d_buf + off[m][1];
-    int32_t *di = reinterpret_cast<int32_t *>(c->d_buf + off[m][2]);
-    HPGQ_HIP_TRY(hipMemcpyAsync(ds, bs[m]->seq + ix[0], bytes[m], hipMemcpyHostToDevice, c->stream));
-    HPGQ_HIP_TRY(hipMemcpyAsync(dq, bs[m]->quality + ix[0], bytes[m], hipMemcpyHostToDevice, c->stream));
-    HPGQ_HIP_TRY(hipMemcpyAsync(di, ix, (size_t)(n + 1) * 4, hipMemcpyHostToDevice, c->stream));
+    if ((rc = stage_copy(c, sl, off[m][2], ix, (size_t)(n + 1) * 4))) return rc;
+    if ((rc = stage_copy(c, sl, off[m][0], bs[m]->seq + ix[0], bytes[m]))) return rc;
+    if ((rc = stage_copy(c, sl, off[m][1], bs[m]->quality + ix[0], bytes[m]))) return rc;
     // absolute indices: shift the base pointers so data_indices need no rewrite
-    A.seq[m] = ds - ix[0];
-    A.qual[m] = dq - ix[0];
-    A.idx[m] = di;
+    A.seq[m] = sl.d + off[m][0] - ix[0];
+    A.qual[m] = sl.d + off[m][1] - ix[0];
+    A.idx[m] = reinterpret_cast<int32_t *>(sl.d + off[m][2]);
   }
-  A.mask = mask_out ? c->d_mask : nullptr;
-  A.trim = trim_out ? c->d_trim : nullptr;
+  HPGQ_HIP_TRY(hipEventRecord(sl.copied, c->cstream));
+  HPGQ_HIP_TRY(hipStreamWaitEvent(c->stream, sl.copied, 0));
+  A.mask = mask_out ? reinterpret_cast<uint8_t *>(sl.d + mask_off) : nullptr;
+  A.trim = trim_out ? reinterpret_cast<uint32_t *>(sl.d + trim_off) : nullptr;
   rc = launch(c, A);
   if (rc) return rc;
-  if (mask_out) HPGQ_HIP_TRY(hipMemcpyAsync(mask_out, c->d_mask, (size_t)n, hipMemcpyDeviceToHost, c->stream));
+  if (mask_out)
+    HPGQ_HIP_TRY(hipMemcpyAsync(sl.h + mask_off, sl.d + mask_off, (size_t)n, hipMemcpyDeviceToHost, c->stream));
   if (trim_out)
-    HPGQ_HIP_TRY(hipMemcpyAsync(trim_out, c->d_trim, (size_t)n * c->nm * 4, hipMemcpyDeviceToHost,
+    HPGQ_HIP_TRY(hipMemcpyAsync(sl.h + trim_off, sl.d + trim_off, (size_t)n * c->nm * 4, hipMemcpyDeviceToHost,
                                 c->stream));
+  HPGQ_HIP_TRY(hipEventRecord(sl.used, c->stream));
+  sl.busy = true;
+  sl.mask_dst = mask_out;
+  sl.trim_dst = trim_out;
+  sl.mask_off = mask_off;
+  sl.trim_off = trim_off;
+  sl.nreads = (size_t)n;
+  sl.ntrim = (size_t)n * c->nm;
   return HPGQ_OK;
 }
 
 int hpgq_sync(hpgq_ctx_t *c) {
   if (!c) return HPGQ_E_INVALID;
   HPGQ_HIP_TRY(hipSetDevice(c->device));
+  // the error flag rides back on the stream: no blocking copy after the sync
+  HPGQ_HIP_TRY(hipMemcpyAsync(c->h_err, c->d_flags + FL_ERR, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
   HPGQ_HIP_TRY(hipStreamSynchronize(c->stream));
-  int32_t err = 0;
-  HPGQ_HIP_TRY(hipMemcpy(&err, c->d_flags + FL_ERR, sizeof(err), hipMemcpyDeviceToHost));
-  return err ? HPGQ_E_READ_TOO_LONG : HPGQ_OK;
+  for (int k = 0; k < 2; ++k) {   // the older slot first (input order of the outputs is per slot anyway)
+    hpgq_ctx::Slot &sl = c->slot[c->cur_slot ^ 1 ^ k];
+    if (sl.busy) slot_deliver(sl);
+  }
+  return *c->h_err ? HPGQ_E_READ_TOO_LONG : HPGQ_OK;
 }
 
 int hpgq_reset(hpgq_ctx_t *c) {

@@ -207,9 +207,13 @@ int  hpgq_run_device(hpgq_ctx_t *ctx, const hpgq_batch_t *b, const hpgq_batch_t 
                      uint8_t *mask_out, uint32_t *trim_out);
 
 /*
- * Host path: pointers are HOST memory.  Copies the batch to the device
- * (pinned staging, async), runs the kernel and copies mask/trim back; the
- * outputs are valid after hpgq_sync().
+ * Host path: pointers are HOST memory (any: malloc'd is fine).  The batch is
+ * copied into one of the ctx's two page-locked staging slots (1 MB pieces,
+ * each piece's H2D queued as soon as it is copied) and the call returns once
+ * the caller's buffers have been read: they are reusable on return.  The
+ * copies run on a second stream, so this batch's H2D overlaps the previous
+ * batch's kernels.  mask_out / trim_out are filled by hpgq_sync() (or when the
+ * slot is reused two calls later), not before.
  */
 int  hpgq_run_host(hpgq_ctx_t *ctx, const hpgq_batch_t *b, const hpgq_batch_t *b2,
                    uint8_t *mask_out, uint32_t *trim_out);
@@ -229,9 +233,10 @@ size_t hpgq_counters_size(const hpgq_ctx_t *ctx);
 /* Copy the counters to host memory (synchronises the ctx). */
 int  hpgq_read_counters(hpgq_ctx_t *ctx, uint64_t *out, size_t n);
 
-/* No-op kept for ABI compatibility: the kernels add their workgroup partials
- * into the counters themselves (global atomics), so the counter buffer holds
- * the totals as soon as the ctx stream has run the batch. */
+/* DEPRECATED no-op, kept only so that round-1 callers still link: the kernels
+ * add their workgroup partials into the counters themselves (global
+ * atomics), so the counter buffer holds the totals as soon as the ctx stream
+ * has run the batch.  New code does not call it. */
 int  hpgq_fold(hpgq_ctx_t *ctx);
 
 /* Device pointer of this ctx's own counter buffer (for an external

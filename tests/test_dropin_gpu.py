@@ -1,0 +1,80 @@
+"""The drop-in binding as INTEGRATION.md writes it (tools/dropin_bench.c):
+malloc'd SoA batches of the reference's 10,000 reads (src/stats_options.c:22)
+packed from AoS reads, hpgq_run_host + hpgq_sync per batch, one ctx per worker
+thread (src/stats_options.c:21: 2 threads) -- the summed counters and every
+mask equal the oracle's over the same FASTQ file.  Also the host path's
+contract: several hpgq_run_host calls in flight before one hpgq_sync."""
+import ctypes as C
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import hpgfastq as H
+import oracle_lib as O
+from fastq_io import read_fastq
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HARNESS = os.path.join(ROOT, "tools", "dropin_bench")
+
+
+@pytest.fixture(scope="module")
+def fastq(tmp_path_factory):
+    d = tmp_path_factory.mktemp("dropin")
+    gen = str(d / "fqgen")
+    subprocess.run(["gcc", "-O2", "-fopenmp", os.path.join(ROOT, "tools", "fqgen.c"), "-o", gen], check=True)
+    path = str(d / "in.fq")
+    subprocess.run([gen, path, "123457", "150", "2"], check=True)
+    return path
+
+
+@pytest.mark.parametrize("threads,batch", [(2, 10000), (1, 997), (3, 4096)])
+def test_dropin_worker_matches_oracle(fastq, tmp_path, threads, batch):
+    assert os.path.exists(HARNESS), "build with make -C hpg-fastq_amd"
+    ctr, msk = str(tmp_path / "ctr.bin"), str(tmp_path / "mask.bin")
+    out = subprocess.run([HARNESS, fastq, "--batch", str(batch), "--threads", str(threads), "--c2",
+                          "--counters", ctr, "--mask", msk], check=True, capture_output=True, text=True,
+                         timeout=300)
+    rec = json.loads(out.stdout.strip().splitlines()[-1])
+    reads = read_fastq(fastq)
+    assert rec["reads"] == reads.n
+    p = H.stats_params(lmax=1024, read_quality_range="20,", read_length_range="50,")
+    m_o, _t, c_o = O.run(p, reads)
+    np.testing.assert_array_equal(np.fromfile(msk, np.uint8), m_o)
+    np.testing.assert_array_equal(np.fromfile(ctr, np.uint64), c_o)
+
+
+@pytest.mark.parametrize("edit", [False, True])
+def test_host_path_calls_in_flight(edit):
+    """Five hpgq_run_host calls before one hpgq_sync: the two staging slots
+    are reused, every batch's mask / trims reach its own arrays, and the
+    caller's input buffers are free to change as soon as a call returns."""
+    if edit:
+        p = H.edit_params(lmax=150, stats=True, left_length=10, left_quality_range="20,",
+                          right_length=30, right_quality_range="20,", max_N=2)
+    else:
+        p = H.stats_params(lmax=150, read_quality_range="20,", read_length_range="50,")
+    batches = [O.synth(n, seed=40 + i, L=150, trunc_pct=10, n_per_1024=8, first=1000 * i)
+               for i, n in enumerate([30000, 1, 25000, 7777, 40000])]
+    masks = [np.full(b.n, 7, np.uint8) for b in batches]
+    trims = [np.zeros(b.n, np.uint32) for b in batches]
+    with H.Engine(p) as e:
+        for b, m, t in zip(batches, masks, trims):
+            seq, qual = b.seq.copy(), b.qual.copy()
+            hb = H.engine.host_batch(seq, qual, b.idx)
+            e.run_host(hb, None, m, t if edit else None)
+            seq[:] = ord("N")   # reused by the caller right away
+            qual[:] = 0
+        e.sync()
+        got = e.counters()
+    want = np.zeros_like(got)
+    for b, m, t in zip(batches, masks, trims):
+        m_o, t_o, c_o = O.run(p, b)
+        np.testing.assert_array_equal(m, m_o)
+        if edit:
+            np.testing.assert_array_equal(t, t_o)
+        want += c_o
+    np.testing.assert_array_equal(got, want)
