@@ -86,6 +86,10 @@ CONFIGS = {
                   unit="Mpairs/s", reads=50_000_000, batch=10_000_000, L=150, seed=4,
                   workload="C4 trims on paired-end 2x150 + --read-quality-range 20, "
                            "(pair kept iff both mates pass; old/main_hpg_fastq_old.c:728)"),
+    "dropin": dict(metric="Mreads/s (150 bp) stats+filter through hpgq_run_host, 10,000-read malloc'd batches",
+                   unit="Mreads/s", reads=4_000_000, batch=10_000, L=150, seed=2,
+                   workload="INTEGRATION.md's fastq_stats_worker: AoS reads packed per 10,000-read batch, "
+                            "hpgq_run_host + hpgq_sync, 2 worker threads with one ctx each (src/stats_options.c:21-22)"),
     "c2_lr": dict(metric="Mreads/s (150 bp) stats+filter with a 5' window filter",
                   unit="Mreads/s", reads=100_000_000, batch=10_000_000, L=150, seed=2,
                   workload="C2 flags + --left-length 10 --left-quality-range 20,"),
@@ -101,6 +105,7 @@ def parse():
     ap.add_argument("--reads", type=int, default=None, help="reads (pairs) per GPU")
     ap.add_argument("--batch-reads", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end CLI leg (C2)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--lmax", type=int, default=None, help="override the config's lmax")
     a = ap.parse_args()
@@ -290,6 +295,123 @@ def read_status(n, seed, first=0):
     return ((x % np.uint64(100)) >= np.uint64(5)).astype(np.uint8)
 
 
+# ---- end to end: FASTQ file -> the CLI (SURVEY §8d's second throughput) -----
+E2E_READS = 5_000_000
+
+
+def numa_cpus(device):
+    """The CPUs of `device`'s NUMA node this process may use (empty: unknown)."""
+    node = H.lib.hpgq_device_numa_node(device)
+    if node < 0:
+        return set()
+    try:
+        spec = open(f"/sys/devices/system/node/node{node}/cpulist").read().strip()
+    except OSError:
+        return set()
+    cpus = set()
+    for part in spec.split(","):
+        a, _, b = part.partition("-")
+        cpus.update(range(int(a), int(b or a) + 1))
+    return cpus & os.sched_getaffinity(0)
+
+
+def e2e_leg(args, device, runs=5):
+    """`hpg-fastq stats --read-quality-range 20, --read-length-range 50,` on a
+    synthetic FASTQ file in /dev/shm (tools/fqgen.c: the same generator,
+    E2E_READS x 150 bp, written by threads on the GPU's NUMA node so the file's
+    pages sit there), `runs` back-to-back CLI runs on this one GPU; the CLI's
+    own throughput line (text read -> parse -> engine, its clock starting after
+    device set-up) per run.  PCIe-inclusive: NOT the bench value."""
+    import re
+    import subprocess
+    import tempfile
+    cli = os.path.join(ROOT, "hpg-fastq_amd", "hpg-fastq")
+    if not os.path.exists(cli):
+        return {"error": "hpg-fastq not built"}
+    tmp = tempfile.mkdtemp(prefix="hpgq_e2e_")
+    gen = os.path.join(tmp, "fqgen")
+    shm = "/dev/shm" if os.path.isdir("/dev/shm") else tmp
+    fq = os.path.join(shm, f"hpgq_e2e_{os.getpid()}.fq")
+    cpus = numa_cpus(device)
+    share = sorted(cpus)[:omp_threads(len(cpus) or 16)] if cpus else None
+
+    def pin():
+        if share:
+            os.sched_setaffinity(0, share)
+    out = {"reads": E2E_READS, "read_length": 150, "runs": runs,
+           "command": "hpg-fastq stats -f <file> --read-quality-range 20, --read-length-range 50, "
+                      f"--gpus 1 --num-threads {len(share) if share else 16}",
+           "numa_cpus": len(share) if share else None}
+    try:
+        subprocess.run(["gcc", "-O2", "-fopenmp", os.path.join(ROOT, "tools", "fqgen.c"), "-o", gen],
+                       check=True, capture_output=True, timeout=120)
+        subprocess.run([gen, fq, str(E2E_READS), "150", "2"], check=True, capture_output=True, timeout=300,
+                       preexec_fn=pin, env=dict(os.environ, OMP_NUM_THREADS=str(len(share) if share else 16)))
+        out["fastq_gb"] = round(os.path.getsize(fq) / 1e9, 3)
+        vals, gbs = [], []
+        for _ in range(runs):
+            r = subprocess.run([cli, "stats", "-f", fq, "-o", tmp, "--read-quality-range", "20,",
+                                "--read-length-range", "50,", "--gpus", "1", "--gpu", str(device),
+                                "--num-threads", str(len(share) if share else 16)],
+                               check=True, capture_output=True, text=True, timeout=300)
+            m = re.search(r"Throughput: (\d+) reads, ([0-9.]+) GB of FastQ in ([0-9.]+) s = ([0-9.]+) Mreads/s",
+                          r.stdout)
+            if not m:
+                return dict(out, error="no throughput line")
+            vals.append(float(m.group(4)))
+            gbs.append(float(m.group(2)) / float(m.group(3)))
+        out.update(mreads_s=round(float(np.median(vals)), 2), mreads_s_runs=[round(v, 2) for v in vals],
+                   gb_s_fastq=round(float(np.median(gbs)), 2))
+    except (OSError, subprocess.SubprocessError) as e:
+        out["error"] = str(e)[:200]
+    finally:
+        for f in (fq, gen):
+            try:
+                os.remove(f)
+            except OSError:
+                pass
+        import shutil
+        shutil.rmtree(tmp, ignore_errors=True)
+    return out
+
+
+def dropin_main(args):
+    """--config dropin: INTEGRATION.md's worker (tools/dropin_bench.c) on 10,000-read
+    batches from malloc'd buffers, 2 worker threads with one ctx each, over a
+    synthetic FASTQ file (reads loaded as AoS before the clock starts)."""
+    import subprocess
+    import tempfile
+    harness = os.path.join(ROOT, "tools", "dropin_bench")
+    tmp = tempfile.mkdtemp(prefix="hpgq_dropin_")
+    gen = os.path.join(tmp, "fqgen")
+    fq = os.path.join("/dev/shm" if os.path.isdir("/dev/shm") else tmp, f"hpgq_dropin_{os.getpid()}.fq")
+    n = args.reads if args.reads != CONFIGS["dropin"]["reads"] else CONFIGS["dropin"]["reads"]
+    try:
+        subprocess.run(["gcc", "-O2", "-fopenmp", os.path.join(ROOT, "tools", "fqgen.c"), "-o", gen],
+                       check=True, capture_output=True, timeout=120)
+        subprocess.run([gen, fq, str(n), "150", "2"], check=True, capture_output=True, timeout=300)
+        r = subprocess.run([harness, fq, "--threads", "2", "--batch", str(args.batch_reads), "--c2",
+                            "--lmax", "1024", "--repeat", str(args.steps)],
+                           check=True, capture_output=True, text=True, timeout=600)
+        rec = json.loads(r.stdout.strip().splitlines()[-1])
+    finally:
+        for f in (fq, gen):
+            try:
+                os.remove(f)
+            except OSError:
+                pass
+        os.rmdir(tmp)
+    cfg = CONFIGS["dropin"]
+    out = {"metric": cfg["metric"], "value": rec["mreads_s"], "unit": cfg["unit"], "n_gpus": 1,
+           "steps": args.steps, "warmup": 0, "ms_per_step": round(rec["best_s"] * 1e3, 3),
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+           "data": "synthetic FASTQ (tools/fqgen.c), host memory",
+           "config": {"workload": cfg["workload"], "reads": rec["reads"], "batch_reads": rec["batch_reads"],
+                      "threads": rec["threads"], "lmax": 1024},
+           "harness": rec}
+    print(json.dumps(out), flush=True)
+
+
 # ---- resident synthetic shard ----------------------------------------------
 def make_batches(args, rank, dev, mates):
     import torch
@@ -321,6 +443,8 @@ def make_batches(args, rank, dev, mates):
 
 def main():
     args = parse()
+    if args.config == "dropin":
+        return dropin_main(args)
     cfg = CONFIGS[args.config]
     import torch
     import torch.distributed as dist
@@ -479,9 +603,14 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, params)
+    if rank == 0 and world == 1 and args.config == "c2" and not args.no_e2e:
+        eng.close()   # (the CLI runs in its own process)
+        eng = None
+        out["e2e"] = e2e_leg(args, local)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    eng.close()
+    if eng is not None:
+        eng.close()
     if world > 1:
         dist.destroy_process_group()
 

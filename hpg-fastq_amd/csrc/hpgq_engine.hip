@@ -10,6 +10,7 @@
 // C-ABI
 // ===========================================================================
 
+#include <cctype>
 #include <climits>
 #include <cstdio>
 #include <cstdlib>
@@ -394,6 +395,20 @@ int hpgq_device_count(void) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess) return 0;
   return n;
+}
+
+int hpgq_device_numa_node(int device) {
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, (int)sizeof(bus), device) != hipSuccess) return -1;
+  for (char *q = bus; *q; ++q) *q = (char)std::tolower((unsigned char)*q);   // sysfs names are lower case
+  char path[128];
+  std::snprintf(path, sizeof(path), "/sys/bus/pci/devices/%s/numa_node", bus);
+  FILE *f = std::fopen(path, "r");
+  if (!f) return -1;
+  int node = -1;
+  if (std::fscanf(f, "%d", &node) != 1) node = -1;
+  std::fclose(f);
+  return node;
 }
 
 static int validate_params(const hpgq_params_t *p) {

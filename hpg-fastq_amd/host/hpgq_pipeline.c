@@ -34,6 +34,7 @@
 #include <errno.h>
 #include <fcntl.h>
 #include <pthread.h>
+#include <sched.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -98,6 +99,46 @@ static double now_s(void) {
   return t.tv_sec + 1e-9 * t.tv_nsec;
 }
 
+/* ---- NUMA placement --------------------------------------------------------- */
+
+/* Run this process's threads (reader, GPU workers, writer -- created after
+ * this call, so they inherit it) on the CPUs of the GPUs' NUMA node, within
+ * the CPUs it may use, and so allocate the page-locked chunks there (first
+ * touch): the reader's copies and the chunks' H2D stay on the GPU's side of
+ * the socket link.  Skipped when the GPUs sit on different nodes, the node is
+ * unknown, or it holds none of the allowed CPUs. */
+static void bind_numa(const cli_options_t *o, int ngpus, int ndev) {
+  int node = -2;
+  for (int g = 0; g < ngpus && g < ndev; ++g) {
+    const int nd = hpgq_device_numa_node((o->device + g) % ndev);
+    if (nd < 0 || (node != -2 && nd != node)) return;
+    node = nd;
+  }
+  if (node < 0) return;
+  char path[96], list[4096];
+  snprintf(path, sizeof(path), "/sys/devices/system/node/node%d/cpulist", node);
+  FILE *f = fopen(path, "r");
+  if (!f) return;
+  const int ok = fgets(list, sizeof(list), f) != NULL;
+  fclose(f);
+  if (!ok) return;
+  cpu_set_t allowed, want;
+  if (sched_getaffinity(0, sizeof(allowed), &allowed)) return;
+  CPU_ZERO(&want);
+  for (char *p = list; *p && *p != '\n';) {   /* "a-b,c,d-e" */
+    char *e;
+    long a = strtol(p, &e, 10), b = a;
+    if (e == p) break;
+    if (*e == '-') b = strtol(e + 1, &e, 10);
+    for (long c = a; c <= b && c < CPU_SETSIZE; ++c)
+      if (CPU_ISSET((int)c, &allowed)) CPU_SET((int)c, &want);
+    p = *e == ',' ? e + 1 : e;
+  }
+  if (CPU_COUNT(&want) == 0) return;
+  if (sched_setaffinity(0, sizeof(want), &want) == 0 && getenv("HPGQ_TRACE"))
+    fprintf(stderr, "hpg-fastq: threads on NUMA node %d (%d CPUs)\n", node, CPU_COUNT(&want));
+}
+
 /* ---- reader ------------------------------------------------------------- */
 
 typedef struct {
@@ -114,7 +155,11 @@ static void *pread_worker(void *arg) {
   while (done < j->n) {
     ssize_t r = pread(j->fd, j->dst + done, j->n - done, j->off + (off_t)done);
     if (r < 0 && errno == EINTR) continue;
-    if (r <= 0) break;
+    if (r < 0) {
+      j->got = -1;
+      return NULL;
+    }
+    if (r == 0) break;
     done += (size_t)r;
   }
   j->got = (ssize_t)done;
@@ -142,13 +187,14 @@ static ssize_t read_parallel(pipe_t *P, char *dst, size_t n) {
     started++;
   }
   ssize_t total = 0;
-  int short_read = 0;
+  int short_read = 0, failed = 0;
   for (int i = 0; i < started; ++i) {
     pthread_join(th[i], NULL);
-    if (!short_read) total += jobs[i].got;
-    if ((size_t)jobs[i].got < jobs[i].n) short_read = 1;   /* EOF inside this piece */
+    if (jobs[i].got < 0) failed = 1;
+    if (!short_read && jobs[i].got > 0) total += jobs[i].got;
+    if (jobs[i].got < 0 || (size_t)jobs[i].got < jobs[i].n) short_read = 1;   /* EOF inside this piece */
   }
-  return total;
+  return failed ? -1 : total;
 }
 
 static void reader_fail(pipe_t *P, int code) {
@@ -180,7 +226,10 @@ static void *reader_main(void *arg) {
         const size_t want = (size_t)(target - g0) < s->cap - 1 ? (size_t)(target - g0) : s->cap - 1;
         if (want > s->len) {
           const ssize_t got = read_parallel(P, s->buf + s->len, want - s->len);
-          if (got < 0) break;
+          if (got < 0) {
+            use = -1;   /* an I/O error, reported as such below */
+            break;
+          }
           P->pos += got;
           s->len += (size_t)got;
         }
@@ -194,12 +243,16 @@ static void *reader_main(void *arg) {
       const size_t room = s->cap - 1 - s->len;   /* 1 byte for a final newline */
       const ssize_t got = read_parallel(P, s->buf + s->len, room);
       if (got < 0) {
-        reader_fail(P, -1);
+        reader_fail(P, HPGQ_E_IO);
         break;
       }
       P->pos += got;
       s->len += (size_t)got;
       s->eof = P->pos >= P->size;
+    }
+    if (use < 0) {
+      reader_fail(P, HPGQ_E_IO);
+      break;
     }
     if (s->eof && s->len > 0 && s->buf[s->len - 1] != '\n') s->buf[s->len++] = '\n';
     if (s->eof || P->cg_batch <= 0) use = hpgq_fastq_complete_prefix(s->buf, (int64_t)s->len, s->eof);
@@ -465,7 +518,12 @@ int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, 
   int G = ngpus * (o->gpu_workers > 0 ? o->gpu_workers : 1);
   if (G > MAX_WORKERS) G = MAX_WORKERS;
   P.nworkers = G;
-  P.nslots = 2 * G + 1;   /* reader + G workers + writer, with room to run ahead */
+  /* one slot per worker + the reader's + the writer's + one to run ahead (a
+   * bound that does not double with the worker count: 16 workers of 256 MB
+   * chunks would otherwise pin 10 GB) */
+  P.nslots = G + 3;
+  if (P.nslots > MAX_SLOTS) P.nslots = MAX_SLOTS;
+  bind_numa(o, ngpus, ndev);
   P.cg_batch = o->cg_on ? o->cg_batch_size : 0;
   worker_t W[MAX_WORKERS];
   memset(W, 0, sizeof(W));
@@ -480,6 +538,10 @@ int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, 
   /* a chunk holds --chunk-mb of text (with --cg: one chaos-game batch) */
   size_t chunk = (size_t)o->chunk_mb << 20;
   if (P.cg_batch > 0 && (size_t)P.cg_batch > chunk) chunk = (size_t)P.cg_batch;
+  const double pinned_gb = (double)P.nslots * (double)(chunk + MAX_CARRY) / 1e9;
+  if (pinned_gb > 4.0)
+    fprintf(stderr, "hpg-fastq: %d chunks of %zu MB: %.1f GB of page-locked host memory\n", P.nslots,
+            (chunk + MAX_CARRY) >> 20, pinned_gb);
   for (int i = 0; i < P.nslots && rc == 0; ++i) {
     P.slot[i].cap = chunk + MAX_CARRY;
     rc = hpgq_host_alloc((void **)&P.slot[i].buf, P.slot[i].cap);

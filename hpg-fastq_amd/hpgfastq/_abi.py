@@ -150,6 +150,7 @@ _SIGS = [
     ("hpgq_parse_records", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     ("hpgq_parser_stream", C.c_void_p, [C.c_void_p]),
     ("hpgq_device_count", C.c_int, []),
+    ("hpgq_device_numa_node", C.c_int, [C.c_int]),
     ("hpgq_strerror", C.c_char_p, [C.c_int]),
     ("hpgq_version", C.c_char_p, []),
     ("hpgq_kernel_name", C.c_char_p, [C.c_void_p]),

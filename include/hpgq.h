@@ -446,6 +446,9 @@ int  hpgq_synth_device(const hpgq_synth_t *s, int64_t first, int64_t n,
 
 /* number of visible HIP devices (0 when none or the runtime fails) */
 int  hpgq_device_count(void);
+/* NUMA node of HIP device `device` (its PCI function's numa_node in sysfs),
+ * -1 when unknown: host threads and buffers that feed it belong there */
+int  hpgq_device_numa_node(int device);
 
 const char *hpgq_strerror(int code);
 const char *hpgq_version(void);
