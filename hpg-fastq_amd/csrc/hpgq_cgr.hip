@@ -33,6 +33,7 @@
 // replay for those reads only.  The word count does not depend on f, so it is
 // exact from the first kernel.
 #include <rccl/rccl.h>
+#include <climits>
 #include <cstring>
 #include "hpgq_common.h"
 
@@ -826,7 +827,8 @@ int hpgq_cgr_fill_device(hpgq_cgr_t *c, const hpgq_batch_t *b, const uint8_t *st
   c->reduced = false;
   const bool valid = mode == HPGQ_CGR_ONLY_VALID_READS;
   if (valid && !status) return HPGQ_OK;   // no status array: every read is skipped (:188)
-  const bool streamed = c->path == HPGQ_CGR_PATH_AUTO && c->k <= hpgq::cgr::stream::kMaxK;
+  const bool streamed = c->path == HPGQ_CGR_PATH_AUTO && c->k <= hpgq::cgr::stream::kMaxK &&
+                        b->num_reads < INT32_MAX;   // (32-bit read cursors)
   if (!streamed) return cgr_exact(c, b, status, mode);
   namespace S = hpgq::cgr::stream;
   if ((int)c->pending.size() == S::kSlots) {   // out of slots: settle the ones in flight

@@ -63,10 +63,10 @@
 // finish moves it into the reference layout (or discards it when the gate is
 // set).  A run of >= kRun (>= 41) D-moves spans at least three aligned 16-byte
 // chunks, and a chunk wholly inside it holds no Z on that axis; so only tiles
-// with a Z-free chunk (VALID: a Z-free chunk that holds a D move -- a run's
-// interior chunks hold >= 9 of its D moves, so one of them does, while wholly
-// skipped stretches do not trigger) or entered with a long open run are
-// scanned exactly, lane by lane.
+// with a Z-free chunk (a tile holding skipped bytes: see run_candidate) or
+// entered with a long open run are scanned exactly (one segmented DPP scan
+// per axis, tile_runs); the run open at such a tile's start is walked back
+// for only when its bound would decide.
 #pragma once
 
 namespace hpgq {
@@ -96,7 +96,7 @@ constexpr uint32_t kV1Hi = 0x01000001u;
 constexpr uint32_t kDLo = 0x00000100u;    // D moves x | y << 1: A 1, C 0
 constexpr uint32_t kDHi = 0x02000003u;    //                     T 3, G 2, N 0
 
-struct SArgs {
+struct SArgs {   // (read indices fit 31 bits: the host sends larger batches to the exact path)
   const char *seq, *qual;
   const int32_t *idx;
   const uint8_t *status;            // VALID: read_status[] (1 = VALID_READ)
@@ -159,15 +159,13 @@ struct Cls {
   uint32_t p0, p1;     // the 32 codes packed, byte j at bits 2j of the 64-bit p1:p0
   uint32_t v;          // bit j: byte j is A/C/G/T
   uint32_t zlo, zhi;   // OR of per-byte Z bits (bit0 x, bit1 y) over the first / last 16 bytes
-  uint32_t dlo, dhi;   // VALID: the same for D moves
   uint32_t bad;        // nonzero: a byte that is not exactly A/C/G/T/N
 };
 
-template <bool VALID>
 __device__ __forceinline__ Cls classify(const uint32_t s[kNdw]) {
   static_assert(kNdw == 8, "the packed code stream assumes 32 bytes per lane");
   Cls c;
-  uint32_t bad = 0, zl = 0, zh = 0, dl = 0, dh = 0, vp[kNdw / 2], g[kNdw];
+  uint32_t bad = 0, zl = 0, zh = 0, vp[kNdw / 2], g[kNdw];
 #pragma unroll
   for (int d = 0; d < kNdw; ++d) {
     const uint32_t code = s[d] & 0x07070707u;
@@ -178,11 +176,6 @@ __device__ __forceinline__ Cls classify(const uint32_t s[kNdw]) {
     // Z bits: a Z move on x is x = 0 (C/G), on y is y = 0 (A/C): ~code & 3
     if (d < 4) zl = __builtin_amdgcn_bitop3_b32(zl, c.cd[d], 0x03030303u, 0xF2);   // zl | (~cd & 3s)
     if (d >= kNdw - 4) zh = __builtin_amdgcn_bitop3_b32(zh, c.cd[d], 0x03030303u, 0xF2);
-    if (VALID) {
-      const uint32_t dm = __builtin_amdgcn_perm(kDHi, kDLo, code);
-      if (d < 4) dl |= dm;
-      else dh |= dm;
-    }
     // the V bit of byte j to bit j: byte weights 1,2,4,8 (<< 4 for odd dwords) by v_dot4
     const uint32_t v1 = __builtin_amdgcn_perm(kV1Hi, kV1Lo, code);
     vp[d >> 1] = (d & 1) ? __builtin_amdgcn_udot4(v1, 0x80402010u, vp[d >> 1], false)
@@ -195,56 +188,101 @@ __device__ __forceinline__ Cls classify(const uint32_t s[kNdw]) {
   for (int d = 0; d < kNdw / 2; ++d) c.v |= vp[d] << (8 * d);
   c.zlo = zl;
   c.zhi = zh;
-  c.dlo = dl;
-  c.dhi = dh;
   c.bad = bad;
   return c;
 }
 
-// per-lane run summary of one axis over its 32 bytes (rare path)
-struct RunSum {
-  uint32_t pfx, sfx, cnt, hz;
+// ---- which tiles could hold a run -----------------------------------------
+// All reads: a tile with a Z-free 16-byte chunk (on either axis).  A run of
+// >= kRun >= 41 D moves spans >= 3 aligned chunks: its first and last chunk
+// hold <= 15 of its D moves each, so the chunks wholly inside it (Z-free)
+// hold >= 11.  Skipped reads make many partly masked chunks Z-free, so a tile
+// holding skipped bytes uses a sharper test that the same count still
+// guarantees: a Z-free chunk with >= 6 D moves, or a lane whose two chunks
+// are Z-free and hold a D move.  (Inside chunks with <= 5 D moves each mean
+// >= 3 inside chunks holding D moves; at most two of them lie outside the
+// lanes wholly inside the run, so a wholly inside lane holds one.)  A tile
+// passing the cheap all-reads test in either case runs that sharper one.
+
+// bit j <- byte j's bit 0, from per-byte 0/1 values (v_dot4 with byte weights)
+__device__ __forceinline__ uint32_t byte_bits(const uint32_t (&b)[kNdw]);
+
+__device__ __forceinline__ bool run_candidate(const Cls &c) {
+  bool cand = false;
+#pragma unroll
+  for (int ax = 0; ax < 2; ++ax) {
+    uint32_t xb[kNdw];
+#pragma unroll
+    for (int d = 0; d < kNdw; ++d) xb[d] = (c.cd[d] >> ax) & 0x01010101u;
+    const uint32_t bits = byte_bits(xb);
+    const uint32_t D = c.v & bits, Z = c.v & ~bits;
+    const bool z0 = (Z & 0xFFFFu) != 0u, z1 = (Z >> 16) != 0u;
+    const int d0 = __builtin_popcount(D & 0xFFFFu), d1 = __builtin_popcount(D >> 16);
+    cand = cand || (!z0 && d0 >= 6) || (!z1 && d1 >= 6) || (!z0 && !z1 && D != 0u);
+  }
+  return __ballot(cand) != 0ull;
+}
+
+// ---- exact run scan of one tile (rare path: tiles that could hold a run) ----
+// Runs within one lane's 32 bytes are < 41 <= kRun (a run needs no Z for
+// kRun D moves), so only runs across lanes matter.  Per lane and axis: hz
+// (the lane holds a Z), cnt (its D moves), pfx / sfx (D moves before its
+// first / after its last Z); then one segmented inclusive scan over the wave
+// (DPP row_shr + row_bcast, as wave_scan) of (hz, hz ? sfx : cnt): each lane
+// learns the run open at its start.
+
+__device__ __forceinline__ uint32_t byte_bits(const uint32_t (&b)[kNdw]) {
+  uint32_t vp[kNdw / 2];
+#pragma unroll
+  for (int d = 0; d < kNdw; ++d)
+    vp[d >> 1] = (d & 1) ? __builtin_amdgcn_udot4(b[d], 0x80402010u, vp[d >> 1], false)
+                         : __builtin_amdgcn_udot4(b[d], 0x08040201u, 0u, false);
+  return vp[0] | (vp[1] << 8) | (vp[2] << 16) | (vp[3] << 24);
+}
+
+// one step of the segmented scan: (f, v) <- (f_nb | f, f ? v : v_nb + v)
+template <int CTRL, int RM, bool BC>
+__device__ __forceinline__ void seg_step(uint32_t &f, uint32_t &v) {
+  const uint32_t nv = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, RM, 0xF, BC);
+  const uint32_t nf = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)f, CTRL, RM, 0xF, BC);
+  v = f ? v : v + nv;
+  f |= nf;
+}
+
+struct TileRuns {
+  bool risky;      // a run >= run_max that does not involve the entering run
+  bool risky_in;   // the entering run e plus the tile's leading D moves reach run_max
+  bool anyz;       // the tile holds a Z on this axis
+  uint32_t out;    // D moves after the tile's last Z (anyz), else the tile's D moves
 };
 
 template <int AX>
-__device__ __forceinline__ RunSum run_sum(const Cls &c) {
-  RunSum r = {0u, 0u, 0u, 0u};
+__device__ __forceinline__ TileRuns tile_runs(const Cls &c, uint32_t e, uint32_t run_max) {
+  uint32_t xb[kNdw];
 #pragma unroll
-  for (int j = 0; j < kLaneBytes; ++j) {
-    if (!((c.v >> j) & 1u)) continue;
-    const uint32_t d = (c.cd[j >> 2] >> (8 * (j & 3) + AX)) & 1u;
-    if (d) {
-      ++r.cnt;
-      ++r.sfx;
-      if (!r.hz) ++r.pfx;
-    } else {
-      r.hz = 1;
-      r.sfx = 0;
-    }
-  }
-  return r;
-}
-
-// exact run scan of one tile on one axis: runs enter with ein, returns the
-// run open at the tile end; risky |= a run >= run_max
-template <int AX>
-__device__ uint32_t scan_tile(const Cls &c, uint32_t ein, uint32_t run_max, bool &risky) {
-  const RunSum rs = run_sum<AX>(c);
-  const uint32_t packed = rs.pfx | (rs.sfx << 8) | (rs.cnt << 16) | (rs.hz << 24);
-  uint32_t run = ein;
-  for (int l = 0; l < 64; ++l) {
-    const uint32_t p = __builtin_amdgcn_readlane(packed, l);
-    const uint32_t pfx = p & 0xFF, sfx = (p >> 8) & 0xFF, cnt = (p >> 16) & 0xFF;
-    if (p >> 24) {
-      if (run + pfx >= run_max) risky = true;
-      run = sfx;
-    } else {
-      run += cnt;
-    }
-    if (run >= run_max) risky = true;
-    run = min(run, 1u << 20);
-  }
-  return run;
+  for (int d = 0; d < kNdw; ++d) xb[d] = (c.cd[d] >> AX) & 0x01010101u;
+  const uint32_t bits = byte_bits(xb);
+  const uint32_t D = c.v & bits, Z = c.v & ~bits;
+  const uint32_t cnt = (uint32_t)__builtin_popcount(D);
+  const uint32_t pfx = (uint32_t)__builtin_popcount(D & ((Z & (0u - Z)) - 1u));   // Z = 0: all of D
+  const uint32_t top = Z ? (0xFFFFFFFFu >> __builtin_clz(Z)) : 0u;               // bits up to the last Z
+  const uint32_t sfx = (uint32_t)__builtin_popcount(D & ~top);
+  uint32_t f = Z ? 1u : 0u, v = Z ? sfx : cnt;
+  seg_step<0x111, 0xF, true>(f, v);
+  seg_step<0x112, 0xF, true>(f, v);
+  seg_step<0x114, 0xF, true>(f, v);
+  seg_step<0x118, 0xF, true>(f, v);
+  seg_step<0x142, 0xA, false>(f, v);
+  seg_step<0x143, 0xC, false>(f, v);
+  // exclusive: lane l - 1's inclusive (lane 0: nothing before)
+  const uint32_t ev = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, false);
+  const uint32_t ef = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)f, 0x138, 0xF, 0xF, false);
+  TileRuns t;
+  t.risky = __ballot(ef && ev + pfx >= run_max) != 0ull;
+  t.risky_in = __ballot(!ef && e + ev + pfx >= run_max) != 0ull;
+  t.anyz = __builtin_amdgcn_readlane(f, 63) != 0u;
+  t.out = __builtin_amdgcn_readlane(v, 63);
+  return t;
 }
 
 __device__ __forceinline__ bool moving_byte(uint8_t ch) { return ch == 'A' || ch == 'C' || ch == 'G' || ch == 'T'; }
@@ -271,7 +309,7 @@ __device__ uint32_t run_before(const SArgs &A, int32_t b0, int32_t at, uint32_t 
 // VALID: the same, skipping the reads that are not valid; t is the read that
 // holds byte at - 1 (-1: none)
 template <int AX>
-__device__ uint32_t run_before_valid(const SArgs &A, int32_t at, int64_t t, uint32_t run_max) {
+__device__ uint32_t run_before_valid(const SArgs &A, int32_t at, int32_t t, uint32_t run_max) {
   uint32_t run = 0;
   int32_t p = at - 1;
   for (; t >= 0 && run < run_max; --t) {
@@ -289,16 +327,21 @@ __device__ uint32_t run_before_valid(const SArgs &A, int32_t at, int64_t t, uint
   return run;
 }
 
+template <int AX>
+struct AxisTag {
+  static constexpr int value = AX;
+};
+
 // the idx window a wave walks: lane j holds idx[r + j] (0x7FFFFFFF past the
 // end); the load is unconditional (clamped index) so that no branch splits the
 // compiler's view of the loads in flight.  VALID: tg = 1 when read r + j's
 // validity differs from read r + j - 1's (the state before read 0 is valid).
 template <bool VALID>
-__device__ __forceinline__ int32_t idx_window(const SArgs &A, int64_t r, int lane, uint32_t &tg) {
-  const int64_t j = r + lane, n = A.num_reads;
+__device__ __forceinline__ int32_t idx_window(const SArgs &A, int32_t r, int lane, uint32_t &tg) {
+  const int32_t j = r + lane, n = (int32_t)A.num_reads;
   const int32_t v = A.idx[j <= n ? j : n];
   if (VALID) {
-    const int64_t ja = j < n ? j : n - 1, jb = j >= 1 && j <= n ? j - 1 : 0;
+    const int32_t ja = j < n ? j : n - 1, jb = j >= 1 && j <= n ? j - 1 : 0;
     const bool va = A.status[ja] == 1, vb = j == 0 || A.status[jb] == 1;
     tg = j < n && va != vb ? 1u : 0u;
   }
@@ -312,9 +355,9 @@ __device__ __forceinline__ int32_t idx_window(const SArgs &A, int64_t r, int lan
 // in flight.  hop: the tile is its span's last, so the cursor moves on to rn
 // (the next span's first read) instead.
 template <bool VALID, bool TOG>
-__device__ __forceinline__ void scatter_starts(const SArgs &A, uint32_t *sc, uint32_t *tc, int64_t &r, int32_t &iw,
+__device__ __forceinline__ void scatter_starts(const SArgs &A, uint32_t *sc, uint32_t *tc, int32_t &r, int32_t &iw,
                                                uint32_t &itg, int32_t base, int32_t limit, int lane, bool hop = false,
-                                               int64_t rn = 0) {
+                                               int32_t rn = 0) {
   auto put = [&](int32_t x, uint32_t tg) {
     const bool in = x < limit;
     const uint32_t o = (uint32_t)(x - base);
@@ -377,6 +420,18 @@ __device__ __forceinline__ uint32_t chunk_bits(uint32_t lo, uint32_t hi) {
   return (u | (u >> 8) | (u >> 16) | (u >> 24)) & 0xFu;
 }
 
+// the same for D moves (A/T on x, G/T on y) of a lane's seq bytes
+__device__ __forceinline__ uint32_t chunk_bits_d(const uint32_t (&s)[kNdw]) {
+  uint32_t dl = 0, dh = 0;
+#pragma unroll
+  for (int d = 0; d < kNdw; ++d) {
+    const uint32_t dm = __builtin_amdgcn_perm(kDHi, kDLo, s[d] & 0x07070707u);
+    if (d < 4) dl |= dm;
+    else dh |= dm;
+  }
+  return chunk_bits(dl, dh);
+}
+
 template <int K, bool VALID>
 __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
   static_assert(K >= 1 && K <= kMaxK, "LDS table");
@@ -403,8 +458,8 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
   const int32_t b0 = __builtin_amdgcn_readfirstlane(A.idx[0]);
   const int32_t b1 = __builtin_amdgcn_readfirstlane(A.idx[A.num_reads]);
   const int32_t a0 = b0 & ~15;
-  const int64_t ns = nspans(a0, b1);
-  const int64_t gw = (int64_t)blockIdx.x * kWaves + wid, nwav = (int64_t)gridDim.x * kWaves;
+  const int32_t ns = (int32_t)nspans(a0, b1);
+  const int32_t gw = (int32_t)blockIdx.x * kWaves + wid, nwav = (int32_t)gridDim.x * kWaves;
   bool risky = false;
 
   // one descriptor pair per call: offsets past b1 + slack read zeros without
@@ -428,36 +483,37 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
   // costs no memory round trip.  The cursor of the next span (rn) is read at
   // span entry and taken over when the span's last tile is scattered.
   if (gw < ns) {
-    int64_t s = gw;
+    int32_t s = gw;
     // lane 0 of each: the previous tile's last lane (packed codes 16..31, last
     // quality dwords, V and starts), the "old" operand of wave_shr:1
     uint32_t pp1, pq6, pq7, pv, pS;
-    // the run open at the tile start per axis: exact when eknown, else at
-    // most 15 (the last 16 bytes hold a Z on both axes) and walked back for
-    // only when a tile needs the exact scan
+    // the run open at the tile start per axis: exact when ekx / eky, else at
+    // most 16 (a tile without a candidate chunk) or 15 (a span context
+    // whose last 16 bytes hold a Z on both axes), walked back for only when
+    // that bound would decide a run
     uint32_t einx = 15, einy = 15;
-    bool eknown = false;
+    bool ekx = false, eky = false;
     // span entry: the 16 bytes before t0 (all 'N' before the batch) and the
     // read starts among the 32 before it; VALID: rv = the read holding byte
     // t0 - 1 (-1: none), the entry state skip_in (1: that read is skipped)
     auto enter = [&](const uint32_t (&cs)[4], const uint32_t (&cq)[2], const uint32_t ps, const int32_t t0,
-                     const int64_t rv, uint32_t &skip_in) {
+                     const int32_t rv, uint32_t &skip_in) {
       uint32_t sw[kNdw];
 #pragma unroll
       for (int d = 0; d < kNdw; ++d) sw[d] = d < kNdw - 4 ? 0x4E4E4E4Eu : cs[d - (kNdw - 4)];
-      const Cls c = classify<false>(sw);
+      const Cls c = classify(sw);
       pp1 = __builtin_amdgcn_readfirstlane(c.p1);
       pq6 = __builtin_amdgcn_readfirstlane(cq[0]);
       pq7 = __builtin_amdgcn_readfirstlane(cq[1]);
       pv = __builtin_amdgcn_readfirstlane(c.v);
       pS = ps;
       einx = einy = 15;
-      eknown = false;
+      ekx = eky = false;
       if (!VALID) {
         if (!(c.zhi & 0x01010101u) || !(c.zhi & 0x02020202u)) {
           einx = run_before<0>(A, b0, t0, kRun);
           einy = run_before<1>(A, b0, t0, kRun);
-          eknown = true;
+          ekx = eky = true;
         }
         return;
       }
@@ -467,21 +523,20 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
       skip_in = rv >= 0 && !vrd ? 1u : 0u;
       const uint32_t st = ps >> 16;   // starts among the 16 bytes
       const uint32_t own = st ? (0xFFFFu << (31 - __builtin_clz(st))) & 0xFFFFu : 0xFFFFu;
-      uint32_t zx = 0, zy = 0;
+      uint32_t xb[kNdw], yb[kNdw];
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const uint32_t b = (c.cd[4 + (i >> 2)] >> (8 * (i & 3))) & 3u;
-        const uint32_t vv = (c.v >> (16 + i)) & 1u;
-        zx |= (vv & ~b & 1u) << i;
-        zy |= (vv & (~b >> 1) & 1u) << i;
+      for (int d = 0; d < kNdw; ++d) {
+        xb[d] = c.cd[d] & 0x01010101u;
+        yb[d] = (c.cd[d] >> 1) & 0x01010101u;
       }
+      const uint32_t zx = (c.v & ~byte_bits(xb)) >> 16, zy = (c.v & ~byte_bits(yb)) >> 16;   // Z moves among the 16
       if (!vrd || !(zx & own) || !(zy & own)) {
         einx = run_before_valid<0>(A, t0, rv, kRun);
         einy = run_before_valid<1>(A, t0, rv, kRun);
-        eknown = true;
+        ekx = eky = true;
       }
     };
-    auto ctx_starts = [&](int64_t &r, int32_t &iw, uint32_t &itg, const int32_t t0) {
+    auto ctx_starts = [&](int32_t &r, int32_t &iw, uint32_t &itg, const int32_t t0) {
       scatter_starts<VALID, false>(A, scx, nullptr, r, iw, itg, t0 - kLaneBytes, t0, lane);
       __builtin_amdgcn_wave_barrier();
       const uint32_t ps = __builtin_amdgcn_readfirstlane(scx[0]);
@@ -496,11 +551,12 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
     // starting in the tile; returns the toggles' parity (the next tile's state
     // is sk ^ parity).
     auto tile = [&](const int32_t t, const int32_t tend, uint32_t (&sw)[kNdw], uint32_t (&qw)[kNdw],
-                    const uint32_t so, const uint32_t sk, const uint32_t tg, const int64_t rf, auto &&mid) {
+                    const uint32_t so, const uint32_t sk, const uint32_t tg, const int32_t rf, auto &&mid) {
       const int32_t o = t + kLaneBytes * lane;
       if (t < b0 || t + kTile > tend) mask_range(o, b0, tend, sw, qw);   // edge tiles
       uint32_t par = 0;
-      if (VALID) {
+      bool masked = false;   // VALID: the tile holds skipped bytes
+      if (VALID && (sk || __ballot(tg != 0u))) {
         // skip bit of byte j = sk ^ (toggles of the lanes below) ^ (toggles of bytes <= j)
         uint32_t px = tg;
         px ^= px << 1;
@@ -513,9 +569,10 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
         const uint32_t skip = px ^ (0u - ((below ^ sk) & 1u));
         par = (uint32_t)__popcll(bal) & 1u;
-        if (__ballot(skip != 0u)) mask_skipped(skip, sw, qw);
+        masked = __ballot(skip != 0u) != 0ull;
+        if (masked) mask_skipped(skip, sw, qw);
       }
-      const Cls c = classify<VALID>(sw);
+      const Cls c = classify(sw);
       uint32_t qor = 0;
 #pragma unroll
       for (int d = 0; d < kNdw; ++d) qor |= qw[d];
@@ -523,24 +580,41 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
       if (__ballot(c.bad != 0u || (qor & 0x80808080u) != 0u)) risky = true;
       // runs: a 16-byte chunk without a Z on an axis (VALID: that holds a D
       // move there), or a long run entering the tile
+      // (a tile without skipped bytes: any Z-free chunk, as for all reads; with
+      // them, only Z-free chunks holding a D move, so that wholly skipped
+      // chunks do not trigger)
       const uint32_t zc = chunk_bits(c.zlo, c.zhi);
-      const bool zfree = VALID ? (chunk_bits(c.dlo, c.dhi) & ~zc) != 0u : zc != 0xFu;
+      bool zfree = zc != 0xFu;
+      if (VALID && masked && zfree && __ballot((chunk_bits_d(sw) & ~zc) != 0u)) zfree = run_candidate(c);
+      else if (VALID && masked) zfree = false;
       if (__builtin_expect(__ballot(zfree) != 0ull || einx > 16 || einy > 16, 0)) {
-        if (!eknown) {
-          if (VALID) {
-            einx = run_before_valid<0>(A, t, rf - 1, kRun);
-            einy = run_before_valid<1>(A, t, rf - 1, kRun);
-          } else {
-            einx = run_before<0>(A, b0, t, kRun);
-            einy = run_before<1>(A, b0, t, kRun);
+        // exact scan; an entering run known only by its bound is walked back
+        // for only when the bound would decide (>= kRun - 16 leading D moves)
+        auto axis = [&](auto ax, uint32_t &ein, bool &ek) __attribute__((always_inline)) {
+          constexpr int AX = decltype(ax)::value;
+          const TileRuns tr = tile_runs<AX>(c, ein, kRun);
+          if (tr.risky) risky = true;
+          if (tr.risky_in) {
+            if (!ek) {
+              ein = VALID ? run_before_valid<AX>(A, t, rf - 1, kRun) : run_before<AX>(A, b0, t, kRun);
+              ek = true;
+              if (tile_runs<AX>(c, ein, kRun).risky_in) risky = true;
+            } else {
+              risky = true;
+            }
           }
-        }
-        einx = scan_tile<0>(c, einx, kRun, risky);
-        einy = scan_tile<1>(c, einy, kRun, risky);
-        eknown = true;
+          if (tr.anyz) {
+            ein = tr.out;
+            ek = true;
+          } else {
+            ein = min(ein + tr.out, 1u << 20);
+          }
+        };
+        axis(AxisTag<0>{}, einx, ekx);
+        axis(AxisTag<1>{}, einy, eky);
       } else {
-        einx = einy = 15;
-        eknown = false;
+        einx = einy = 16;   // (see the header: a tile without a candidate chunk leaves <= 16)
+        ekx = eky = false;
       }
       // neighbours (lane 0: the previous tile's last lane / the span context)
       const uint32_t np1 = dpp_shr1(pp1, c.p1);   // the code stream below byte 0
@@ -598,10 +672,10 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
       pS = dpp_ror1(so);
       return par;
     };
-    int32_t tA = a0 + (int32_t)(s << kSpanLog), tB;
+    int32_t tA = (int32_t)(a0 + ((int64_t)s << kSpanLog)), tB;
     int32_t eA = (int32_t)min((int64_t)tA + kSpan, (int64_t)b1), eB;
-    int64_t r = sfirst[s];
-    int64_t rn = sfirst[min(s + nwav, ns - 1)];
+    int32_t r = sfirst[s];
+    int32_t rn = sfirst[min(s + nwav, ns - 1)];
     uint32_t itg = 0;
     int32_t iw = idx_window<VALID>(A, r, lane, itg);
     uint32_t skA = 0, skB = 0;   // VALID: skip state at the tile starts
@@ -617,7 +691,7 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
       enter(cs, cq, ps, tA, r - 1, skA);
     }
     uint32_t sA[kNdw], qA[kNdw], sB[kNdw], qB[kNdw], soA, soB, tgA = 0, tgB = 0;
-    int64_t rfA = r, rfB = 0;   // VALID: the first read starting in the tile
+    int32_t rfA = r, rfB = 0;   // VALID: the first read starting in the tile
     scatter_starts<VALID, VALID>(A, sc, tcb, r, iw, itg, tA, tA + kTile, lane, tA + kTile >= eA, rn);
     soA = take_bits(&sc[lane]);
     if (VALID) tgA = take_bits(&tcb[lane]);
@@ -627,9 +701,9 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
     // unconditional, so the compiler counts the loads in flight exactly and
     // a tile waits only for its own bytes); false past the wave's last tile
     auto half = [&](const int32_t tx, const int32_t ex, uint32_t (&sx)[kNdw], uint32_t (&qx)[kNdw], const uint32_t sox,
-                    const uint32_t skx, const uint32_t tgx, const int64_t rfx, uint32_t *scpy, uint32_t *tcpy,
+                    const uint32_t skx, const uint32_t tgx, const int32_t rfx, uint32_t *scpy, uint32_t *tcpy,
                     int32_t &ty, int32_t &ey, uint32_t (&sy)[kNdw], uint32_t (&qy)[kNdw], uint32_t &soy,
-                    uint32_t &sky, uint32_t &tgy, int64_t &rfy) {
+                    uint32_t &sky, uint32_t &tgy, int32_t &rfy) {
       ty = tx + kTile;
       ey = ex;
       bool entering = false, fin = false;
@@ -637,7 +711,7 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
       if (ty >= ex) {   // x is its span's last tile: y is the next span's first
         s += nwav;
         if (s < ns) {
-          ty = a0 + (int32_t)(s << kSpanLog);
+          ty = (int32_t)(a0 + ((int64_t)s << kSpanLog));
           ey = (int32_t)min((int64_t)ty + kSpan, (int64_t)b1);
           entering = true;
           rn = sfirst[min(s + nwav, ns - 1)];
@@ -646,7 +720,7 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
           fin = true;
         }
       }
-      const int64_t rv = r - 1;   // entering: the read holding byte ty - 1
+      const int32_t rv = r - 1;   // entering: the read holding byte ty - 1
       const v4u a = __builtin_amdgcn_raw_buffer_load_b128(rs, entering ? (uint32_t)ty - 16u : kPast, 0, 0);
       const v2u q = __builtin_amdgcn_raw_buffer_load_b64(rq, entering ? (uint32_t)ty - 8u : kPast, 0, 0);
       const uint32_t oy = fin ? kPast : (uint32_t)(ty + kLaneBytes * lane);
