@@ -378,8 +378,11 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   // segment's first lane stores its sum)
   const bool w_direct = LR && w_rl == 0 && w_ll <= 4 * NW;
   // EDIT: the trim bounds, read once (see NX above)
-  ColdParams cold{};
-  if (EDIT) cold = *A.cold;
+  // (held across the loop: re-reading them per unit prologue cut the
+  // single-end SGPR spills 90 -> 71 but cost 5 % of C4, and paired-end
+  // spilled more VGPRs that way)
+  ColdParams cold_all{};
+  if (EDIT) cold_all = *A.cold;
   // biased-sum bounds (A.phred is phred + 128): pass iff min_len <= n <= max_len and lo_r*n <= S <= hi_r*n
   const int lo_r = A.min_q + A.phred, hi_r = A.max_q + A.phred;
   const int dlim = A.defer_len;   // longer reads go to the next stage
@@ -491,12 +494,23 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       if (lane == 0) A.defer_bits[U.u] = pbits;
       ndefer += (uint32_t)__builtin_popcountll(dm);
     }
+    // EDIT (paired-end), usual windows: both mates' trim loads in flight
+    // before the first is finished (one exposed round trip per unit, not one
+    // per mate; single-end keeps trim_word, whose registers fit better)
+    TrimLoads tl[NM];
+    const ColdParams &cold = cold_all;
+    const bool usual = EDIT && NM == 2 && trim_usual(cold);
+    if (usual) {
+#pragma unroll
+      for (int m = 0; m < NM; ++m)
+        tl[m] = trim_issue(cold, rq[m], live ? bq[m] + ia[m] : (int)0x80000000, ie[m] - ia[m]);
+    }
 #pragma unroll
     for (int m = 0; m < NM; ++m) {
       int a = ia[m], e = ie[m];
       tw[m] = 0;
       if (EDIT) {   // trim here, then describe the trimmed window
-        tw[m] = live ? trim_word(cold, rq[m], bq[m] + a, e - a) : 0u;
+        tw[m] = !live ? 0u : usual ? trim_finish(cold, tl[m], e - a) : trim_word(cold, rq[m], bq[m] + a, e - a);
         if (A.trim && live) A.trim[(size_t)m * (size_t)A.num_reads + rid] = tw[m];
         a += (int)(tw[m] & 0xFFFFu);
         e -= (int)(tw[m] >> 16);

@@ -110,16 +110,14 @@ static void *worker(void *arg) {
     if (bi >= g_nbatches) break;
     const batch_t *bt = &g_batches[bi];
     const size_t n = bt->n;
-    size_t bytes = 0;
-    for (size_t i = 0; i < n; i++) bytes += strlen(bt->reads[i].sequence);
-    char *seq = malloc(bytes + 1), *qual = malloc(bytes + 1);
-    int32_t *idx = malloc((n + 1) * sizeof(int32_t));
+    int32_t *idx = malloc((n + 1) * sizeof(int32_t));   /* offsets first: one strlen per read */
     idx[0] = 0;
+    for (size_t i = 0; i < n; i++) idx[i + 1] = idx[i] + (int32_t)strlen(bt->reads[i].sequence);
+    char *seq = malloc((size_t)idx[n] + 1), *qual = malloc((size_t)idx[n] + 1);
     for (size_t i = 0; i < n; i++) {
-      const size_t len = strlen(bt->reads[i].sequence);
+      const size_t len = (size_t)(idx[i + 1] - idx[i]);
       memcpy(seq + idx[i], bt->reads[i].sequence, len);
       memcpy(qual + idx[i], bt->reads[i].quality, len);
-      idx[i + 1] = idx[i] + (int32_t)len;
     }
     hpgq_batch_t b = {(int64_t)n, seq, qual, idx};
     uint8_t *mask = malloc(n);

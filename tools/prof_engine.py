@@ -69,6 +69,13 @@ elif args.mode == "edit":
 elif args.mode == "maxn":   # C2 plus max_N / max_out_of_quality (the N / out-of-range filter variant)
     p = H.stats_params(lmax=L, read_quality_range="20,", read_length_range="50,", max_N=2,
                        max_out_of_quality=20)
+elif args.mode == "pe_edit":   # C4 trims on paired-end (bench --config c4_pe)
+    p = H.edit_params(lmax=L, stats=True, left_length=10, left_quality_range="20,",
+                      right_length=30, right_quality_range="20,", read_quality_range="20,")
+    p.paired = 1
+elif args.mode == "edit_noor":   # C4 + --max-N 2 (bench --config c4_noor)
+    p = H.edit_params(lmax=L, stats=True, left_length=10, left_quality_range="20,",
+                      right_length=30, right_quality_range="20,", max_N=2)
 elif args.mode in ("edit0", "editL", "editR"):   # timing probes: the edit kernel, fewer trims
     p = H.edit_params(lmax=L, stats=True, left_length=10 if args.mode == "editL" else 0,
                       left_quality_range="20,", right_length=30 if args.mode == "editR" else 0,
