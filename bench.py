@@ -90,6 +90,10 @@ CONFIGS = {
                    unit="Mreads/s", reads=4_000_000, batch=10_000, L=150, seed=2,
                    workload="INTEGRATION.md's fastq_stats_worker: AoS reads packed per 10,000-read batch, "
                             "hpgq_run_host + hpgq_sync, 2 worker threads with one ctx each (src/stats_options.c:21-22)"),
+    "c2_kmers": dict(metric="Mreads/s (150 bp) stats --kmers 5-mer counts (passed reads of C2)",
+                     unit="Mreads/s", reads=50_000_000, batch=10_000_000, L=150, seed=2,
+                     workload="stats --kmers on C2 reads: 5-mers of the reads that pass "
+                              "--read-quality-range 20, --read-length-range 50, (engine mask), per start position"),
     "c2_lr": dict(metric="Mreads/s (150 bp) stats+filter with a 5' window filter",
                   unit="Mreads/s", reads=100_000_000, batch=10_000_000, L=150, seed=2,
                   workload="C2 flags + --left-length 10 --left-quality-range 20,"),
@@ -220,7 +224,14 @@ def cpu_baseline(args, params):
         bufs.append((seq, qual, idx))
     bs = [H.Batch(n, sq.ctypes.data, ql.ctypes.data, ix.ctypes.data) for sq, ql, ix in bufs]
     nt = [threads]
-    if cgr:
+    if args.config == "c2_kmers":
+        lib.oracle_kmers.argtypes = [C.POINTER(H.Batch), C.c_void_p, C.c_int, C.c_void_p]
+        lib.oracle_kmers.restype = C.c_int
+        by_pos = np.zeros(1024 * (L - 4), np.uint64)
+        run = lambda p=None: lib.oracle_kmers(C.byref(bs[0]), None, L, by_pos.ctypes.data)  # noqa: E731
+        what = "oracle_kmers (hpgq_oracle.c, one thread), every read"
+        threads = 1
+    elif cgr:
         # independent fill calls (one per batch of 20 k reads) spread over the threads
         nb = 20
         per = n // nb
@@ -468,7 +479,22 @@ def main():
     offs = np.cumsum([0] + [b[0] for b in batches])
 
     statuses = []
-    if cgr:
+    kmers = args.config == "c2_kmers"
+    km = None
+    if kmers:
+        # the engine's C2 masks once (setup), then each step counts the passed
+        # reads' 5-mers: the k-mer kernel alone is what the step times
+        eng = H.Engine(params, device=local)
+        for i, (n, mm, _nb) in enumerate(batches):
+            sq, ql, ix = mm[0]
+            eng.run_device(H.engine.device_batch(n, sq.data_ptr(), ql.data_ptr(), ix.data_ptr()), None,
+                           d_mask.data_ptr() + int(offs[i]), None)
+        eng.sync()
+        km = H.Kmers(L, device=local, stream=eng.stream)
+        kernel_name = "hpgq::kmers::kmer_tile_kernel (+kmer_maxlen_kernel)"
+        # seq + offsets + the mask (quality is not read)
+        alg = [(nb - 4 * (n + 1)) // 2 + 4 * (n + 1) + n for (n, _m, nb) in batches]
+    elif cgr:
         eng = H.ChaosGame(7, 33, device=local)
         kernel_name = f"hpgq::cgr::stream::cgr_stream_kernel<7, {'true' if valid else 'false'}> (+span_first)"
         # algorithmic bytes per read: seq + quality + offset (tables stay in LDS)
@@ -506,11 +532,13 @@ def main():
     per_step = cgr or world > 1
 
     def step(s=None):
-        eng.reset()
+        (km if kmers else eng).reset()
         for i, b in enumerate(hb):
             if s is not None and i == 0 and (per_step or s == 0):
                 ev[s][0].record(ext)
-            if cgr:
+            if kmers:
+                km.count_device(b[0], d_mask.data_ptr() + int(offs[i]))
+            elif cgr:
                 if valid:
                     eng.fill_device(b[0], statuses[i].data_ptr(), H.CGR_ONLY_VALID_READS)
                 else:
@@ -554,7 +582,9 @@ def main():
         timed_ms = ev[0][0].elapsed_time(ev[-1][1])
 
     # sanity: every read accounted for
-    if cgr:
+    if kmers:
+        assert int(km.by_pos().sum()) > 0
+    elif cgr:
         _ts, _tq, wc = eng.tables()
         assert wc > 0 or os.environ.get("HPGQ_BENCH_NOCHECK")   # (timing-probe builds add nothing)
     else:
@@ -609,6 +639,8 @@ def main():
         out["e2e"] = e2e_leg(args, local)
     if rank == 0:
         print(json.dumps(out), flush=True)
+    if km is not None:
+        km.close()
     if eng is not None:
         eng.close()
     if world > 1:

@@ -8,12 +8,28 @@
 // counted at every start position p <= len-5 of every merged read.  Output:
 // by_pos[1024][lmax-4] u64; the global counter of a k-mer is its row sum.
 //
-// Kernel: position tiles.  A workgroup owns kP start positions and an LDS
-// table [1024 kmers][kP] (64 KB, u32: one read adds at most 1 per cell), and
-// walks a stride of reads, each lane one read at a time: one 16-byte and one
-// 4-byte buffer load cover the 20 bytes the tile's 5-mers span, codes come from
-// a v_perm lookup with an exact byte check, and a 5-bit validity register
-// gates the LDS adds.  Nonzero cells are flushed with global atomics.
+// Kernels.  A 5-mer's counter lives at (start position, id): 1024 x lmax-4
+// counters, too many for one workgroup's LDS, so a workgroup owns a TILE of
+// kP start positions ([kP][1024] u32 = 128 KB, position-major so that the 64
+// lanes' adds at one position spread over the banks by id) for the whole
+// call and adds it to by_pos once at its end.  Every tile re-reads the
+// reads' windows; the workgroups that hold the T tiles of one read group sit
+// on one XCD and walk the same reads in the same order, so the re-reads hit
+// that XCD's L2 (blockIdx -> XCD is round robin: b mod 8).  A prepass takes
+// the longest counted read, so tiles past it (the CLI's lmax 1024 on 150 bp
+// reads) exit at once instead of scanning every read.
+//   kmer_maxlen_kernel  max length over the counted reads (atomicMax)
+//   kmer_tile_kernel    two lanes per read, 16 start positions each (one
+//                       lane per read made every 16-byte load touch its own
+//                       segment: the texture addresser was 85 % busy; four
+//                       lanes per read spent more on per-lane set-up than it
+//                       saved), software-pipelined (the next group's bytes
+//                       are fetched while this one is counted, its offsets
+//                       one group earlier still): 20 bytes per lane, 2-bit
+//                       codes packed by v_dot4, a mask of the 5-mers that
+//                       count (OR of 5 shifts of the non-ACGT bits), then per
+//                       start position one v_alignbit + v_bitop3 for the cell
+//                       address and one ds_add_u32 of 0 or 1.
 #include "hpgq_common.h"
 
 #include <algorithm>
@@ -23,8 +39,12 @@ namespace kmers {
 
 constexpr int kK = 5;
 constexpr int kNum = 1 << (2 * kK);   // 1024
-constexpr int kP = 16;                // start positions per tile
+constexpr int kP = 32;                // start positions per tile
 constexpr int kWG = 1024;
+constexpr int kLanesPerRead = 2;      // a read's tile: 2 lanes x 16 start positions
+constexpr int kPosPerLane = kP / kLanesPerRead;
+constexpr int kReadsPerWave = 64 / kLanesPerRead;
+constexpr int kGroup = (kWG / 64) * kReadsPerWave;   // reads per workgroup step (512)
 
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
@@ -35,52 +55,137 @@ constexpr uint32_t kExHi = 0x47010154u;   // codes 4..7: T, -, -, G
 constexpr uint32_t kValLo = 0x01000000u;  // C = 1 at code 3
 constexpr uint32_t kValHi = 0x02000003u;  // T = 3 at code 4, G = 2 at code 7
 
-// 4 bytes -> 2-bit codes (byte lanes) and a valid bit per byte (bit 8*i)
-__device__ __forceinline__ void codes4(uint32_t w, uint32_t &val, uint32_t &ok) {
+// 4 bytes -> their 2-bit codes packed first byte highest (byte i of 4 at
+// bits 2(3-i)) and a bit per byte that is NOT exactly A/C/G/T (bit i)
+__device__ __forceinline__ void codes4(uint32_t w, uint32_t &packed, uint32_t &bad) {
   const uint32_t code = w & 0x07070707u;
   const uint32_t d = w ^ __builtin_amdgcn_perm(kExHi, kExLo, code);
-  const uint32_t nz = (((d & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | d) & 0x80808080u;   // inexact bytes
-  ok = ~(nz >> 7) & 0x01010101u;
-  val = __builtin_amdgcn_perm(kValHi, kValLo, code);
+  // bit 7 of each byte of d that is nonzero: ((d & 7F..) + 7F..) | d, & 80..
+  const uint32_t nz = __builtin_amdgcn_bitop3_b32((d & 0x7F7F7F7Fu) + 0x7F7F7F7Fu, d, 0x80808080u, 0xA8);   // (a | b) & c
+  bad = __builtin_amdgcn_udot4(nz >> 7, 0x08040201u, 0u, false);
+  packed = __builtin_amdgcn_udot4(__builtin_amdgcn_perm(kValHi, kValLo, code), 0x01041040u, 0u, false);
 }
 
-__global__ void __launch_bounds__(kWG) kmer_kernel(const char *seq, const int32_t *idx, int64_t n,
-                                                   const uint8_t *mask, int npos,
-                                                   unsigned long long *out) {
-  __shared__ uint32_t t[kNum * kP];
-  for (int i = threadIdx.x; i < kNum * kP; i += kWG) t[i] = 0;
+__device__ __forceinline__ bool counted(const uint8_t *mask, int64_t r) { return !mask || mask[r] == 1; }
+
+// one workgroup per CU, grid-stride; one atomic per workgroup (one per wave
+// made 8 K atomics on one word: 112 us per 10 M reads)
+__global__ void __launch_bounds__(1024) kmer_maxlen_kernel(const int32_t *idx, int64_t n, const uint8_t *mask,
+                                                           int *maxlen) {
+  __shared__ int wm[16];
+  int m = 0;
+  for (int64_t r = (int64_t)blockIdx.x * 1024 + threadIdx.x; r < n; r += (int64_t)gridDim.x * 1024)
+    if (counted(mask, r)) m = max(m, idx[r + 1] - idx[r]);
+  for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
   __syncthreads();
-  const int p0 = blockIdx.x * kP;
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 16; ++w) m = max(m, wm[w]);
+    if (m) atomicMax(maxlen, m);
+  }
+}
+
+__global__ void __launch_bounds__(kWG) kmer_tile_kernel(const char *seq, const int32_t *idx, int64_t n,
+                                                        const uint8_t *mask, int npos, const int *maxlen,
+                                                        unsigned long long *out) {
+  __shared__ uint32_t t[kP * kNum];   // [position][id]
+  // tiles with a start position some counted read reaches
+  const int last_start = min(npos, *maxlen - (kK - 1));   // starts 0 .. last_start-1
+  const int T = last_start > 0 ? (last_start + kP - 1) / kP : 0;
+  const int b = (int)blockIdx.x, xcd = b & 7, slot = b >> 3;
+  const int classes = T ? (int)(gridDim.x >> 3) / T : 0;   // read-group classes per XCD
+  if (T == 0 || slot >= classes * T) return;
+  const int tile = slot % T, cls = slot / T;
+  const int p0 = tile * kP;
+  for (int i = threadIdx.x; i < kP * kNum; i += kWG) t[i] = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int part = lane & (kLanesPerRead - 1);   // the lane's start positions: p0 + 16 part + [0, 16)
   const int32_t data_end = __builtin_amdgcn_readfirstlane(idx[n]);
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
       (void *)seq, (short)0, data_end + HPGQ_DEVICE_SLACK, 0x00020000);
-  for (int64_t r = (int64_t)blockIdx.y * kWG + threadIdx.x; r < n; r += (int64_t)gridDim.y * kWG) {
-    if (mask && mask[r] != 1) continue;
-    const int a = idx[r];
-    const int last = min(idx[r + 1] - a - kK, npos - 1);   // last start position counted
-    if (last < p0) continue;
-    const v4u w = __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(a + p0), 0, 0);
-    const uint32_t w4 = __builtin_amdgcn_raw_buffer_load_b32(rs, (uint32_t)(a + p0 + 16), 0, 0);
-    uint32_t val[5], ok[5];
+  // read offsets and mask through descriptors too: the loads past the batch
+  // (the pipeline's prefetch past the last group) read 0 and move nothing
+  const __amdgpu_buffer_rsrc_t ri = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)idx, (short)0, (uint32_t)((n + 1) * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)mask, (short)0, mask ? (uint32_t)n : 0u, 0x00020000);
+  const int64_t ngroups = (n + kGroup - 1) / kGroup;
+  const int64_t gstride = 8 * (int64_t)classes;
+  const int64_t g0 = xcd + 8 * (int64_t)cls;
+  // a read's offsets and mask byte (the read's 4 lanes load the same words;
+  // unconditional loads: past the end they read 0, so the compiler counts
+  // the loads in flight exactly)
+  struct Meta {
+    int32_t a, e;
+    uint32_t m;
+  };
+  auto meta = [&](int64_t g) __attribute__((always_inline)) {
+    const int64_t r = g * kGroup + wave * kReadsPerWave + (lane >> 1);
+    const uint32_t ro = r < n ? (uint32_t)r : 0x3FFFFFF0u;
+    Meta M;
+    M.a = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(ri, ro * 4u, 0, 0);
+    M.e = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(ri, ro * 4u + 4u, 0, 0);
+    M.m = mask ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rm, ro, 0, 0) : (r < n ? 1u : 0u);
+    return M;
+  };
+  // the lane's 20 bytes (16 starts + 4): a 16-byte and a 4-byte load (part
+  // 0's last 4 are part 1's first; part 1's, the tile's last 4); a read's 2
+  // lanes read 36 contiguous bytes
+  struct Win {
+    v4u a;
+    uint32_t b;
+  };
+  auto window = [&](const Meta &M) __attribute__((always_inline)) {
+    const uint32_t o = (uint32_t)(M.a + p0 + kPosPerLane * part);
+    Win W;
+    W.a = __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0);
+    W.b = __builtin_amdgcn_raw_buffer_load_b32(rs, o + 16u, 0, 0);
+    return W;
+  };
+  // software pipeline: group g counted while g + stride's window and
+  // g + 2 stride's offsets are in flight
+  Meta cur = meta(g0);
+  Win w = window(cur);
+  Meta nxt = meta(g0 + gstride);
+  const uint32_t rowb = (uint32_t)(kPosPerLane * part) << 12;   // the lane's first position row (x 4096 B)
+  for (int64_t g = g0; g < ngroups; g += gstride) {
+    // the read's last start, relative to the lane's first (< 0: none here;
+    // masked-out reads: none)
+    const int last = cur.m == 1u ? min(cur.e - cur.a - kK, npos - 1) - (p0 + kPosPerLane * part) : -1;
+    uint32_t pk[5], bd[5];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) codes4(w[i], val[i], ok[i]);
-    codes4(w4, val[4], ok[4]);
-    uint32_t id = 0, vb = 0;
+    for (int i = 0; i < 4; ++i) codes4(w.a[i], pk[i], bd[i]);
+    codes4(w.b, pk[4], bd[4]);
+    w = window(nxt);   // next group's window (its offsets arrived during this group)
+    cur = nxt;
+    nxt = meta(g + 2 * gstride);
+    if (__ballot(last >= 0) == 0ull) continue;   // the whole wave's reads end before these starts
+    // the 20 codes as a 40-bit stream s1:s0, the first byte highest (byte i
+    // at bits 2(19 - i)): the 5-mer starting at j, first base most
+    // significant, is bits [2(15 - j), 2(20 - j))
+    const uint32_t s1 = pk[0];
+    const uint32_t s0 = (pk[1] << 24) | (pk[2] << 16) | (pk[3] << 8) | pk[4];
+    const uint32_t bad = bd[0] | (bd[1] << 4) | (bd[2] << 8) | (bd[3] << 12) | (bd[4] << 16);
+    // the 5-mer at j counts iff bytes j..j+4 are A/C/G/T and j <= last
+    uint32_t e = ~(bad | (bad >> 1) | (bad >> 2) | (bad >> 3) | (bad >> 4));
+    e &= last >= kPosPerLane - 1 ? 0xFFFFu : last >= 0 ? (2u << last) - 1u : 0u;
 #pragma unroll
-    for (int i = 0; i < kP + kK - 1; ++i) {
-      const uint32_t c = (val[i >> 2] >> (8 * (i & 3))) & 3u;
-      const uint32_t v = (ok[i >> 2] >> (8 * (i & 3))) & 1u;
-      id = ((id << 2) | c) & (kNum - 1);
-      vb = ((vb << 1) | v) & 31u;
-      const int j = i - (kK - 1);   // the 5-mer ending at byte i starts at p0 + j
-      if (j >= 0 && vb == 31u && j <= last - p0) atomicAdd(&t[id * kP + j], 1u);
+    for (int j = 0; j < kPosPerLane; ++j) {
+      // cell byte address ((16 part + j) * 1024 + id) * 4: the id cut out at
+      // bits 2..11 by one v_alignbit, the position row ORed in (v_bitop3);
+      // a start that does not count adds 0 (no select, no spare cell)
+      const int sh = 2 * (15 - j) - 2;
+      const uint32_t win = sh < 0 ? s0 << 2 : __builtin_amdgcn_alignbit(s1, s0, sh);
+      const uint32_t addr = __builtin_amdgcn_bitop3_b32(win, 0xFFCu, rowb + ((uint32_t)j << 12), 0xEA);
+      atomicAdd(reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(t) + addr), (e >> j) & 1u);
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < kNum * kP; i += kWG) {
-    const uint32_t v = t[i];
-    const int p = p0 + (i % kP);
-    if (v && p < npos) atomicAdd(&out[(size_t)(i / kP) * npos + p], (unsigned long long)v);
+  for (int i = threadIdx.x; i < kP * kNum; i += kWG) {
+    const uint32_t c = t[i];
+    const int p = p0 + i / kNum;
+    if (c && p < npos) atomicAdd(&out[(size_t)(i % kNum) * npos + p], (unsigned long long)c);
   }
 }
 
@@ -93,6 +198,7 @@ struct hpgq_kmers {
   hipStream_t stream = nullptr;
   bool own_stream = false;
   unsigned long long *d_out = nullptr;
+  int *d_maxlen = nullptr;   // per call: the longest counted read
   int cus = 0;
 };
 
@@ -119,7 +225,7 @@ int hpgq_kmers_open(hpgq_kmers_t **km, int device, int lmax, void *stream) {
     k->own_stream = true;
   }
   const size_t bytes = (size_t)hpgq::kmers::kNum * (size_t)(k->npos > 0 ? k->npos : 1) * 8;
-  if (hipMalloc(&k->d_out, bytes) != hipSuccess) {
+  if (hipMalloc(&k->d_out, bytes) != hipSuccess || hipMalloc(&k->d_maxlen, sizeof(int)) != hipSuccess) {
     hpgq_kmers_close(k);
     return HPGQ_E_NOMEM;
   }
@@ -137,6 +243,7 @@ void hpgq_kmers_close(hpgq_kmers_t *k) {
   (void)hipSetDevice(k->device);
   if (k->stream) (void)hipStreamSynchronize(k->stream);
   (void)hipFree(k->d_out);
+  (void)hipFree(k->d_maxlen);
   if (k->own_stream) (void)hipStreamDestroy(k->stream);
   delete k;
 }
@@ -147,13 +254,24 @@ int hpgq_kmers_count_device(hpgq_kmers_t *k, const hpgq_batch_t *b, const uint8_
   if (!b->seq || !b->data_indices) return HPGQ_E_INVALID;
   HPGQ_HIP_TRY(hipSetDevice(k->device));
   using namespace hpgq::kmers;
-  const int tiles = (k->npos + kP - 1) / kP;
-  const int64_t need = (b->num_reads + kWG - 1) / kWG;
-  // about two resident workgroups per CU over all tiles
-  const int64_t ny = std::max<int64_t>(1, std::min<int64_t>(need, (2 * k->cus + tiles - 1) / tiles));
-  hipLaunchKernelGGL(kmer_kernel, dim3(tiles, (unsigned)ny), dim3(kWG), 0, k->stream, b->seq,
-                     b->data_indices, (int64_t)b->num_reads, mask, k->npos, k->d_out);
-  HPGQ_HIP_TRY(hipGetLastError());
+  // one resident workgroup per CU (128 KB of LDS); 8 x (tiles the lmax allows)
+  // x read-group classes, so every tile of a class has its workgroup on each
+  // XCD (the kernel takes the tiles the longest read needs and idles the rest)
+  const int tmax = (k->npos + kP - 1) / kP;
+  const int grid = 8 * tmax * std::max(1, k->cus / (8 * tmax));
+  constexpr int64_t kPart = (int64_t)1 << 28;   // reads per launch (32-bit offsets into idx)
+  for (int64_t lo = 0; lo < b->num_reads; lo += kPart) {
+    const int64_t n = std::min(kPart, b->num_reads - lo);
+    const int32_t *ix = b->data_indices + lo;
+    const uint8_t *mk = mask ? mask + lo : nullptr;
+    HPGQ_HIP_TRY(hipMemsetAsync(k->d_maxlen, 0, sizeof(int), k->stream));
+    hipLaunchKernelGGL(kmer_maxlen_kernel, dim3((unsigned)std::min<int64_t>((n + 1023) / 1024, k->cus)), dim3(1024),
+                       0, k->stream, ix, n, mk, k->d_maxlen);
+    HPGQ_HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(kmer_tile_kernel, dim3((unsigned)grid), dim3(kWG), 0, k->stream, b->seq, ix, n, mk, k->npos,
+                       (const int *)k->d_maxlen, k->d_out);
+    HPGQ_HIP_TRY(hipGetLastError());
+  }
   return HPGQ_OK;
 }
 

@@ -90,3 +90,29 @@ def test_kmers_random_combinations(case):
         O.kmers(b, lmax, masks[i] if masks else None, want)
     got = gpu_kmers(lmax, batches, masks, offset=int(rng.integers(0, 40)))
     np.testing.assert_array_equal(got, want)
+
+
+def test_kmers_lmax1024_short_reads_and_empty_masks():
+    """The CLI's --lmax 1024 on 150 bp reads (the tiles past the longest counted
+    read idle), a batch whose reads are all masked out and one of reads
+    shorter than a 5-mer (no tile at all), then a long-read batch on the same
+    counters: every tile still adds exactly once."""
+    rng = np.random.default_rng(11)
+    short = O.synth(50_000, seed=3, L=150)
+    masked = _random_reads(rng, 500, 0, 900)
+    tiny = _random_reads(rng, 700, 0, 4)
+    long_ = _random_reads(rng, 900, 500, 1100)
+    batches = [short, masked, tiny, long_]
+    masks = [np.ones(short.n, np.uint8), np.zeros(masked.n, np.uint8), np.ones(tiny.n, np.uint8),
+             (rng.random(long_.n) < 0.5).astype(np.uint8)]
+    want = np.zeros((1024, 1020), dtype=np.uint64)
+    for b, m in zip(batches, masks):
+        O.kmers(b, 1024, m, want)
+    np.testing.assert_array_equal(gpu_kmers(1024, batches, masks), want)
+
+
+def test_kmers_many_groups_per_workgroup():
+    """More read groups than workgroups: each workgroup's tile walks several
+    groups of its class (2.5 M reads, lmax 150)."""
+    reads = O.synth(2_500_000, seed=4, L=150)
+    np.testing.assert_array_equal(gpu_kmers(150, [reads]), O.kmers(reads, 150))

@@ -21,6 +21,7 @@ ap.add_argument("--iters", type=int, default=5)
 ap.add_argument("--mode", default="c2")
 ap.add_argument("--L", type=int, default=150)
 ap.add_argument("--k", type=int, default=7)
+ap.add_argument("--kmers", action="store_true", help="also count 5-mers (stats --kmers) after the engine")
 args = ap.parse_args()
 
 dev = torch.device("cuda", 0)
@@ -108,4 +109,11 @@ for _ in range(args.iters):
 eng.sync()
 c = eng.counters()
 print("reads", n, "passed", int(c[H.S_NUM_PASSED]), "iters", args.iters)
+if args.kmers:   # then --kmers counts of the passed reads (the engine's mask), args.iters times
+    km = H.Kmers(L, stream=eng.stream)
+    for _ in range(args.iters):
+        km.count_device(bs[0], mask.data_ptr())
+    km.sync()
+    print("kmers", int(km.by_pos().sum()))
+    km.close()
 eng.close()
