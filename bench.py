@@ -583,7 +583,7 @@ def main():
 
     # sanity: every read accounted for
     if kmers:
-        assert int(km.by_pos().sum()) > 0
+        assert int(km.by_pos().sum()) > 0 or os.environ.get("HPGQ_BENCH_NOCHECK")   # (timing probes)
     elif cgr:
         _ts, _tq, wc = eng.tables()
         assert wc > 0 or os.environ.get("HPGQ_BENCH_NOCHECK")   # (timing-probe builds add nothing)

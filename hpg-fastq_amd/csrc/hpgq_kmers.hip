@@ -12,7 +12,8 @@
 // counters, too many for one workgroup's LDS, so a workgroup owns a TILE of
 // kP start positions ([kP][1024] u32 = 128 KB, position-major so that the 64
 // lanes' adds at one position spread over the banks by id) for the whole
-// call and adds it to by_pos once at its end.  Every tile re-reads the
+// call and stores it to its slab at the end; kmer_reduce_kernel adds a tile's
+// slabs into by_pos.  Every tile re-reads the
 // reads' windows; the workgroups that hold the T tiles of one read group sit
 // on one XCD and walk the same reads in the same order, so the re-reads hit
 // that XCD's L2 (blockIdx -> XCD is round robin: b mod 8).  A prepass takes
@@ -45,6 +46,7 @@ constexpr int kLanesPerRead = 2;      // a read's tile: 2 lanes x 16 start posit
 constexpr int kPosPerLane = kP / kLanesPerRead;
 constexpr int kReadsPerWave = 64 / kLanesPerRead;
 constexpr int kGroup = (kWG / 64) * kReadsPerWave;   // reads per workgroup step (512)
+static_assert(kWG == kNum, "the flush gives each thread one id");
 
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
@@ -68,8 +70,8 @@ __device__ __forceinline__ void codes4(uint32_t w, uint32_t &packed, uint32_t &b
 
 __device__ __forceinline__ bool counted(const uint8_t *mask, int64_t r) { return !mask || mask[r] == 1; }
 
-// one workgroup per CU, grid-stride; one atomic per workgroup (one per wave
-// made 8 K atomics on one word: 112 us per 10 M reads)
+// eight workgroups per CU, grid-stride; one atomic per workgroup (one per
+// wave made 8 K atomics on one word: 112 us per 10 M reads)
 __global__ void __launch_bounds__(1024) kmer_maxlen_kernel(const int32_t *idx, int64_t n, const uint8_t *mask,
                                                            int *maxlen) {
   __shared__ int wm[16];
@@ -87,7 +89,7 @@ __global__ void __launch_bounds__(1024) kmer_maxlen_kernel(const int32_t *idx, i
 
 __global__ void __launch_bounds__(kWG) kmer_tile_kernel(const char *seq, const int32_t *idx, int64_t n,
                                                         const uint8_t *mask, int npos, const int *maxlen,
-                                                        unsigned long long *out) {
+                                                        uint32_t *slab) {
   __shared__ uint32_t t[kP * kNum];   // [position][id]
   // tiles with a start position some counted read reaches
   const int last_start = min(npos, *maxlen - (kK - 1));   // starts 0 .. last_start-1
@@ -182,11 +184,32 @@ __global__ void __launch_bounds__(kWG) kmer_tile_kernel(const char *seq, const i
     }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < kP * kNum; i += kWG) {
-    const uint32_t c = t[i];
-    const int p = p0 + i / kNum;
-    if (c && p < npos) atomicAdd(&out[(size_t)(i % kNum) * npos + p], (unsigned long long)c);
-  }
+  // the table goes to this workgroup's slab with plain coalesced stores;
+  // kmer_reduce_kernel sums a tile's slabs into by_pos (u64 atomics straight
+  // from here -- one cache line per lane, 48 workgroups per cell -- took 300
+  // us of a 970 us launch)
+  uint32_t *my = slab + (size_t)b * (kP * kNum);
+  for (int i = threadIdx.x; i < kP * kNum; i += kWG) my[i] = t[i];
+}
+
+// by_pos[id][p0 + row] += the sum of a tile's slabs (8 XCDs x classes); one
+// thread per (tile, row, id), consecutive threads consecutive ids (the slab
+// reads coalesce)
+__global__ void __launch_bounds__(256) kmer_reduce_kernel(const uint32_t *slab, int npos, const int *maxlen, int grid,
+                                                          unsigned long long *out) {
+  const int last_start = min(npos, *maxlen - (kK - 1));
+  const int T = last_start > 0 ? (last_start + kP - 1) / kP : 0;
+  const int64_t f = (int64_t)blockIdx.x * 256 + threadIdx.x;   // tile * kP * kNum + row * kNum + id
+  const int tile = (int)(f / (kP * kNum)), cell = (int)(f % (kP * kNum));
+  const int classes = T ? (grid >> 3) / T : 0;
+  if (tile >= T) return;
+  const int p = tile * kP + cell / kNum;
+  if (p >= npos) return;
+  uint32_t sum = 0;
+  for (int cls = 0; cls < classes; ++cls)
+#pragma unroll
+    for (int x = 0; x < 8; ++x) sum += slab[((size_t)(8 * (cls * T + tile) + x)) * (kP * kNum) + cell];
+  if (sum) out[(size_t)(cell % kNum) * npos + p] += sum;
 }
 
 }  // namespace kmers
@@ -199,6 +222,8 @@ struct hpgq_kmers {
   bool own_stream = false;
   unsigned long long *d_out = nullptr;
   int *d_maxlen = nullptr;   // per call: the longest counted read
+  uint32_t *d_slab = nullptr;   // per tile workgroup: its table of the call
+  int grid = 0;
   int cus = 0;
 };
 
@@ -234,6 +259,19 @@ int hpgq_kmers_open(hpgq_kmers_t **km, int device, int lmax, void *stream) {
     hpgq_kmers_close(k);
     return HPGQ_E_HIP;
   }
+  {
+    using namespace hpgq::kmers;
+    // one resident workgroup per CU (128 KB of LDS); 8 x (tiles the lmax
+    // allows) x read-group classes, so every tile of a class has its
+    // workgroup on each XCD (the kernel takes the tiles the longest read
+    // needs and idles the rest)
+    const int tmax = std::max(1, (k->npos + kP - 1) / kP);
+    k->grid = 8 * tmax * std::max(1, k->cus / (8 * tmax));
+    if (k->npos > 0 && hipMalloc(&k->d_slab, (size_t)k->grid * kP * kNum * sizeof(uint32_t)) != hipSuccess) {
+      hpgq_kmers_close(k);
+      return HPGQ_E_NOMEM;
+    }
+  }
   *km = k;
   return HPGQ_OK;
 }
@@ -244,6 +282,7 @@ void hpgq_kmers_close(hpgq_kmers_t *k) {
   if (k->stream) (void)hipStreamSynchronize(k->stream);
   (void)hipFree(k->d_out);
   (void)hipFree(k->d_maxlen);
+  (void)hipFree(k->d_slab);
   if (k->own_stream) (void)hipStreamDestroy(k->stream);
   delete k;
 }
@@ -254,22 +293,21 @@ int hpgq_kmers_count_device(hpgq_kmers_t *k, const hpgq_batch_t *b, const uint8_
   if (!b->seq || !b->data_indices) return HPGQ_E_INVALID;
   HPGQ_HIP_TRY(hipSetDevice(k->device));
   using namespace hpgq::kmers;
-  // one resident workgroup per CU (128 KB of LDS); 8 x (tiles the lmax allows)
-  // x read-group classes, so every tile of a class has its workgroup on each
-  // XCD (the kernel takes the tiles the longest read needs and idles the rest)
   const int tmax = (k->npos + kP - 1) / kP;
-  const int grid = 8 * tmax * std::max(1, k->cus / (8 * tmax));
   constexpr int64_t kPart = (int64_t)1 << 28;   // reads per launch (32-bit offsets into idx)
   for (int64_t lo = 0; lo < b->num_reads; lo += kPart) {
     const int64_t n = std::min(kPart, b->num_reads - lo);
     const int32_t *ix = b->data_indices + lo;
     const uint8_t *mk = mask ? mask + lo : nullptr;
     HPGQ_HIP_TRY(hipMemsetAsync(k->d_maxlen, 0, sizeof(int), k->stream));
-    hipLaunchKernelGGL(kmer_maxlen_kernel, dim3((unsigned)std::min<int64_t>((n + 1023) / 1024, k->cus)), dim3(1024),
-                       0, k->stream, ix, n, mk, k->d_maxlen);
+    hipLaunchKernelGGL(kmer_maxlen_kernel, dim3((unsigned)std::min<int64_t>((n + 1023) / 1024, 8 * k->cus)),
+                       dim3(1024), 0, k->stream, ix, n, mk, k->d_maxlen);
     HPGQ_HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(kmer_tile_kernel, dim3((unsigned)grid), dim3(kWG), 0, k->stream, b->seq, ix, n, mk, k->npos,
-                       (const int *)k->d_maxlen, k->d_out);
+    hipLaunchKernelGGL(kmer_tile_kernel, dim3((unsigned)k->grid), dim3(kWG), 0, k->stream, b->seq, ix, n, mk,
+                       k->npos, (const int *)k->d_maxlen, k->d_slab);
+    HPGQ_HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(kmer_reduce_kernel, dim3((unsigned)(((int64_t)tmax * kP * kNum + 255) / 256)), dim3(256), 0,
+                       k->stream, (const uint32_t *)k->d_slab, k->npos, (const int *)k->d_maxlen, k->grid, k->d_out);
     HPGQ_HIP_TRY(hipGetLastError());
   }
   return HPGQ_OK;
