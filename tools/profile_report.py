@@ -1,6 +1,6 @@
 """Turn a tools/gpu_profile.sh run (gpurun_out/prof) into the committed profiles/.
 
-  python tools/profile_report.py --round r01
+  python tools/profile_report.py --round r03 --prof gpurun_out/prof3
 
 Writes
   profiles/<round>_bench_kernel_stats.csv   rocprofv3 --stats of `python3 bench.py --gpus 1
@@ -25,12 +25,12 @@ PROF = os.path.join(ROOT, "gpurun_out", "prof")
 OUT = os.path.join(ROOT, "profiles")
 
 
-KERNELS = {"c2": ("engine_tri_kernel", "engine_kernel", "trim_kernel"),
-           "c3": ("engine_tri_kernel", "engine_kernel", "trim_kernel"),
-           "c4": ("engine_tri_kernel", "engine_kernel", "trim_kernel"),
+ENG = ("engine_tri_kernel", "engine_tri_x_kernel", "engine_kernel")
+KERNELS = {"c2": ENG, "c3": ENG, "c4": ENG, "c4_noor": ENG, "c4_pe": ENG,
            "c5": ("cgr_stream_kernel", "span_first_kernel"),
-           "c2_lr": ("engine_tri_x_kernel", "engine_kernel"),
-           "c2_250": ("engine_tri_kernel", "engine_kernel")}
+           "c5_valid": ("cgr_stream_kernel", "span_first_kernel"),
+           "c2_lr": ENG, "c2_250": ENG,
+           "c2_kmers": ("kmer_tile_kernel", "kmer_maxlen_kernel", "kmer_reduce_kernel")}
 
 
 def counters(sub, kerns):
@@ -82,7 +82,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--round", required=True)
     ap.add_argument("--kernel", default="engine_tri_kernel")
+    ap.add_argument("--prof", default=None, help="profile output dir (default gpurun_out/prof)")
     a = ap.parse_args()
+    global PROF
+    if a.prof:
+        PROF = os.path.join(ROOT, a.prof) if not os.path.isabs(a.prof) else a.prof
     os.makedirs(OUT, exist_ok=True)
     stats = glob.glob(os.path.join(PROF, "trace", "**", "run_kernel_stats.csv"), recursive=True)
     if stats:
@@ -102,9 +106,20 @@ def main():
             sq1, _ = counters("sq1", a.kernel)
             sq2, _ = counters("sq2", a.kernel)
             rec["sq"] = {**sq1, **sq2}
+        if cfg in ("c5", "c5_valid"):   # LDS bound of the CGR stream pass
+            mode = "cgr" if cfg == "c5" else "cgrv"
+            l1, _ = counters(f"lds1_{mode}", "cgr_stream_kernel")
+            l2, _ = counters(f"lds2_{mode}", "cgr_stream_kernel")
+            if l1 or l2:
+                rec["sq"] = {**l1, **l2}
+                if l2.get("SQ_LDS_IDX_ACTIVE"):
+                    rec["lds_conflict_ratio"] = round(l2["SQ_LDS_BANK_CONFLICT"] / l2["SQ_LDS_IDX_ACTIVE"], 4)
         cb = bench_line(os.path.join(PROF, f"bench_{cfg}.json"))
         if cb:
             json.dump(cb, open(os.path.join(OUT, f"{a.round}_bench_{cfg}.json"), "w"), indent=1)
+        bt = glob.glob(os.path.join(PROF, f"btrace_{cfg}", "**", "run_kernel_stats.csv"), recursive=True)
+        if bt:
+            shutil.copy(bt[0], os.path.join(OUT, f"{a.round}_bench_{cfg}_kernel_stats.csv"))
         for name in (f"{a.round}_pmc_engine_{cfg}.json", f"pmc_engine_{cfg}.json"):
             json.dump(rec, open(os.path.join(OUT, name), "w"), indent=1)
         print(cfg, json.dumps({k: v for k, v in rec.items() if k != "sq"}))
