@@ -10,27 +10,36 @@
 //
 // Kernels.  A 5-mer's counter lives at (start position, id): 1024 x lmax-4
 // counters, too many for one workgroup's LDS, so a workgroup owns a TILE of
-// kP start positions ([kP][1024] u32 = 128 KB, position-major so that the 64
-// lanes' adds at one position spread over the banks by id) for the whole
-// call and stores it to its slab at the end; kmer_reduce_kernel adds a tile's
-// slabs into by_pos.  Every tile re-reads the
-// reads' windows; the workgroups that hold the T tiles of one read group sit
-// on one XCD and walk the same reads in the same order, so the re-reads hit
-// that XCD's L2 (blockIdx -> XCD is round robin: b mod 8).  A prepass takes
-// the longest counted read, so tiles past it (the CLI's lmax 1024 on 150 bp
+// kP = 32 start positions ([1024][kP] u32 = 128 KB) for the whole call and
+// stores it to its slab at the end; kmer_reduce_kernel adds a tile's slabs
+// into by_pos.  Every tile re-reads the reads' windows; the workgroups that
+// hold the T tiles of one read group sit on one XCD and walk the same reads in
+// the same order, so the re-reads hit that XCD's L2 (blockIdx -> XCD is round
+// robin: b mod 8).  When lmax allows more than 8 tiles a prepass takes the
+// longest counted read, so tiles past it (the CLI's lmax 1024 on 150 bp
 // reads) exit at once instead of scanning every read.
 //   kmer_maxlen_kernel  max length over the counted reads (atomicMax)
-//   kmer_tile_kernel    two lanes per read, 16 start positions each (one
-//                       lane per read made every 16-byte load touch its own
-//                       segment: the texture addresser was 85 % busy; four
-//                       lanes per read spent more on per-lane set-up than it
-//                       saved), software-pipelined (the next group's bytes
-//                       are fetched while this one is counted, its offsets
-//                       one group earlier still): 20 bytes per lane, 2-bit
-//                       codes packed by v_dot4, a mask of the 5-mers that
-//                       count (OR of 5 shifts of the non-ACGT bits), then per
-//                       start position one v_alignbit + v_bitop3 for the cell
-//                       address and one ds_add_u32 of 0 or 1.
+//   kmer_tile_kernel    two lanes per read and tile (20 bytes each: 16
+//                       starts + 4), software-pipelined (the next group's
+//                       bytes are fetched while this one is counted, its
+//                       offsets one group earlier still).  Table id-major,
+//                       cell (p, id) at id * 32 + p: a start position is an
+//                       LDS bank.  The 32 lanes of a group visit their starts
+//                       in rotated orders, so at every step they sit on 32
+//                       distinct positions and their ds_add_u32 hit 32
+//                       distinct banks (position-major with every lane at the
+//                       same position made random ids collide: 71 % of the
+//                       LDS cycles were bank conflicts).  Per byte: a v_perm
+//                       LUT for the 2-bit code and one for the exactness test;
+//                       per start: one v_alignbit (the lane's shift for that
+//                       step), one v_bitop3 (its position's bank), one v_bfe
+//                       (0 or 1) and the add.  Bound: the texture addresser
+//                       (tools/ubench/window_rates.hip: gathering a read's
+//                       36-byte tile window costs ~4.6 TA cycles per read and
+//                       tile in any lane shape, as much as streaming the whole
+//                       150-byte read; one lane per read was as fast but made
+//                       1024-read groups whose L2 re-reads doubled the HBM
+//                       traffic).
 #include "hpgq_common.h"
 
 #include <algorithm>
@@ -40,44 +49,66 @@ namespace kmers {
 
 constexpr int kK = 5;
 constexpr int kNum = 1 << (2 * kK);   // 1024
-constexpr int kP = 32;                // start positions per tile
+constexpr int kP = 32;                // start positions per tile (one LDS bank each)
 constexpr int kWG = 1024;
-constexpr int kLanesPerRead = 2;      // a read's tile: 2 lanes x 16 start positions
-constexpr int kPosPerLane = kP / kLanesPerRead;
-constexpr int kReadsPerWave = 64 / kLanesPerRead;
-constexpr int kGroup = (kWG / 64) * kReadsPerWave;   // reads per workgroup step (512)
+constexpr int kReadsPerWave = 32;     // two lanes per read
+constexpr int kGroup = kWG / 2;       // reads per workgroup step
+constexpr int kSpill = 8;             // tiles above which the maxlen prepass runs
 static_assert(kWG == kNum, "the flush gives each thread one id");
 
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
-// byte & 7 is one-to-one on A(1) C(3) T(4) G(7); the expected byte per code
-// (0x01 never matches) and the 2-bit code per code
+// byte & 7 is one-to-one on A(1) C(3) T(4) G(7).  kEx*: the expected byte per
+// code; the codes no base has get bytes whose low 3 bits are neither the code
+// nor the code ^ 4, so that (byte ^ expected) is never 0 or 0x0C for them
+// (see codes4).  kVal*: the 2-bit code per code.
 constexpr uint32_t kExLo = 0x43014101u;   // codes 0..3: -, A, -, C
-constexpr uint32_t kExHi = 0x47010154u;   // codes 4..7: T, -, -, G
+constexpr uint32_t kExHi = 0x47010454u;   // codes 4..7: T, -, -, G
 constexpr uint32_t kValLo = 0x01000000u;  // C = 1 at code 3
 constexpr uint32_t kValHi = 0x02000003u;  // T = 3 at code 4, G = 2 at code 7
 
 // 4 bytes -> their 2-bit codes packed first byte highest (byte i of 4 at
-// bits 2(3-i)) and a bit per byte that is NOT exactly A/C/G/T (bit i)
+// bits 2(3-i)) and a bit per byte that is NOT exactly A/C/G/T (bit i).
+// d = byte ^ expected is 0 exactly for A/C/G/T; as a v_perm selector over
+// {0xFFFFFFFF, 0xFFFFFF00} it gives 0x00 for 0 and 0xFF for any other value
+// but 12 (selectors 1-11 pick 0xFF bytes or sign bits that are set, >= 13 is
+// 0xFF), and 12 cannot occur: byte ^ 0x0C has low 3 bits code ^ 4, and no
+// expected byte's low 3 bits are its code ^ 4.
 __device__ __forceinline__ void codes4(uint32_t w, uint32_t &packed, uint32_t &bad) {
   const uint32_t code = w & 0x07070707u;
   const uint32_t d = w ^ __builtin_amdgcn_perm(kExHi, kExLo, code);
-  // bit 7 of each byte of d that is nonzero: ((d & 7F..) + 7F..) | d, & 80..
-  const uint32_t nz = __builtin_amdgcn_bitop3_b32((d & 0x7F7F7F7Fu) + 0x7F7F7F7Fu, d, 0x80808080u, 0xA8);   // (a | b) & c
-  bad = __builtin_amdgcn_udot4(nz >> 7, 0x08040201u, 0u, false);
+  const uint32_t bm = __builtin_amdgcn_perm(0xFFFFFFFFu, 0xFFFFFF00u, d);
+  bad = __builtin_amdgcn_udot4(bm & 0x01010101u, 0x08040201u, 0u, false);
   packed = __builtin_amdgcn_udot4(__builtin_amdgcn_perm(kValHi, kValLo, code), 0x01041040u, 0u, false);
 }
 
 __device__ __forceinline__ bool counted(const uint8_t *mask, int64_t r) { return !mask || mask[r] == 1; }
 
-// eight workgroups per CU, grid-stride; one atomic per workgroup (one per
-// wave made 8 K atomics on one word: 112 us per 10 M reads)
+// eight workgroups per CU, grid-stride, four reads per thread (one 16-byte
+// offset load); one atomic per workgroup (one per wave made 8 K atomics on
+// one word: 112 us per 10 M reads)
 __global__ void __launch_bounds__(1024) kmer_maxlen_kernel(const int32_t *idx, int64_t n, const uint8_t *mask,
                                                            int *maxlen) {
   __shared__ int wm[16];
+  const __amdgpu_buffer_rsrc_t ri = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)idx, (short)0, (uint32_t)((n + 1) * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)mask, (short)0, mask ? (uint32_t)n : 0u, 0x00020000);
   int m = 0;
-  for (int64_t r = (int64_t)blockIdx.x * 1024 + threadIdx.x; r < n; r += (int64_t)gridDim.x * 1024)
-    if (counted(mask, r)) m = max(m, idx[r + 1] - idx[r]);
+  for (int64_t r = 4 * ((int64_t)blockIdx.x * 1024 + threadIdx.x); r < n; r += 4 * (int64_t)gridDim.x * 1024) {
+    if (r + 4 > n) {   // the last reads: one by one (a dword past n would read 0)
+      for (int64_t i = r; i < n; ++i)
+        if (counted(mask, i)) m = max(m, idx[i + 1] - idx[i]);
+      break;
+    }
+    const v4u a = __builtin_amdgcn_raw_buffer_load_b128(ri, (uint32_t)r * 4u, 0, 0);
+    const int32_t e = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(ri, (uint32_t)r * 4u + 16u, 0, 0);
+    const uint32_t mk = mask ? __builtin_amdgcn_raw_buffer_load_b32(rm, (uint32_t)r, 0, 0) : 0x01010101u;
+    const int32_t b[5] = {(int32_t)a[0], (int32_t)a[1], (int32_t)a[2], (int32_t)a[3], e};
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (((mk >> (8 * i)) & 0xFFu) == 1u) m = max(m, b[i + 1] - b[i]);
+  }
   for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o));
   if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = m;
   __syncthreads();
@@ -87,12 +118,34 @@ __global__ void __launch_bounds__(1024) kmer_maxlen_kernel(const int32_t *idx, i
   }
 }
 
+// the 16 starts of one half-tile of a lane's window: its code stream shifted
+// for the alignbit cuts (t1:t0 = the 20 bytes' codes << 7, first byte
+// highest: the 5-mer at half position h is bits [2(15 - h) + 7, + 10)) and
+// its count mask rotated to the lane's visiting order (bit j = the start the
+// lane visits at step j)
+struct Half {
+  uint32_t t1, t0, er;
+};
+
+__device__ __forceinline__ Half half_of(const uint32_t (&pk)[5], const uint32_t (&bd)[5], int last, int q) {
+  const uint32_t s0 = (pk[1] << 24) | (pk[2] << 16) | (pk[3] << 8) | pk[4];
+  const uint32_t b = bd[0] | (bd[1] << 4) | (bd[2] << 8) | (bd[3] << 12) | (bd[4] << 16);
+  // the 5-mer at h counts iff bytes h..h+4 are A/C/G/T and h <= last
+  uint32_t e = ~(b | (b >> 1) | (b >> 2) | (b >> 3) | (b >> 4));
+  e &= last >= 15 ? 0xFFFFu : last >= 0 ? (2u << last) - 1u : 0u;
+  Half H;
+  H.t1 = __builtin_amdgcn_alignbit(pk[0], s0, 25);
+  H.t0 = s0 << 7;
+  H.er = (e | (e << 16)) >> q;
+  return H;
+}
+
 __global__ void __launch_bounds__(kWG) kmer_tile_kernel(const char *seq, const int32_t *idx, int64_t n,
                                                         const uint8_t *mask, int npos, const int *maxlen,
                                                         uint32_t *slab) {
-  __shared__ uint32_t t[kP * kNum];   // [position][id]
+  __shared__ uint32_t t[kNum * kP];   // [id][position]
   // tiles with a start position some counted read reaches
-  const int last_start = min(npos, *maxlen - (kK - 1));   // starts 0 .. last_start-1
+  const int last_start = min(npos, (maxlen ? *maxlen : npos + kK - 1) - (kK - 1));   // starts 0 .. last_start-1
   const int T = last_start > 0 ? (last_start + kP - 1) / kP : 0;
   const int b = (int)blockIdx.x, xcd = b & 7, slot = b >> 3;
   const int classes = T ? (int)(gridDim.x >> 3) / T : 0;   // read-group classes per XCD
@@ -102,7 +155,11 @@ __global__ void __launch_bounds__(kWG) kmer_tile_kernel(const char *seq, const i
   for (int i = threadIdx.x; i < kP * kNum; i += kWG) t[i] = 0;
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int part = lane & (kLanesPerRead - 1);   // the lane's start positions: p0 + 16 part + [0, 16)
+  // lanes 2i, 2i + 1 take read i's half-tiles hl = 0, 1 (starts 16 hl + [0,
+  // 16)); the lane visits start 16 hl + (q + j) mod 16 at step j, so the 32
+  // lanes of a group (lanes 0-31, 32-63: one LDS cycle each) sit on 32
+  // distinct positions at every step
+  const int q = (lane >> 1) & 15, hl = lane & 1;
   const int32_t data_end = __builtin_amdgcn_readfirstlane(idx[n]);
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
       (void *)seq, (short)0, data_end + HPGQ_DEVICE_SLACK, 0x00020000);
@@ -115,9 +172,8 @@ __global__ void __launch_bounds__(kWG) kmer_tile_kernel(const char *seq, const i
   const int64_t ngroups = (n + kGroup - 1) / kGroup;
   const int64_t gstride = 8 * (int64_t)classes;
   const int64_t g0 = xcd + 8 * (int64_t)cls;
-  // a read's offsets and mask byte (the read's 4 lanes load the same words;
-  // unconditional loads: past the end they read 0, so the compiler counts
-  // the loads in flight exactly)
+  // a read's offsets and mask byte (unconditional loads: past the end they
+  // read 0, so the compiler counts the loads in flight exactly)
   struct Meta {
     int32_t a, e;
     uint32_t m;
@@ -131,56 +187,55 @@ __global__ void __launch_bounds__(kWG) kmer_tile_kernel(const char *seq, const i
     M.m = mask ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rm, ro, 0, 0) : (r < n ? 1u : 0u);
     return M;
   };
-  // the lane's 20 bytes (16 starts + 4): a 16-byte and a 4-byte load (part
-  // 0's last 4 are part 1's first; part 1's, the tile's last 4); a read's 2
-  // lanes read 36 contiguous bytes
+  // the lane's 20 bytes (16 starts + 4): a read's two lanes read 36
+  // contiguous bytes
   struct Win {
     v4u a;
-    uint32_t b;
+    uint32_t c;
   };
   auto window = [&](const Meta &M) __attribute__((always_inline)) {
-    const uint32_t o = (uint32_t)(M.a + p0 + kPosPerLane * part);
+    const uint32_t o = (uint32_t)(M.a + p0 + 16 * hl);
     Win W;
     W.a = __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0);
-    W.b = __builtin_amdgcn_raw_buffer_load_b32(rs, o + 16u, 0, 0);
+    W.c = __builtin_amdgcn_raw_buffer_load_b32(rs, o + 16u, 0, 0);
     return W;
   };
+  // per step j: the alignbit shift of the visited start (30 - 2 (q + j mod
+  // 16); alignbit reads 5 bits) and its cell's position bits
+  uint32_t sh[16], row[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const uint32_t h = (uint32_t)((q + j) & 15);
+    sh[j] = 30u - 2u * h;
+    row[j] = 4u * (h + 16u * (uint32_t)hl);
+  }
+  constexpr uint32_t kIdBits = (uint32_t)(kNum - 1) << 7;   // id * 128 = id * kP * 4
   // software pipeline: group g counted while g + stride's window and
   // g + 2 stride's offsets are in flight
   Meta cur = meta(g0);
   Win w = window(cur);
   Meta nxt = meta(g0 + gstride);
-  const uint32_t rowb = (uint32_t)(kPosPerLane * part) << 12;   // the lane's first position row (x 4096 B)
   for (int64_t g = g0; g < ngroups; g += gstride) {
-    // the read's last start, relative to the lane's first (< 0: none here;
+    // the read's last start, relative to the tile's first (< 0: none here;
     // masked-out reads: none)
-    const int last = cur.m == 1u ? min(cur.e - cur.a - kK, npos - 1) - (p0 + kPosPerLane * part) : -1;
+    const int last = cur.m == 1u ? min(cur.e - cur.a - kK, npos - 1) - p0 : -1;
     uint32_t pk[5], bd[5];
+    const uint32_t wd[5] = {w.a[0], w.a[1], w.a[2], w.a[3], w.c};
 #pragma unroll
-    for (int i = 0; i < 4; ++i) codes4(w.a[i], pk[i], bd[i]);
-    codes4(w.b, pk[4], bd[4]);
+    for (int i = 0; i < 5; ++i) codes4(wd[i], pk[i], bd[i]);
     w = window(nxt);   // next group's window (its offsets arrived during this group)
     cur = nxt;
     nxt = meta(g + 2 * gstride);
     if (__ballot(last >= 0) == 0ull) continue;   // the whole wave's reads end before these starts
-    // the 20 codes as a 40-bit stream s1:s0, the first byte highest (byte i
-    // at bits 2(19 - i)): the 5-mer starting at j, first base most
-    // significant, is bits [2(15 - j), 2(20 - j))
-    const uint32_t s1 = pk[0];
-    const uint32_t s0 = (pk[1] << 24) | (pk[2] << 16) | (pk[3] << 8) | pk[4];
-    const uint32_t bad = bd[0] | (bd[1] << 4) | (bd[2] << 8) | (bd[3] << 12) | (bd[4] << 16);
-    // the 5-mer at j counts iff bytes j..j+4 are A/C/G/T and j <= last
-    uint32_t e = ~(bad | (bad >> 1) | (bad >> 2) | (bad >> 3) | (bad >> 4));
-    e &= last >= kPosPerLane - 1 ? 0xFFFFu : last >= 0 ? (2u << last) - 1u : 0u;
+    const Half hf = half_of(pk, bd, last - 16 * hl, q);
 #pragma unroll
-    for (int j = 0; j < kPosPerLane; ++j) {
-      // cell byte address ((16 part + j) * 1024 + id) * 4: the id cut out at
-      // bits 2..11 by one v_alignbit, the position row ORed in (v_bitop3);
-      // a start that does not count adds 0 (no select, no spare cell)
-      const int sh = 2 * (15 - j) - 2;
-      const uint32_t win = sh < 0 ? s0 << 2 : __builtin_amdgcn_alignbit(s1, s0, sh);
-      const uint32_t addr = __builtin_amdgcn_bitop3_b32(win, 0xFFCu, rowb + ((uint32_t)j << 12), 0xEA);
-      atomicAdd(reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(t) + addr), (e >> j) & 1u);
+    for (int j = 0; j < 16; ++j) {
+      // cell byte address id * 128 + position * 4: the id cut out at bits
+      // 7..16 by one v_alignbit, the position's bits from row (v_bitop3);
+      // a start that does not count adds 0
+      const uint32_t win = __builtin_amdgcn_alignbit(hf.t1, hf.t0, sh[j]);
+      const uint32_t addr = __builtin_amdgcn_bitop3_b32(win, kIdBits, row[j], 0xEA);   // (a & b) | c
+      atomicAdd(reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(t) + addr), __builtin_amdgcn_ubfe(hf.er, j, 1));
     }
   }
   __syncthreads();
@@ -193,23 +248,23 @@ __global__ void __launch_bounds__(kWG) kmer_tile_kernel(const char *seq, const i
 }
 
 // by_pos[id][p0 + row] += the sum of a tile's slabs (8 XCDs x classes); one
-// thread per (tile, row, id), consecutive threads consecutive ids (the slab
-// reads coalesce)
+// thread per (tile, id, row), consecutive threads consecutive positions (the
+// slab reads and the by_pos adds coalesce)
 __global__ void __launch_bounds__(256) kmer_reduce_kernel(const uint32_t *slab, int npos, const int *maxlen, int grid,
                                                           unsigned long long *out) {
-  const int last_start = min(npos, *maxlen - (kK - 1));
+  const int last_start = min(npos, (maxlen ? *maxlen : npos + kK - 1) - (kK - 1));
   const int T = last_start > 0 ? (last_start + kP - 1) / kP : 0;
-  const int64_t f = (int64_t)blockIdx.x * 256 + threadIdx.x;   // tile * kP * kNum + row * kNum + id
+  const int64_t f = (int64_t)blockIdx.x * 256 + threadIdx.x;   // tile * kP * kNum + id * kP + row
   const int tile = (int)(f / (kP * kNum)), cell = (int)(f % (kP * kNum));
   const int classes = T ? (grid >> 3) / T : 0;
   if (tile >= T) return;
-  const int p = tile * kP + cell / kNum;
+  const int p = tile * kP + cell % kP;
   if (p >= npos) return;
   uint32_t sum = 0;
   for (int cls = 0; cls < classes; ++cls)
 #pragma unroll
     for (int x = 0; x < 8; ++x) sum += slab[((size_t)(8 * (cls * T + tile) + x)) * (kP * kNum) + cell];
-  if (sum) out[(size_t)(cell % kNum) * npos + p] += sum;
+  if (sum) out[(size_t)(cell / kP) * npos + p] += sum;
 }
 
 }  // namespace kmers
@@ -299,15 +354,21 @@ int hpgq_kmers_count_device(hpgq_kmers_t *k, const hpgq_batch_t *b, const uint8_
     const int64_t n = std::min(kPart, b->num_reads - lo);
     const int32_t *ix = b->data_indices + lo;
     const uint8_t *mk = mask ? mask + lo : nullptr;
-    HPGQ_HIP_TRY(hipMemsetAsync(k->d_maxlen, 0, sizeof(int), k->stream));
-    hipLaunchKernelGGL(kmer_maxlen_kernel, dim3((unsigned)std::min<int64_t>((n + 1023) / 1024, 8 * k->cus)),
-                       dim3(1024), 0, k->stream, ix, n, mk, k->d_maxlen);
-    HPGQ_HIP_TRY(hipGetLastError());
+    // few tiles (lmax <= 260): every tile is work for reads near lmax, and
+    // the prepass (~30 us per 10 M reads) would cost more than it saves
+    const int *ml = nullptr;
+    if (tmax > kSpill) {
+      HPGQ_HIP_TRY(hipMemsetAsync(k->d_maxlen, 0, sizeof(int), k->stream));
+      hipLaunchKernelGGL(kmer_maxlen_kernel, dim3((unsigned)std::min<int64_t>((n + 4095) / 4096, 8 * k->cus)),
+                         dim3(1024), 0, k->stream, ix, n, mk, k->d_maxlen);
+      HPGQ_HIP_TRY(hipGetLastError());
+      ml = k->d_maxlen;
+    }
     hipLaunchKernelGGL(kmer_tile_kernel, dim3((unsigned)k->grid), dim3(kWG), 0, k->stream, b->seq, ix, n, mk,
-                       k->npos, (const int *)k->d_maxlen, k->d_slab);
+                       k->npos, ml, k->d_slab);
     HPGQ_HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(kmer_reduce_kernel, dim3((unsigned)(((int64_t)tmax * kP * kNum + 255) / 256)), dim3(256), 0,
-                       k->stream, (const uint32_t *)k->d_slab, k->npos, (const int *)k->d_maxlen, k->grid, k->d_out);
+                       k->stream, (const uint32_t *)k->d_slab, k->npos, ml, k->grid, k->d_out);
     HPGQ_HIP_TRY(hipGetLastError());
   }
   return HPGQ_OK;
