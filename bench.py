@@ -494,7 +494,7 @@ def main():
                            d_mask.data_ptr() + int(offs[i]), None)
         eng.sync()
         km = H.Kmers(L, device=local, stream=eng.stream)
-        kernel_name = "hpgq::kmers::kmer_tile_kernel (+kmer_maxlen_kernel)"
+        kernel_name = "hpgq::kmers::kmer_tile_kernel (+kmer_reduce_kernel; +kmer_maxlen_kernel above 8 tiles)"
         # seq + offsets + the mask (quality is not read)
         alg = [(nb - 4 * (n + 1)) // 2 + 4 * (n + 1) + n for (n, _m, nb) in batches]
     elif cgr:

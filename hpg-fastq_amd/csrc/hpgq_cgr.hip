@@ -672,6 +672,8 @@ struct hpgq_cgr {
   // until then, as for any asynchronous fill).
   int path = HPGQ_CGR_PATH_AUTO;
   int32_t *d_span_first = nullptr;
+  unsigned long long *d_toggles = nullptr;   // ONLY_VALID_READS: validity toggle bits per read
+  int64_t toggles_cap = 0;                   // words
   unsigned long long *d_scratch = nullptr;
   uint32_t *d_slots = nullptr;            // [kSlots][2]: gate, done
   struct Fill {
@@ -809,6 +811,7 @@ void hpgq_cgr_close(hpgq_cgr_t *c) {
   (void)hipFree(c->d_flags);
   (void)hipFree(c->d_sum);
   (void)hipFree(c->d_span_first);
+  (void)hipFree(c->d_toggles);
   (void)hipFree(c->d_scratch);
   (void)hipFree(c->d_slots);
   (void)hipFree(c->d_pack);
@@ -835,12 +838,23 @@ int hpgq_cgr_fill_device(hpgq_cgr_t *c, const hpgq_batch_t *b, const uint8_t *st
     int rc = hpgq_cgr_sync(c);
     if (rc) return rc;
   }
+  const int64_t words = b->num_reads / 64 + 1;   // span_first_kernel's toggle words
+  if (valid && words > c->toggles_cap) {
+    HPGQ_HIP_TRY(hipStreamSynchronize(c->stream));   // (fills in flight may still read the old words)
+    (void)hipFree(c->d_toggles);
+    c->d_toggles = nullptr;
+    c->toggles_cap = 0;
+    const int64_t cap = words + words / 4 + 64;
+    if (hipMalloc(&c->d_toggles, cap * 8) != hipSuccess) return HPGQ_E_NOMEM;
+    c->toggles_cap = cap;
+  }
   const int slot = (int)c->pending.size();
   S::SArgs SA;
   SA.seq = b->seq;
   SA.qual = b->quality;
   SA.idx = b->data_indices;
   SA.status = valid ? status : nullptr;
+  SA.toggles = valid ? c->d_toggles : nullptr;
   SA.num_reads = b->num_reads;
   SA.base_quality = c->base_quality;
   SA.span_first = c->d_span_first;

@@ -100,6 +100,8 @@ struct SArgs {   // (read indices fit 31 bits: the host sends larger batches to 
   const char *seq, *qual;
   const int32_t *idx;
   const uint8_t *status;            // VALID: read_status[] (1 = VALID_READ)
+  unsigned long long *toggles;      // VALID: bit r: read r's validity differs from read r-1's
+                                    // (valid before read 0); written by span_first_kernel
   int64_t num_reads;
   uint32_t base_quality;
   int32_t *span_first;              // [kMaxSpans] first read with idx[r] >= span start - 32
@@ -117,7 +119,10 @@ __device__ __forceinline__ int64_t nspans(int32_t a0, int32_t b1) {
 
 // span_first[s] = the first read r with idx[r] >= a0 + s*kSpan - 32: thread r
 // writes the spans whose (start - 32) lies in (idx[r-1], idx[r]]; thread 0
-// also clears this fill's gate and done slots
+// also clears this fill's gate and done slots.  VALID: each wave also stores
+// the validity toggles of its 64 reads as one word (ballot), words 0 ..
+// num_reads / 64 (the stream kernel reads them through a range-checked
+// descriptor: past them, 0).
 // (grid-stride: a few thousand workgroups walk the whole idx array; one
 // thread per read made the launch dispatch-bound at ~17 us per 5 M reads)
 __global__ void __launch_bounds__(256) span_first_kernel(SArgs A) {
@@ -125,16 +130,25 @@ __global__ void __launch_bounds__(256) span_first_kernel(SArgs A) {
   const int32_t a0 = b0 & ~15;
   const int64_t ns = nspans(a0, b1);
   const int64_t stride = (int64_t)gridDim.x * 256;
-  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r <= A.num_reads; r += stride) {
-    if (r == 0) {
-      *A.gate = 0u;
-      *A.done = 0u;
+  const int lane = threadIdx.x & 63;
+  for (int64_t r0 = (int64_t)blockIdx.x * 256 + (threadIdx.x & ~63); r0 <= A.num_reads; r0 += stride) {
+    const int64_t r = r0 + lane;
+    if (r <= A.num_reads) {
+      if (r == 0) {
+        *A.gate = 0u;
+        *A.done = 0u;
+      }
+      const int64_t hi = (int64_t)A.idx[r] + 32 - a0;   // s*kSpan <= hi
+      const int64_t lo = r == 0 ? -1 : (int64_t)A.idx[r - 1] + 32 - a0;   // s*kSpan > lo
+      const int64_t s0 = lo < 0 ? 0 : (lo >> kSpanLog) + 1;
+      const int64_t s1 = r == A.num_reads ? ns - 1 : (hi >> kSpanLog);   // past the last start: the end sentinel
+      for (int64_t s = s0; s <= s1 && s < ns; ++s) A.span_first[s] = (int32_t)r;
     }
-    const int64_t hi = (int64_t)A.idx[r] + 32 - a0;   // s*kSpan <= hi
-    const int64_t lo = r == 0 ? -1 : (int64_t)A.idx[r - 1] + 32 - a0;   // s*kSpan > lo
-    const int64_t s0 = lo < 0 ? 0 : (lo >> kSpanLog) + 1;
-    const int64_t s1 = r == A.num_reads ? ns - 1 : (hi >> kSpanLog);   // past the last start: the end sentinel
-    for (int64_t s = s0; s <= s1 && s < ns; ++s) A.span_first[s] = (int32_t)r;
+    if (A.status) {
+      const bool t = r < A.num_reads && (A.status[r] == 1) != (r == 0 || A.status[r - 1] == 1);
+      const unsigned long long m = __ballot(t);
+      if (lane == 0) A.toggles[r0 >> 6] = m;
+    }
   }
 }
 
@@ -335,16 +349,15 @@ struct AxisTag {
 // the idx window a wave walks: lane j holds idx[r + j] (0x7FFFFFFF past the
 // end); the load is unconditional (clamped index) so that no branch splits the
 // compiler's view of the loads in flight.  VALID: tg = 1 when read r + j's
-// validity differs from read r + j - 1's (the state before read 0 is valid).
+// validity differs from read r + j - 1's (the state before read 0 is valid):
+// bit r + j of span_first_kernel's toggle words, one dword load per lane
+// (rt: their descriptor; past the words, 0)
 template <bool VALID>
-__device__ __forceinline__ int32_t idx_window(const SArgs &A, int32_t r, int lane, uint32_t &tg) {
+__device__ __forceinline__ int32_t idx_window(const SArgs &A, __amdgpu_buffer_rsrc_t rt, int32_t r, int lane,
+                                              uint32_t &tg) {
   const int32_t j = r + lane, n = (int32_t)A.num_reads;
   const int32_t v = A.idx[j <= n ? j : n];
-  if (VALID) {
-    const int32_t ja = j < n ? j : n - 1, jb = j >= 1 && j <= n ? j - 1 : 0;
-    const bool va = A.status[ja] == 1, vb = j == 0 || A.status[jb] == 1;
-    tg = j < n && va != vb ? 1u : 0u;
-  }
+  if (VALID) tg = __builtin_amdgcn_ubfe(__builtin_amdgcn_raw_buffer_load_b32(rt, ((uint32_t)j >> 5) * 4u, 0, 0), j & 31, 1);
   return j <= n ? v : 0x7FFFFFFF;
 }
 
@@ -355,9 +368,9 @@ __device__ __forceinline__ int32_t idx_window(const SArgs &A, int32_t r, int lan
 // in flight.  hop: the tile is its span's last, so the cursor moves on to rn
 // (the next span's first read) instead.
 template <bool VALID, bool TOG>
-__device__ __forceinline__ void scatter_starts(const SArgs &A, uint32_t *sc, uint32_t *tc, int32_t &r, int32_t &iw,
-                                               uint32_t &itg, int32_t base, int32_t limit, int lane, bool hop = false,
-                                               int32_t rn = 0) {
+__device__ __forceinline__ void scatter_starts(const SArgs &A, __amdgpu_buffer_rsrc_t rt, uint32_t *sc, uint32_t *tc,
+                                               int32_t &r, int32_t &iw, uint32_t &itg, int32_t base, int32_t limit,
+                                               int lane, bool hop = false, int32_t rn = 0) {
   auto put = [&](int32_t x, uint32_t tg) {
     const bool in = x < limit;
     const uint32_t o = (uint32_t)(x - base);
@@ -373,12 +386,12 @@ __device__ __forceinline__ void scatter_starts(const SArgs &A, uint32_t *sc, uin
     int c;
     do {
       uint32_t tg = 0;
-      const int32_t x = idx_window<VALID>(A, r, lane, tg);
+      const int32_t x = idx_window<VALID>(A, rt, r, lane, tg);
       c = put(x, tg);
     } while (c == 64);
   }
   if (hop) r = rn;
-  iw = idx_window<VALID>(A, r, lane, itg);
+  iw = idx_window<VALID>(A, rt, r, lane, itg);
 }
 
 // a lane's bytes at o (o >= 0) from a buffer descriptor; bytes past the end read 0
@@ -471,6 +484,9 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
   const uint32_t kPast = nrec;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)A.seq, (short)0, nrec, 0x00020000);
   const __amdgpu_buffer_rsrc_t rq = __builtin_amdgcn_make_buffer_rsrc((void *)A.qual, (short)0, nrec, 0x00020000);
+  // VALID: span_first_kernel's toggle words 0 .. num_reads / 64
+  const __amdgpu_buffer_rsrc_t rt = __builtin_amdgcn_make_buffer_rsrc(
+      (void *)A.toggles, (short)0, VALID ? (uint32_t)((A.num_reads / 64 + 1) * 8) : 0u, 0x00020000);
   // span cursors through the scalar cache (read-only here)
   const __attribute__((address_space(4))) int32_t *sfirst =
       (const __attribute__((address_space(4))) int32_t *)A.span_first;
@@ -537,7 +553,7 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
       }
     };
     auto ctx_starts = [&](int32_t &r, int32_t &iw, uint32_t &itg, const int32_t t0) {
-      scatter_starts<VALID, false>(A, scx, nullptr, r, iw, itg, t0 - kLaneBytes, t0, lane);
+      scatter_starts<VALID, false>(A, rt, scx, nullptr, r, iw, itg, t0 - kLaneBytes, t0, lane);
       __builtin_amdgcn_wave_barrier();
       const uint32_t ps = __builtin_amdgcn_readfirstlane(scx[0]);
       __builtin_amdgcn_wave_barrier();
@@ -677,7 +693,7 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
     int32_t r = sfirst[s];
     int32_t rn = sfirst[min(s + nwav, ns - 1)];
     uint32_t itg = 0;
-    int32_t iw = idx_window<VALID>(A, r, lane, itg);
+    int32_t iw = idx_window<VALID>(A, rt, r, lane, itg);
     uint32_t skA = 0, skB = 0;   // VALID: skip state at the tile starts
     {
       uint32_t cs[4] = {0x4E4E4E4Eu, 0x4E4E4E4Eu, 0x4E4E4E4Eu, 0x4E4E4E4Eu}, cq[2] = {0u, 0u};
@@ -692,7 +708,7 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
     }
     uint32_t sA[kNdw], qA[kNdw], sB[kNdw], qB[kNdw], soA, soB, tgA = 0, tgB = 0;
     int32_t rfA = r, rfB = 0;   // VALID: the first read starting in the tile
-    scatter_starts<VALID, VALID>(A, sc, tcb, r, iw, itg, tA, tA + kTile, lane, tA + kTile >= eA, rn);
+    scatter_starts<VALID, VALID>(A, rt, sc, tcb, r, iw, itg, tA, tA + kTile, lane, tA + kTile >= eA, rn);
     soA = take_bits(&sc[lane]);
     if (VALID) tgA = take_bits(&tcb[lane]);
     load32(rs, (uint32_t)(tA + kLaneBytes * lane), sA);
@@ -728,7 +744,7 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
       load32(rq, oy, qy);
       const uint32_t par = tile(tx, ex, sx, qx, sox, skx, tgx, rfx, [&] {
         rfy = r;
-        scatter_starts<VALID, VALID>(A, scpy, tcpy, r, iw, itg, ty, fin ? INT32_MIN : ty + kTile, lane,
+        scatter_starts<VALID, VALID>(A, rt, scpy, tcpy, r, iw, itg, ty, fin ? INT32_MIN : ty + kTile, lane,
                                      ty + kTile >= ey, rn);
         soy = take_bits(&scpy[lane]);
         if (VALID) tgy = take_bits(&tcpy[lane]);

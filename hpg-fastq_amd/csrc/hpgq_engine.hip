@@ -64,7 +64,9 @@ struct hpgq_ctx {
   bool adaptive = false;
   int mode = 0;              // chain of the next call
   int wide_calls = 0;        // calls since the last probe in wide-first mode
-  uint32_t *h_report = nullptr, *d_report = nullptr;   // mapped host words (deferred, reads)
+  uint32_t *h_report = nullptr, *d_report = nullptr;   // mapped host words (deferred, reads, seq)
+  uint32_t seq = 0;          // sequence number of the last call's report
+  uint32_t min_seq = 0;      // reports older than this (before a probe) are ignored
   int parity = 0;
   uint64_t *d_bits1 = nullptr, *d_bits2 = nullptr;   // deferred reads per s1 unit
   size_t bits_cap = 0;
@@ -312,7 +314,7 @@ static int plan(hpgq_ctx *c, int cus) {
   void *h = nullptr;
   HPGQ_HIP_TRY(hipHostMalloc(&h, 64, hipHostMallocMapped));
   c->h_report = static_cast<uint32_t *>(h);
-  c->h_report[0] = c->h_report[1] = 0;
+  c->h_report[0] = c->h_report[1] = c->h_report[2] = 0;
   void *d = nullptr;
   HPGQ_HIP_TRY(hipHostGetDevicePointer(&d, h, 0));
   c->d_report = static_cast<uint32_t *>(d);
@@ -326,7 +328,8 @@ static int pick_chain(hpgq_ctx *c) {
   if (!c->adaptive) return 0;
   volatile uint32_t *r = c->h_report;
   const uint32_t deferred = r[0], reads = r[1];
-  const bool known = reads != 0;
+  // (a report from before the last probe may still land after it: ignored)
+  const bool known = reads != 0 && (int32_t)(r[2] - c->min_seq) >= 0;
   const bool mostly_long = known && (uint64_t)deferred * 2 >= reads;
   if (c->mode == 0) {
     if (mostly_long) {
@@ -337,7 +340,7 @@ static int pick_chain(hpgq_ctx *c) {
     c->mode = 0;
   } else if (++c->wide_calls >= kProbeEvery) {
     c->wide_calls = 0;
-    r[0] = r[1] = 0;   // the probe's own report decides
+    c->min_seq = c->seq + 1;   // the probe's own report decides
     return 0;
   }
   return c->mode;
@@ -530,7 +533,7 @@ static int launch(hpgq_ctx *c, hpgq::EngineArgs &A) {
   const Chain &ch = c->ch[k];
   if (!ch.has3) {   // the catch-all alone
     A.unit_bits = A.unit_and = nullptr;
-    A.pending = A.pending_clear = nullptr;
+    A.pending = A.pending_clear = A.pending_clear2 = nullptr;
     A.defer_bits = nullptr;
     A.defer_count = nullptr;
     A.defer_len = INT_MAX;
@@ -544,7 +547,7 @@ static int launch(hpgq_ctx *c, hpgq::EngineArgs &A) {
   // stage 1: every read; deferrals -> bits1, count -> PEND1[s]
   hpgq::EngineArgs A1 = A;
   A1.unit_bits = A1.unit_and = nullptr;
-  A1.pending = A1.pending_clear = nullptr;
+  A1.pending = A1.pending_clear = A1.pending_clear2 = nullptr;
   A1.defer_bits = c->d_bits1;
   A1.defer_count = f + FL_PEND1 + s;
   A1.defer_len = ch.s1.defer_len;
@@ -563,10 +566,12 @@ static int launch(hpgq_ctx *c, hpgq::EngineArgs &A) {
     A2.unit_reads = ch.s1.block;
     A2.pending = last_count;
     A2.pending_clear = last_clear;
+    A2.pending_clear2 = nullptr;
     A2.defer_bits = c->d_bits2;
     A2.defer_count = f + FL_PEND2 + s;
     A2.defer_len = ch.s2.defer_len;
     A2.report = c->d_report;   // how many reads hex deferred: the next call's choice
+    A2.report_seq = ++c->seq;
     rc = launch_stage(c, ch.s2, A2);
     if (rc) return rc;
     and_bits = c->d_bits1;   // bits2 words are only written for units with bits1 set
@@ -581,6 +586,10 @@ static int launch(hpgq_ctx *c, hpgq::EngineArgs &A) {
   A3.unit_reads = ch.s1.block;
   A3.pending = last_count;
   A3.pending_clear = last_clear;
+  // a chain without stage 2 (wide first) leaves PEND2 alone: clear the next
+  // call's, or a stale count from an earlier hex-first call of that parity
+  // makes its catch-all walk every unit
+  A3.pending_clear2 = ch.has2 ? nullptr : f + FL_PEND2 + o;
   A3.defer_bits = nullptr;
   A3.defer_count = nullptr;
   A3.defer_len = INT_MAX;

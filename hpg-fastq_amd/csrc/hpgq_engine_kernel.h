@@ -85,14 +85,16 @@ struct EngineArgs {
   int unit_reads;
   const uint32_t *pending;    // follow-up: reads deferred to this stage (0: exit at once)
   uint32_t *pending_clear;    // follow-up: the same counter of the next call, zeroed here
+  uint32_t *pending_clear2;   // (a chain without stage 2: the next call's stage-2 counter too)
   // deferral out (segmented kernels): reads longer than defer_len go to the next
   // stage: bits per unit (every unit this kernel visits stores its word) + count
   uint64_t *defer_bits;
   uint32_t *defer_count;
   int defer_len;
-  // follow-up: host-mapped words [deferred reads, batch reads] for the host's
-  // choice of the next call's first stage (may be null)
+  // follow-up: host-mapped words [deferred reads, batch reads, call sequence
+  // number] for the host's choice of the next call's first stage (may be null)
   uint32_t *report;
+  uint32_t report_seq;
 };
 
 // ---------------------------------------------------------------------------
@@ -271,9 +273,11 @@ __device__ __forceinline__ int unit_read(const Unit &U, int base, uint32_t *scra
 __device__ __forceinline__ bool follow_up_idle(const EngineArgs &A) {
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     if (A.pending_clear) *A.pending_clear = 0u;
-    if (A.report) {   // (a plain store over PCIe into pinned host memory)
+    if (A.pending_clear2) *A.pending_clear2 = 0u;
+    if (A.report) {   // (plain stores over PCIe into pinned host memory)
       A.report[0] = *A.pending;
       A.report[1] = (uint32_t)A.num_reads;
+      A.report[2] = A.report_seq;
     }
   }
   return A.unit_bits != nullptr && uni((int)*A.pending) == 0;

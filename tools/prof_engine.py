@@ -22,6 +22,7 @@ ap.add_argument("--mode", default="c2")
 ap.add_argument("--L", type=int, default=150)
 ap.add_argument("--k", type=int, default=7)
 ap.add_argument("--kmers", action="store_true", help="also count 5-mers (stats --kmers) after the engine")
+ap.add_argument("--invalid-pct", type=float, default=None, help="cgrv: this share of skipped reads instead of bench.py's 5 %%")
 args = ap.parse_args()
 
 dev = torch.device("cuda", 0)
@@ -44,7 +45,10 @@ if args.mode in ("cgr", "cgrv"):
     if args.mode == "cgrv":   # ONLY_VALID_READS with bench.py's 5 % invalid status
         sys.path.insert(0, ROOT)
         from bench import read_status
-        st = torch.from_numpy(read_status(n, 5)).to(dev)
+        st = read_status(n, 5)
+        if args.invalid_pct is not None:   # probes: another share of skipped reads (0: none)
+            st = (np.random.default_rng(5).random(n) >= args.invalid_pct / 100).astype(np.uint8)
+        st = torch.from_numpy(st).to(dev)
         torch.cuda.synchronize()
     for _ in range(args.iters):
         if st is not None:
