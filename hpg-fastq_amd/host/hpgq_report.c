@@ -245,8 +245,12 @@ int cli_report(const cli_options_t *o, const hpgq_params_t *p, const uint64_t *c
     fclose(f);
   }
   if ((f = open_out(o, base, "read.quality.histogram.data"))) {
-    /* keys are signed (bin = key & 255, Q13); min..max key as :368-385 */
-    int lo = 1000, hi = -1000;
+    /* keys are signed (bin = key & 255, Q13); rows min_qual..max_qual as
+       src/stats_report.c:410-425, whose max_qual starts at 0: with every key
+       negative the rows still run up to key 0 (the reference then reads its
+       array at negative indices; here those rows print the negative keys'
+       own bins) */
+    int lo = 1000, hi = 0;
     for (int i = 0; i < HPGQ_MEANQ_BINS; i++)
       if (hq[i]) {
         const int key = i >= 128 ? i - 256 : i;

@@ -147,10 +147,12 @@ def report_files(ctr, lmax, phred, base, opts):
         "%i\t%i\n" % (i, _i32(hl[i])) for i in range(1, max_len + 1)).encode()
 
     # ---- report_quality (:355-390): keys are signed (bin = key & 255) ----
+    # rows min_qual..max_qual with max_qual starting at 0 (:410): all-negative
+    # keys still run up to key 0
     keys = [(b - 256 if b >= 128 else b) for b in range(pyref.MEANQ_BINS) if hq[b]]
     lines = []
     if keys:
-        for key in range(min(keys), max(keys) + 1):
+        for key in range(min(keys), max(max(keys), 0) + 1):
             lines.append("%i\t%i\n" % (key - phred, _i32(hq[key & 255])))
     out["read.quality.histogram.data"] = "".join(lines).encode()
 

@@ -109,3 +109,20 @@ def test_report_writer_golden(san, tmp_path, case):
     want = os.path.join(GOLD, "report", case)
     for name in sorted(os.listdir(want)):
         assert (out / name).read_bytes() == open(os.path.join(want, name), "rb").read(), name
+
+
+def test_report_quality_rows_run_to_key_zero(san, tmp_path):
+    """src/stats_report.c:410 starts max_qual at 0, so when every
+    mean-quality key is negative (raw quality bytes >= 128, signed char:
+    quirk Q13) the read.quality.histogram rows still run up to key 0 (keys
+    -16 .. 0 here). The C writer and the restatement agree, and the rows
+    follow that rule."""
+    reads = O.synth(3000, seed=4, L=150, trunc_pct=0)
+    reads.qual[:] = 0xF0 + (np.arange(reads.qual.size) % 2)   # bytes 0xF0/0xF1: -16/-15 as char
+    _, _, ctr = O.run(H.stats_params(lmax=150), reads)
+    out = _report(san, tmp_path, ctr, 150, [])
+    exp = report_ref.report_files(ctr, 150, 33, "in.fq", {"filter_on": False})
+    got = (out / "in.fq.read.quality.histogram.data").read_bytes()
+    assert got == exp["read.quality.histogram.data"]
+    keys = [int(line.split(b"\t")[0]) + 33 for line in got.splitlines()]
+    assert keys[0] < 0 and keys[-1] == 0 and keys == list(range(keys[0], 1)), keys

@@ -27,3 +27,6 @@ for mode in cgr cgrv; do
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH -d $P/lds1_$mode -o run --output-format csv -- $A > $P/lds1_$mode.log 2>&1 &&
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS -d $P/lds2_$mode -o run --output-format csv -- $A > $P/lds2_$mode.log 2>&1 || exit 8
 done
+A="python tools/prof_engine.py --mode c2 --kmers --iters 3"
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_VALU -d $P/lds2_kmers -o run --output-format csv -- $A > $P/lds2_kmers.log 2>&1 &&
+timeout -k 10 300 rocprofv3 --kernel-trace --pmc TA_TA_BUSY_sum GRBM_GUI_ACTIVE -d $P/ta_kmers -o run --output-format csv -- $A > $P/ta_kmers.log 2>&1 || exit 9

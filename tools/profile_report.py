@@ -114,6 +114,15 @@ def main():
                 rec["sq"] = {**l1, **l2}
                 if l2.get("SQ_LDS_IDX_ACTIVE"):
                     rec["lds_conflict_ratio"] = round(l2["SQ_LDS_BANK_CONFLICT"] / l2["SQ_LDS_IDX_ACTIVE"], 4)
+        if cfg == "c2_kmers":   # LDS banks and the texture addresser
+            l2, _ = counters("lds2_kmers", "kmer_tile_kernel")
+            ta, _ = counters("ta_kmers", "kmer_tile_kernel")
+            if l2 or ta:
+                rec["sq"] = {**l2, **ta}
+                if l2.get("SQ_LDS_IDX_ACTIVE"):
+                    rec["lds_conflict_ratio"] = round(l2["SQ_LDS_BANK_CONFLICT"] / l2["SQ_LDS_IDX_ACTIVE"], 4)
+                if ta.get("GRBM_GUI_ACTIVE"):   # GRBM sums 8 XCDs, TA_TA_BUSY_sum 256 CUs
+                    rec["ta_busy_frac"] = round(ta["TA_TA_BUSY_sum"] / 256 / (ta["GRBM_GUI_ACTIVE"] / 8), 4)
         cb = bench_line(os.path.join(PROF, f"bench_{cfg}.json"))
         if cb:
             json.dump(cb, open(os.path.join(OUT, f"{a.round}_bench_{cfg}.json"), "w"), indent=1)
