@@ -88,6 +88,11 @@ struct hpgq_ctx {
     size_t mask_off = 0, trim_off = 0, nreads = 0, ntrim = 0;   // ntrim: reads x mates
   } slot[2];
   int cur_slot = 0;
+  // hpgq_host_batch: the slot reserved for a batch the caller writes in place
+  // (-1: none), and its size; hpgq_run_host on exactly that batch DMAs it
+  int staged = -1;
+  int64_t staged_n = 0;
+  size_t staged_bytes[2] = {0, 0};
   int32_t *h_err = nullptr;   // pinned: the error flag, copied back by hpgq_sync
   ncclComm_t comm = nullptr;
 };
@@ -662,6 +667,51 @@ static int stage_copy(hpgq_ctx *c, hpgq_ctx::Slot &sl, size_t off, const void *s
   return HPGQ_OK;
 }
 
+// a host batch's layout in a staging slot: per mate [seq | quality |
+// data_indices] (seq and quality padded by HPGQ_DEVICE_SLACK), then the mask and
+// the trims; returns the slot bytes
+static size_t host_layout(int nm, int64_t n, const size_t (&bytes)[2], size_t (&off)[2][3], size_t &mask_off,
+                          size_t &trim_off) {
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  size_t total = 0;
+  for (int m = 0; m < nm; ++m) {
+    off[m][0] = total; total += al(bytes[m] + HPGQ_DEVICE_SLACK);   // seq
+    off[m][1] = total; total += al(bytes[m] + HPGQ_DEVICE_SLACK);   // quality
+    off[m][2] = total; total += al((size_t)(n + 1) * 4);            // data_indices
+  }
+  mask_off = total;
+  total += al((size_t)n);
+  trim_off = total;
+  total += al((size_t)n * nm * 4);
+  return total;
+}
+
+int hpgq_host_batch(hpgq_ctx_t *c, int64_t num_reads, size_t nbytes, size_t nbytes2, hpgq_batch_t *b,
+                    hpgq_batch_t *b2) {
+  if (!c || !b || num_reads < 1 || nbytes > (size_t)INT32_MAX || nbytes2 > (size_t)INT32_MAX) return HPGQ_E_INVALID;
+  if ((c->nm == 2) != (b2 != nullptr)) return HPGQ_E_INVALID;
+  HPGQ_HIP_TRY(hipSetDevice(c->device));
+  const size_t bytes[2] = {nbytes, c->nm == 2 ? nbytes2 : 0};
+  size_t off[2][3], mask_off, trim_off;
+  const size_t total = host_layout(c->nm, num_reads, bytes, off, mask_off, trim_off);
+  c->staged = -1;
+  hpgq_ctx::Slot *sp = nullptr;
+  const int rc = slot_acquire(c, total, sp);
+  if (rc) return rc;
+  hpgq_batch_t *bs[2] = {b, b2};
+  for (int m = 0; m < c->nm; ++m) {
+    bs[m]->num_reads = num_reads;
+    bs[m]->seq = sp->h + off[m][0];
+    bs[m]->quality = sp->h + off[m][1];
+    bs[m]->data_indices = reinterpret_cast<int32_t *>(sp->h + off[m][2]);
+  }
+  c->staged = c->cur_slot;
+  c->staged_n = num_reads;
+  c->staged_bytes[0] = bytes[0];
+  c->staged_bytes[1] = bytes[1];
+  return HPGQ_OK;
+}
+
 int hpgq_run_host(hpgq_ctx_t *c, const hpgq_batch_t *b, const hpgq_batch_t *b2,
                   uint8_t *mask_out, uint32_t *trim_out) {
   if (!c || !b) return HPGQ_E_INVALID;
@@ -672,32 +722,51 @@ int hpgq_run_host(hpgq_ctx_t *c, const hpgq_batch_t *b, const hpgq_batch_t *b2,
   if (n == 0) return HPGQ_OK;
   HPGQ_HIP_TRY(hipSetDevice(c->device));
   const hpgq_batch_t *bs[2] = {b, b2};
-  size_t bytes[2] = {0, 0}, off[2][3];
-  size_t total = 0;
-  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  size_t bytes[2] = {0, 0}, off[2][3], mask_off, trim_off;
   for (int m = 0; m < c->nm; ++m) {
     const int32_t *ix = bs[m]->data_indices;
     bytes[m] = (size_t)(ix[n] - ix[0]);
-    off[m][0] = total; total += al(bytes[m] + HPGQ_DEVICE_SLACK);   // seq
-    off[m][1] = total; total += al(bytes[m] + HPGQ_DEVICE_SLACK);   // quality
-    off[m][2] = total; total += al((size_t)(n + 1) * 4);            // data_indices
   }
-  const size_t mask_off = total;
-  total += al((size_t)n);
-  const size_t trim_off = total;
-  total += al((size_t)n * c->nm * 4);
+  const size_t total = host_layout(c->nm, n, bytes, off, mask_off, trim_off);
+  // a batch written in place by hpgq_host_batch: the same slot and layout
+  // (sized by the staged byte counts), no host copy
+  bool in_place = false;
+  if (c->staged >= 0) {
+    const hpgq_ctx::Slot &st = c->slot[c->staged];
+    size_t so[2][3], smask, strim;
+    (void)host_layout(c->nm, c->staged_n, c->staged_bytes, so, smask, strim);
+    in_place = c->staged == c->cur_slot && n == c->staged_n;
+    for (int m = 0; m < c->nm && in_place; ++m) {
+      const int32_t *ix = bs[m]->data_indices;
+      in_place = bs[m]->seq == st.h + so[m][0] && bs[m]->quality == st.h + so[m][1] &&
+                 ix == reinterpret_cast<const int32_t *>(st.h + so[m][2]) && ix[0] == 0 &&
+                 bytes[m] <= c->staged_bytes[m];
+    }
+    if (in_place) {
+      std::memcpy(off, so, sizeof(off));
+      mask_off = smask;
+      trim_off = strim;
+    }
+    c->staged = -1;
+  }
   hpgq_ctx::Slot *sp = nullptr;
-  int rc = slot_acquire(c, total, sp);
-  if (rc) return rc;
+  int rc = HPGQ_OK;
+  if (in_place) sp = &c->slot[c->cur_slot];
+  else if ((rc = slot_acquire(c, total, sp))) return rc;
   hpgq_ctx::Slot &sl = *sp;
   hpgq::EngineArgs A{};
   fill_args(c, A);
   A.num_reads = n;
+  if (in_place)   // the caller wrote the slot: ONE DMA of its inputs (each HIP call costs host time)
+    HPGQ_HIP_TRY(hipMemcpyAsync(sl.d, sl.h, off[c->nm - 1][2] + (size_t)(n + 1) * 4, hipMemcpyHostToDevice,
+                                c->cstream));
   for (int m = 0; m < c->nm; ++m) {
     const int32_t *ix = bs[m]->data_indices;
-    if ((rc = stage_copy(c, sl, off[m][2], ix, (size_t)(n + 1) * 4))) return rc;
-    if ((rc = stage_copy(c, sl, off[m][0], bs[m]->seq + ix[0], bytes[m]))) return rc;
-    if ((rc = stage_copy(c, sl, off[m][1], bs[m]->quality + ix[0], bytes[m]))) return rc;
+    if (!in_place) {
+      if ((rc = stage_copy(c, sl, off[m][2], ix, (size_t)(n + 1) * 4))) return rc;
+      if ((rc = stage_copy(c, sl, off[m][0], bs[m]->seq + ix[0], bytes[m]))) return rc;
+      if ((rc = stage_copy(c, sl, off[m][1], bs[m]->quality + ix[0], bytes[m]))) return rc;
+    }
     // absolute indices: shift the base pointers so data_indices need no rewrite
     A.seq[m] = sl.d + off[m][0] - ix[0];
     A.qual[m] = sl.d + off[m][1] - ix[0];

@@ -97,6 +97,8 @@ _SIGS = [
                                   C.c_void_p, C.c_void_p]),
     ("hpgq_run_host", C.c_int, [C.c_void_p, C.POINTER(Batch), C.POINTER(Batch),
                                 C.c_void_p, C.c_void_p]),
+    ("hpgq_host_batch", C.c_int, [C.c_void_p, C.c_int64, C.c_size_t, C.c_size_t,
+                                  C.POINTER(Batch), C.POINTER(Batch)]),
     ("hpgq_sync", C.c_int, [C.c_void_p]),
     ("hpgq_reset", C.c_int, [C.c_void_p]),
     ("hpgq_counters_size", C.c_size_t, [C.c_void_p]),

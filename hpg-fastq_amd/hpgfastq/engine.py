@@ -78,6 +78,22 @@ class Engine:
         check(lib.hpgq_run_host(self._h, C.byref(batch), C.byref(batch2) if batch2 else None,
                                 _ptr(mask), _ptr(trim)), "hpgq_run_host")
 
+    def run_host_in_place(self, mates, mask=None, trim=None):
+        """hpgq_host_batch + hpgq_run_host: each (seq u8, qual u8, idx i32 from 0)
+        of `mates` is written straight into the ctx's staging slot (no copy in
+        the library); mask/trim are numpy outputs valid after sync()."""
+        bs = [Batch() for _ in mates]
+        nb = [int(ix[-1]) for (_s, _q, ix) in mates]
+        n = len(mates[0][2]) - 1
+        check(lib.hpgq_host_batch(self._h, n, nb[0], nb[1] if len(mates) > 1 else 0, C.byref(bs[0]),
+                                  C.byref(bs[1]) if len(mates) > 1 else None), "hpgq_host_batch")
+        for b, (sq, ql, ix) in zip(bs, mates):
+            C.memmove(b.data_indices, ix.ctypes.data, ix.nbytes)
+            C.memmove(b.seq, sq.ctypes.data, int(ix[-1]))
+            C.memmove(b.quality, ql.ctypes.data, int(ix[-1]))
+        check(lib.hpgq_run_host(self._h, C.byref(bs[0]), C.byref(bs[1]) if len(mates) > 1 else None,
+                                _ptr(mask), _ptr(trim)), "hpgq_run_host")
+
     def run_device(self, batch, batch2=None, mask_ptr=None, trim_ptr=None):
         check(lib.hpgq_run_device(self._h, C.byref(batch), C.byref(batch2) if batch2 else None,
                                   mask_ptr, trim_ptr), "hpgq_run_device")

@@ -218,6 +218,24 @@ int  hpgq_run_device(hpgq_ctx_t *ctx, const hpgq_batch_t *b, const hpgq_batch_t 
 int  hpgq_run_host(hpgq_ctx_t *ctx, const hpgq_batch_t *b, const hpgq_batch_t *b2,
                    uint8_t *mask_out, uint32_t *trim_out);
 
+/*
+ * Host path without the staging copy: reserve the ctx's next page-locked
+ * staging slot for a batch of num_reads reads holding nbytes sequence bytes
+ * (and as many quality bytes; nbytes2 for mate 2 of a paired ctx, else 0 and
+ * b2 NULL).  On return b (b2) point into the slot: the caller writes
+ * data_indices[0..num_reads] (starting at 0, ending at <= nbytes), the
+ * sequence and the quality bytes there -- e.g. while packing its reads -- and
+ * calls hpgq_run_host with exactly that batch, which then only queues the DMA
+ * (no host copy; the reference worker's pack becomes the only one).  The
+ * pointers are valid until that hpgq_run_host, or the next hpgq_host_batch /
+ * hpgq_run_host on the ctx (which abandons the reservation); waiting for the
+ * slot's previous batch, as hpgq_run_host does, may deliver that batch's
+ * outputs.  Replaces the worker's malloc of the SoA batch
+ * (fastq_stats_worker; src/stats_fastq.c:202-250).
+ */
+int  hpgq_host_batch(hpgq_ctx_t *ctx, int64_t num_reads, size_t nbytes, size_t nbytes2,
+                     hpgq_batch_t *b, hpgq_batch_t *b2);
+
 /* Wait for all work on the ctx stream.  HPGQ_E_READ_TOO_LONG when stats are on
  * and a read that passed the filter is longer than lmax (the per-position
  * counters cannot hold it; it is counted in HPGQ_S_LONG_READS).  Without

@@ -1,5 +1,6 @@
 """The drop-in binding as INTEGRATION.md writes it (tools/dropin_bench.c):
-malloc'd SoA batches of the reference's 10,000 reads (src/stats_options.c:22)
+SoA batches of the reference's 10,000 reads (src/stats_options.c:22), packed
+into the ctx's staging slot (hpgq_host_batch) or into malloc'd buffers,
 packed from AoS reads, hpgq_run_host + hpgq_sync per batch, one ctx per worker
 thread (src/stats_options.c:21: 2 threads) -- the summed counters and every
 mask equal the oracle's over the same FASTQ file.  Also the host path's
@@ -31,14 +32,18 @@ def fastq(tmp_path_factory):
     return path
 
 
-@pytest.mark.parametrize("threads,batch", [(2, 10000), (1, 997), (3, 4096)])
-def test_dropin_worker_matches_oracle(fastq, tmp_path, threads, batch):
+@pytest.mark.parametrize("threads,batch,copy", [(2, 10000, False), (1, 997, False), (3, 4096, False),
+                                               (2, 10000, True), (3, 4096, True)])
+def test_dropin_worker_matches_oracle(fastq, tmp_path, threads, batch, copy):
+    """copy=False: the worker packs into the ctx's staging slot (hpgq_host_batch);
+    copy=True: into malloc'd buffers that hpgq_run_host copies."""
     assert os.path.exists(HARNESS), "build with make -C hpg-fastq_amd"
     ctr, msk = str(tmp_path / "ctr.bin"), str(tmp_path / "mask.bin")
     out = subprocess.run([HARNESS, fastq, "--batch", str(batch), "--threads", str(threads), "--c2",
-                          "--counters", ctr, "--mask", msk], check=True, capture_output=True, text=True,
-                         timeout=300)
+                          "--counters", ctr, "--mask", msk, "--repeat", "2"] + (["--copy"] if copy else []),
+                         check=True, capture_output=True, text=True, timeout=300)
     rec = json.loads(out.stdout.strip().splitlines()[-1])
+    assert rec["staging"] == ("copy" if copy else "in_place")
     reads = read_fastq(fastq)
     assert rec["reads"] == reads.n
     p = H.stats_params(lmax=1024, read_quality_range="20,", read_length_range="50,")
@@ -73,6 +78,42 @@ def test_host_path_calls_in_flight(edit):
     want = np.zeros_like(got)
     for b, m, t in zip(batches, masks, trims):
         m_o, t_o, c_o = O.run(p, b)
+        np.testing.assert_array_equal(m, m_o)
+        if edit:
+            np.testing.assert_array_equal(t, t_o)
+        want += c_o
+    np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize("paired,edit", [(False, False), (False, True), (True, False), (True, True)])
+def test_host_batch_in_place(paired, edit):
+    """hpgq_host_batch + hpgq_run_host (the batch written into the staging slot,
+    no host copy), mixed with copied batches on the same ctx and several calls
+    in flight: masks, trims and counters equal the oracle's."""
+    kw = dict(left_length=10, left_quality_range="20,", right_length=30, right_quality_range="20,")
+    p = (H.edit_params(lmax=150, stats=True, **kw) if edit
+         else H.stats_params(lmax=150, read_quality_range="20,", read_length_range="50,"))
+    p.paired = 1 if paired else 0
+    mates = 2 if paired else 1
+    sizes = [20000, 1, 9999, 30000, 4096]
+    bat = [[O.synth(n, seed=70 + i, L=150, trunc_pct=10, n_per_1024=8, first=1000 * i, mate=m)
+            for m in range(mates)] for i, n in enumerate(sizes)]
+    masks = [np.full(n, 7, np.uint8) for n in sizes]
+    trims = [np.zeros(n * mates, np.uint32) for n in sizes]
+    with H.Engine(p) as e:
+        for i, (bs, m, t) in enumerate(zip(bat, masks, trims)):
+            if i % 2 == 0:   # in place
+                e.run_host_in_place([(b.seq, b.qual, b.idx) for b in bs], m, t if edit else None)
+            else:            # copied
+                hbs = [H.engine.host_batch(b.seq, b.qual, b.idx) for b in bs]
+                e.run_host(hbs[0], hbs[1] if paired else None, m, t if edit else None)
+            if i == 2:
+                e.sync()
+        e.sync()
+        got = e.counters()
+    want = np.zeros_like(got)
+    for bs, m, t in zip(bat, masks, trims):
+        m_o, t_o, c_o = O.run(p, bs[0], bs[1] if paired else None)
         np.testing.assert_array_equal(m, m_o)
         if edit:
             np.testing.assert_array_equal(t, t_o)

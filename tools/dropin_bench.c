@@ -11,12 +11,14 @@
  *             src/stats_options.c:21), one hpgq ctx each (GPU t % ndev).  A
  *             worker takes the next batch, packs it into malloc'd SoA buffers,
  *             calls hpgq_run_host + hpgq_sync and frees the buffers --
- *             fastq_stats_worker of INTEGRATION.md (src/stats_fastq.c:202-250).
+ *             fastq_stats_worker of INTEGRATION.md (src/stats_fastq.c:202-250);
+ *             the SoA buffers are the ctx's staging slot (hpgq_host_batch),
+ *             or with --copy malloc'd ones that hpgq_run_host copies.
  *   consumer  nothing per read; the ctxs' counters are summed at the end.
  * Prints one JSON line.  --counters F / --mask F write the summed u64 counter
  * set and the per-read masks (input order) for tests/test_dropin_gpu.py.
  *
- *   dropin_bench in.fq [--batch 10000] [--threads 2] [--lmax 1024] [--c2]
+ *   dropin_bench in.fq [--batch 10000] [--threads 2] [--lmax 1024] [--c2] [--copy]
  *                      [--counters F] [--mask F] [--repeat R]
  * --c2: the C2 filter (--read-quality-range 20, --read-length-range 50,).
  */
@@ -102,7 +104,11 @@ typedef struct {
   hpgq_ctx_t *ctx;
 } worker_t;
 
-/* INTEGRATION.md fastq_stats_worker, once per batch */
+static int g_copy;   /* --copy: the malloc'd-batch worker (hpgq_run_host copies it) */
+
+/* INTEGRATION.md fastq_stats_worker, once per batch: the reads are packed
+ * straight into the ctx's staging slot (hpgq_host_batch), or with --copy into
+ * malloc'd buffers that hpgq_run_host copies into the slot */
 static void *worker(void *arg) {
   worker_t *w = arg;
   for (;;) {
@@ -113,15 +119,28 @@ static void *worker(void *arg) {
     int32_t *idx = malloc((n + 1) * sizeof(int32_t));   /* offsets first: one strlen per read */
     idx[0] = 0;
     for (size_t i = 0; i < n; i++) idx[i + 1] = idx[i] + (int32_t)strlen(bt->reads[i].sequence);
-    char *seq = malloc((size_t)idx[n] + 1), *qual = malloc((size_t)idx[n] + 1);
-    for (size_t i = 0; i < n; i++) {
-      const size_t len = (size_t)(idx[i + 1] - idx[i]);
-      memcpy(seq + idx[i], bt->reads[i].sequence, len);
-      memcpy(qual + idx[i], bt->reads[i].quality, len);
+    hpgq_batch_t b;
+    char *seq, *qual;
+    int rc = HPGQ_OK;
+    if (g_copy) {
+      seq = malloc((size_t)idx[n] + 1);
+      qual = malloc((size_t)idx[n] + 1);
+      b = (hpgq_batch_t){(int64_t)n, seq, qual, idx};
+    } else {
+      rc = hpgq_host_batch(w->ctx, (int64_t)n, (size_t)idx[n], 0, &b, NULL);
+      if (rc == HPGQ_OK) memcpy((int32_t *)b.data_indices, idx, (n + 1) * sizeof(int32_t));
+      seq = (char *)b.seq;
+      qual = (char *)b.quality;
     }
-    hpgq_batch_t b = {(int64_t)n, seq, qual, idx};
+    if (rc == HPGQ_OK) {
+      for (size_t i = 0; i < n; i++) {
+        const size_t len = (size_t)(idx[i + 1] - idx[i]);
+        memcpy(seq + idx[i], bt->reads[i].sequence, len);
+        memcpy(qual + idx[i], bt->reads[i].quality, len);
+      }
+    }
     uint8_t *mask = malloc(n);
-    int rc = hpgq_run_host(w->ctx, &b, NULL, mask, NULL);
+    if (rc == HPGQ_OK) rc = hpgq_run_host(w->ctx, &b, NULL, mask, NULL);
     if (rc == HPGQ_OK) rc = hpgq_sync(w->ctx);   /* mask valid, buffers reusable */
     if (rc != HPGQ_OK) {
       fprintf(stderr, "hpgq: %s\n", hpgq_strerror(rc));
@@ -129,8 +148,10 @@ static void *worker(void *arg) {
     }
     if (g_mask) memcpy(g_mask + bt->first, mask, n);
     free(mask);
-    free(seq);
-    free(qual);
+    if (g_copy) {
+      free(seq);
+      free(qual);
+    }
     free(idx);
   }
   return NULL;
@@ -138,7 +159,7 @@ static void *worker(void *arg) {
 
 int main(int argc, char **argv) {
   if (argc < 2) {
-    fprintf(stderr, "usage: dropin_bench in.fq [--batch N] [--threads T] [--lmax L] [--c2] "
+    fprintf(stderr, "usage: dropin_bench in.fq [--batch N] [--threads T] [--lmax L] [--c2] [--copy] "
                     "[--counters F] [--mask F] [--repeat R]\n");
     return 2;
   }
@@ -151,6 +172,7 @@ int main(int argc, char **argv) {
     else if (!strcmp(argv[i], "--lmax") && i + 1 < argc) lmax = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--repeat") && i + 1 < argc) repeat = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--c2")) c2 = 1;
+    else if (!strcmp(argv[i], "--copy")) g_copy = 1;
     else if (!strcmp(argv[i], "--counters") && i + 1 < argc) ctr_path = argv[++i];
     else if (!strcmp(argv[i], "--mask") && i + 1 < argc) mask_path = argv[++i];
     else {
@@ -220,9 +242,10 @@ int main(int argc, char **argv) {
   }
   printf("{\"reads\": %zu, \"batches\": %zu, \"batch_reads\": %zu, \"threads\": %d, \"gpus\": %d, "
          "\"repeat\": %d, \"best_s\": %.6f, \"mean_s\": %.6f, \"mreads_s\": %.3f, \"mreads_s_mean\": %.3f, "
-         "\"load_s\": %.3f, \"num_input\": %llu, \"num_passed\": %llu}\n",
+         "\"load_s\": %.3f, \"num_input\": %llu, \"num_passed\": %llu, \"staging\": \"%s\"}\n",
          g_total, g_nbatches, batch, threads, threads < ndev ? threads : ndev, repeat, best, sum / repeat,
          g_total / best / 1e6, g_total / (sum / repeat) / 1e6, load_s,
-         (unsigned long long)tot[HPGQ_S_NUM_INPUT], (unsigned long long)tot[HPGQ_S_NUM_PASSED]);
+         (unsigned long long)tot[HPGQ_S_NUM_INPUT], (unsigned long long)tot[HPGQ_S_NUM_PASSED],
+         g_copy ? "copy" : "in_place");
   return 0;
 }
