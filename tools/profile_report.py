@@ -29,7 +29,7 @@ ENG = ("engine_tri_kernel", "engine_tri_x_kernel", "engine_kernel")
 KERNELS = {"c2": ENG, "c3": ENG, "c4": ENG, "c4_noor": ENG, "c4_pe": ENG,
            "c5": ("cgr_stream_kernel", "span_first_kernel"),
            "c5_valid": ("cgr_stream_kernel", "span_first_kernel"),
-           "c2_lr": ENG, "c2_250": ENG,
+           "c2_lr": ENG, "c2_250": ENG, "c2_noor": ENG,
            "c2_kmers": ("kmer_tile_kernel", "kmer_maxlen_kernel", "kmer_reduce_kernel")}
 
 
