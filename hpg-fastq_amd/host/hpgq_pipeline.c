@@ -61,6 +61,11 @@ typedef struct {
   uint32_t *trim, *rec_start, *seq_start, *plus_start, *qual_start;
   int32_t *idx;
   size_t res_cap;
+  /* edit: the chunk's output records per class (0 edit.fq / passed, 1 failed),
+   * assembled by the GPU worker so the writer only writes them in order */
+  char *out[2];
+  size_t out_cap[2], out_len[2];
+  uint64_t out_n[2];
 } slot_t;
 
 typedef struct {
@@ -298,34 +303,28 @@ static int write_span(FILE *f, const char *p, size_t n) { return fwrite(p, 1, n,
 static int write_slot(pipe_t *P, slot_t *s) {
   const int edit = P->o->command == CMD_EDIT;
   const int filter_on = P->o->filter_on;
+  if (edit) {   /* the worker assembled the trimmed records (assemble_edit) */
+    FILE *fc[2] = {P->out_pass, P->out_fail};
+    for (int c = 0; c < 2; ++c)
+      if (fc[c] && s->out_len[c] && write_span(fc[c], s->out[c], s->out_len[c])) return -1;
+    P->written_pass += s->out_n[0];
+    P->written_fail += s->out_n[1];
+    return 0;
+  }
   for (int64_t i = 0; i < s->nreads; ++i) {
     const int pass = s->mask[i] != 0;
     FILE *f = pass || !filter_on ? P->out_pass : P->out_fail;
-    if (!f) continue;
-    const uint32_t a = s->rec_start[i];
-    const uint32_t e = i + 1 < s->nreads ? s->rec_start[i + 1] : (uint32_t)s->use;
-    if (!edit) {
-      /* whole input record; consecutive records of one class as one span */
-      int64_t j = i + 1;
-      while (j < s->nreads && (s->mask[j] != 0) == pass) ++j;
+    /* whole input records; consecutive records of one class as one span */
+    int64_t j = i + 1;
+    while (j < s->nreads && (s->mask[j] != 0) == pass) ++j;
+    if (f) {
+      const uint32_t a = s->rec_start[i];
       const uint32_t ee = j < s->nreads ? s->rec_start[j] : (uint32_t)s->use;
       if (write_span(f, s->buf + a, ee - a)) return -1;
       if (pass) P->written_pass += (uint64_t)(j - i);
       else P->written_fail += (uint64_t)(j - i);
-      i = j - 1;
-      continue;
     }
-    (void)e;
-    const uint32_t ts = s->trim[i] & 0xFFFFu, te = s->trim[i] >> 16;
-    const uint32_t len = (uint32_t)(s->idx[i + 1] - s->idx[i]);
-    const uint32_t keep = len - ts - te;
-    if (write_span(f, s->buf + a, s->seq_start[i] - a) ||                          /* header line */
-        write_span(f, s->buf + s->seq_start[i] + ts, keep) || fputc('\n', f) == EOF ||
-        write_span(f, s->buf + s->plus_start[i], s->qual_start[i] - s->plus_start[i]) ||   /* '+' line */
-        write_span(f, s->buf + s->qual_start[i] + ts, keep) || fputc('\n', f) == EOF)
-      return -1;
-    if (pass || !filter_on) P->written_pass++;
-    else P->written_fail++;
+    i = j - 1;
   }
   return 0;
 }
@@ -352,6 +351,54 @@ static void *writer_main(void *arg) {
 }
 
 /* ---- GPU worker (this thread) -------------------------------------------- */
+
+/* edit: a chunk's trimmed records per output class, in input order (header
+ * line, seq[ts, len - te), '+' line, qual[ts, len - te); each at most its input
+ * record's bytes), built on the worker thread: with the writer formatting them
+ * read by read through stdio (6 calls per read) `edit` ran at 6.8 Mreads/s end
+ * to end against 135 for `stats` */
+static int assemble_edit(pipe_t *P, slot_t *s) {
+  const int filter_on = P->o->filter_on;
+  FILE *fc[2] = {P->out_pass, P->out_fail};
+  for (int c = 0; c < 2; ++c) {
+    s->out_len[c] = 0;
+    s->out_n[c] = 0;
+    if (fc[c] && s->out_cap[c] < s->use + 64) {
+      free(s->out[c]);
+      s->out_cap[c] = s->use + s->use / 8 + 64;
+      s->out[c] = malloc(s->out_cap[c]);
+      if (!s->out[c]) {
+        s->out_cap[c] = 0;
+        return HPGQ_E_NOMEM;
+      }
+    }
+  }
+  char *d[2] = {s->out[0], s->out[1]};
+  for (int64_t i = 0; i < s->nreads; ++i) {
+    const int c = s->mask[i] != 0 || !filter_on ? 0 : 1;
+    if (!fc[c]) continue;
+    const uint32_t a = s->rec_start[i];
+    const uint32_t ts = s->trim[i] & 0xFFFFu, te = s->trim[i] >> 16;
+    const uint32_t len = (uint32_t)(s->idx[i + 1] - s->idx[i]);
+    const uint32_t keep = len - ts - te;
+    const uint32_t hl = s->seq_start[i] - a, pl = s->qual_start[i] - s->plus_start[i];
+    char *o = d[c];
+    memcpy(o, s->buf + a, hl);                               /* header line */
+    o += hl;
+    memcpy(o, s->buf + s->seq_start[i] + ts, keep);
+    o += keep;
+    *o++ = '\n';
+    memcpy(o, s->buf + s->plus_start[i], pl);                 /* '+' line */
+    o += pl;
+    memcpy(o, s->buf + s->qual_start[i] + ts, keep);
+    o += keep;
+    *o++ = '\n';
+    d[c] = o;
+    s->out_n[c]++;
+  }
+  for (int c = 0; c < 2; ++c) s->out_len[c] = fc[c] ? (size_t)(d[c] - s->out[c]) : 0;
+  return 0;
+}
 
 static int ensure_results(slot_t *s, int64_t n) {
   if ((size_t)n <= s->res_cap) return 0;
@@ -454,6 +501,7 @@ static int worker_chunk(worker_t *W, slot_t *s) {
   }
   trace_at(W->P, s->chunk, 3, -1);
   if (rc == 0) rc = hpgq_sync(W->ctx);
+  if (rc == 0 && edit) rc = assemble_edit(W->P, s);
   if (rc == 0 && W->cg) {   /* after the parse and the mask; settled before the next parse reuses b */
     rc = hpgq_cgr_fill_device(W->cg, &b, o->filter_on ? W->d_mask : NULL,
                               o->filter_on ? HPGQ_CGR_ONLY_VALID_READS : HPGQ_CGR_ALL_READS);
@@ -646,6 +694,8 @@ done:
     free(P.slot[i].seq_start);
     free(P.slot[i].plus_start);
     free(P.slot[i].qual_start);
+    free(P.slot[i].out[0]);
+    free(P.slot[i].out[1]);
     free(P.slot[i].idx);
   }
   free(P.carry);
