@@ -39,6 +39,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/stat.h>
+#include <sys/uio.h>
 #include <time.h>
 #include <unistd.h>
 
@@ -300,6 +301,47 @@ static void *reader_main(void *arg) {
 
 static int write_span(FILE *f, const char *p, size_t n) { return fwrite(p, 1, n, f) == n ? 0 : -1; }
 
+/* the spans of one output class, flushed by writev (the stream is drained
+ * first: nothing of it is buffered in stdio across these calls) */
+#define SPAN_IOV 1024
+typedef struct {
+  FILE *f;
+  struct iovec v[SPAN_IOV];
+  int n;
+} spans_t;
+
+static int spans_flush(spans_t *S) {
+  int k = 0;
+  while (k < S->n) {
+    const int cnt = S->n - k;
+    const ssize_t w = writev(fileno(S->f), S->v + k, cnt);
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      return -1;
+    }
+    size_t left = (size_t)w;   /* partial write: skip the whole iovecs, trim the next */
+    while (k < S->n && left >= S->v[k].iov_len) left -= S->v[k++].iov_len;
+    if (k < S->n) {
+      S->v[k].iov_base = (char *)S->v[k].iov_base + left;
+      S->v[k].iov_len -= left;
+    }
+  }
+  S->n = 0;
+  return 0;
+}
+
+static int spans_add(spans_t *S, const char *p, size_t n) {
+  if (S->n && (const char *)S->v[S->n - 1].iov_base + S->v[S->n - 1].iov_len == p) {   /* contiguous */
+    S->v[S->n - 1].iov_len += n;
+    return 0;
+  }
+  if (S->n == SPAN_IOV && spans_flush(S)) return -1;
+  S->v[S->n].iov_base = (void *)p;
+  S->v[S->n].iov_len = n;
+  S->n++;
+  return 0;
+}
+
 static int write_slot(pipe_t *P, slot_t *s) {
   const int edit = P->o->command == CMD_EDIT;
   const int filter_on = P->o->filter_on;
@@ -311,21 +353,33 @@ static int write_slot(pipe_t *P, slot_t *s) {
     P->written_fail += s->out_n[1];
     return 0;
   }
+  /* whole input records, consecutive records of one class as one span, the
+   * spans of each class gathered into writev calls of up to SPAN_IOV spans
+   * (one write per span -- ~5 KB at 6 % failed reads -- ran at 4 GB/s into
+   * tmpfs, which takes 8.6 GB/s in 64 KB writes) */
+  static __thread spans_t S[2];
+  S[0].f = P->out_pass;
+  S[1].f = P->out_fail;   /* (without a filter every record is class 0) */
+  for (int c = 0; c < 2; ++c) {
+    S[c].n = 0;
+    if (S[c].f && fflush(S[c].f)) return -1;
+  }
   for (int64_t i = 0; i < s->nreads; ++i) {
     const int pass = s->mask[i] != 0;
-    FILE *f = pass || !filter_on ? P->out_pass : P->out_fail;
-    /* whole input records; consecutive records of one class as one span */
+    spans_t *sp = &S[pass || !filter_on ? 0 : 1];
     int64_t j = i + 1;
     while (j < s->nreads && (s->mask[j] != 0) == pass) ++j;
-    if (f) {
+    if (sp->f) {
       const uint32_t a = s->rec_start[i];
       const uint32_t ee = j < s->nreads ? s->rec_start[j] : (uint32_t)s->use;
-      if (write_span(f, s->buf + a, ee - a)) return -1;
+      if (spans_add(sp, s->buf + a, ee - a)) return -1;
       if (pass) P->written_pass += (uint64_t)(j - i);
       else P->written_fail += (uint64_t)(j - i);
     }
     i = j - 1;
   }
+  for (int c = 0; c < 2; ++c)
+    if (S[c].f && S[c].n && spans_flush(&S[c])) return -1;
   return 0;
 }
 
