@@ -688,7 +688,7 @@ static size_t host_layout(int nm, int64_t n, const size_t (&bytes)[2], size_t (&
 
 int hpgq_host_batch(hpgq_ctx_t *c, int64_t num_reads, size_t nbytes, size_t nbytes2, hpgq_batch_t *b,
                     hpgq_batch_t *b2) {
-  if (!c || !b || num_reads < 1 || nbytes > (size_t)INT32_MAX || nbytes2 > (size_t)INT32_MAX) return HPGQ_E_INVALID;
+  if (!c || !b || num_reads < 0 || nbytes > (size_t)INT32_MAX || nbytes2 > (size_t)INT32_MAX) return HPGQ_E_INVALID;
   if ((c->nm == 2) != (b2 != nullptr)) return HPGQ_E_INVALID;
   HPGQ_HIP_TRY(hipSetDevice(c->device));
   const size_t bytes[2] = {nbytes, c->nm == 2 ? nbytes2 : 0};

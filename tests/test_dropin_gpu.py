@@ -95,7 +95,7 @@ def test_host_batch_in_place(paired, edit):
          else H.stats_params(lmax=150, read_quality_range="20,", read_length_range="50,"))
     p.paired = 1 if paired else 0
     mates = 2 if paired else 1
-    sizes = [20000, 1, 9999, 30000, 4096]
+    sizes = [20000, 1, 0, 9999, 30000, 4096]   # (an empty batch in place: reserved, nothing to run)
     bat = [[O.synth(n, seed=70 + i, L=150, trunc_pct=10, n_per_1024=8, first=1000 * i, mate=m)
             for m in range(mates)] for i, n in enumerate(sizes)]
     masks = [np.full(n, 7, np.uint8) for n in sizes]
