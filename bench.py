@@ -18,6 +18,14 @@ not the driver's line):
   python bench.py [--gpus N --steps K --warmup W] [--config c2|c3|c4|c5]
   python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 
+`--gpus N` with N > 1 and no WORLD_SIZE in the environment starts the N rank
+processes itself (fresh interpreters, one per GPU, before this process touches
+the GPU) and relays rank 0's line; under torch.distributed.run each rank checks
+that WORLD_SIZE equals --gpus.  Rank control (rendezvous, barriers, the
+max-over-ranks time) runs on gloo; the data path's one exchange is libhpgq's
+RCCL all-reduce, whose rank count is reported as config.rccl_ranks.
+`--launch-dry-run` exercises the launcher and the read sharding on CPU (no GPU).
+
 Prints ONE JSON line (rank 0) with `roofline` (the hot kernel, HIP events on
 the engine's own stream) and `cpu_baseline` (oracle/liboracle.so, C+OpenMP,
 timed on this host's cores on a bounded sample, rank 0 at N=1 only).
@@ -34,7 +42,15 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "hpg-fastq_amd"))
 
-import hpgfastq as H  # noqa: E402
+H = None   # hpgfastq, imported by the rank processes (the launcher never loads libhpgq)
+
+
+def _load_hpgfastq():
+    global H
+    if H is None:
+        import hpgfastq
+        H = hpgfastq
+    return H
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
 
@@ -113,7 +129,17 @@ def parse():
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end CLI leg (C2)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--lmax", type=int, default=None, help="override the config's lmax")
+    ap.add_argument("--route", default=None,
+                    help="A/B only: engine kernel route (hpgq_debug_set_route: auto, single, tri, hex, "
+                         "wide, auto_fixed)")
+    ap.add_argument("--launch-dry-run", action="store_true",
+                    help="launcher + read sharding on CPU: gloo ranks, no GPU, no kernels")
+    ap.add_argument("--share-device", action="store_true",
+                    help="functional test of N ranks on fewer GPUs (ranks share device LOCAL_RANK mod "
+                         "count; RCCL over its socket transport): not a scaling measurement")
     a = ap.parse_args()
+    if a.gpus < 1:
+        ap.error("--gpus must be >= 1")
     if a.steps < 1 or a.warmup < 0:
         ap.error("--steps must be >= 1 and --warmup >= 0")
     cfg = CONFIGS[a.config]
@@ -347,9 +373,6 @@ def e2e_leg(args, device, runs=5):
     cpus = numa_cpus(device)
     share = sorted(cpus)[:omp_threads(len(cpus) or 16)] if cpus else None
 
-    def pin():
-        if share:
-            os.sched_setaffinity(0, share)
     out = {"reads": E2E_READS, "read_length": 150, "runs": runs,
            "command": "hpg-fastq stats -f <file> --read-quality-range 20, --read-length-range 50, "
                       f"--gpus 1 --num-threads {len(share) if share else 16}",
@@ -357,8 +380,11 @@ def e2e_leg(args, device, runs=5):
     try:
         subprocess.run(["gcc", "-O2", "-fopenmp", os.path.join(ROOT, "tools", "fqgen.c"), "-o", gen],
                        check=True, capture_output=True, timeout=120)
-        subprocess.run([gen, fq, str(E2E_READS), "150", "2"], check=True, capture_output=True, timeout=300,
-                       preexec_fn=pin, env=dict(os.environ, OMP_NUM_THREADS=str(len(share) if share else 16)))
+        # fqgen pins itself to the GPU's NUMA CPUs (no preexec_fn: this process
+        # may already run GPU runtime threads)
+        subprocess.run([gen, fq, str(E2E_READS), "150", "2", ",".join(map(str, share or []))], check=True,
+                       capture_output=True, timeout=300,
+                       env=dict(os.environ, OMP_NUM_THREADS=str(len(share) if share else 16)))
         out["fastq_gb"] = round(os.path.getsize(fq) / 1e9, 3)
         vals, gbs = [], []
         for rep in range(runs + 1):   # run 0 warms the GPU clocks and the file's pages: not counted
@@ -401,7 +427,7 @@ def dropin_main(args):
     tmp = tempfile.mkdtemp(prefix="hpgq_dropin_")
     gen = os.path.join(tmp, "fqgen")
     fq = os.path.join("/dev/shm" if os.path.isdir("/dev/shm") else tmp, f"hpgq_dropin_{os.getpid()}.fq")
-    n = args.reads if args.reads != CONFIGS["dropin"]["reads"] else CONFIGS["dropin"]["reads"]
+    n = args.reads
     try:
         subprocess.run(["gcc", "-O2", "-fopenmp", os.path.join(ROOT, "tools", "fqgen.c"), "-o", gen],
                        check=True, capture_output=True, timeout=120)
@@ -463,21 +489,176 @@ def make_batches(args, rank, dev, mates):
     return out
 
 
+# ---- N ranks: the launcher (no GPU in this process) --------------------------
+def free_port():
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(args):
+    """`--gpus N` (N > 1) without WORLD_SIZE: start N rank processes of this
+    script, one per GPU (the old tool's --gpu-num-devices,
+    old/main_hpg_fastq_old.c:113,161), with RANK / LOCAL_RANK / WORLD_SIZE and a
+    127.0.0.1 rendezvous, and relay rank 0's JSON line.  This process never
+    touches the GPU (nor loads libhpgq) and never execs: the ranks are fresh
+    child interpreters.  A rank that fails ends the others; the exit code is
+    the first failure's."""
+    import subprocess
+    n = args.gpus
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   HSA_ENABLE_IPC_MODE_LEGACY="0")
+        if args.share_device:
+            # ranks sharing one device: RCCL refuses two ranks on one GPU of one
+            # host, so each rank names its own host and the ranks talk over
+            # RCCL's socket transport on loopback (function, not speed)
+            env.update(NCCL_HOSTID=f"hpgq-bench-rank{r}", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1")
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL, text=True))
+    rc = 0
+    while any(p.poll() is None for p in procs):
+        bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+        if bad:
+            rc = bad[0]
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            t_end = time.time() + 15
+            for p in procs:
+                try:
+                    p.wait(timeout=max(0.1, t_end - time.time()))
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            break
+        time.sleep(0.1)
+    out = procs[0].stdout.read()
+    procs[0].stdout.close()
+    if rc == 0:
+        rc = next((p.returncode for p in procs if p.returncode != 0), 0)
+    line = [ln for ln in out.splitlines() if ln.startswith("{")]
+    if rc == 0 and line:
+        print(line[-1], flush=True)
+    elif rc == 0:
+        print("bench: rank 0 printed no result line", file=sys.stderr)
+        rc = 1
+    return rc
+
+
+def rank_env(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}: launch one rank per GPU "
+              f"(`python bench.py --gpus N` starts them, or torch.distributed.run --nproc-per-node N)",
+              file=sys.stderr)
+        sys.exit(2)
+    return world, rank, local
+
+
+def shard(args, rank):
+    """Rank r owns reads [r*R, (r+1)*R) of the counter-based generator."""
+    return [rank * args.reads, (rank + 1) * args.reads]
+
+
+def result_line(args, cfg, world, el, steps_reads, roofline, rccl_ranks, dtype, extra_config=None):
+    cfgd = {"workload": cfg["workload"], "reads_per_gpu": args.reads, "read_length": args.read_length,
+            "batch_reads": args.batch_reads,
+            "parallelism": f"read-sharded x{world}, RCCL all-reduce of "
+                           + ("the u32 CGR tables" if args.config in ("c5", "c5_valid") else "the counters")}
+    if world > 1:
+        cfgd["rccl_ranks"] = rccl_ranks
+    cfgd.update(extra_config or {})
+    return {
+        "metric": cfg["metric"],
+        "value": None if el is None else round(steps_reads / el / 1e6, 2),
+        "unit": cfg["unit"],
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": None if el is None else round(el / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": dtype,
+        "data": "synthetic (counter-based generator, resident in HBM)",
+        "config": cfgd,
+        "roofline": roofline,
+    }
+
+
+def dry_run_rank(args, world, rank):
+    """--launch-dry-run: the rank plumbing on CPU.  Each rank derives its read
+    range, fills the host offsets of its first reads with the same generator
+    (hpgq_synth_indices_host: no device), and rank 0 checks over gloo that the
+    ranges are disjoint and cover [0, world*R) before printing the line."""
+    import torch.distributed as dist
+    _load_hpgfastq()
+    cfg = CONFIGS[args.config]
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    lo, hi = shard(args, rank)
+    n = min(1000, args.reads)
+    s = H.Synth(args.seed, args.read_length, 5, 5, 1, 33, 0)
+    idx = np.zeros(n + 1, np.int32)
+    H.check(H.lib.hpgq_synth_indices_host(C.byref(s), lo, n, idx.ctypes.data), "idx")
+    mine = {"rank": rank, "range": [lo, hi], "first_bytes": int(idx[-1]), "pid": os.getpid()}
+    t0 = time.perf_counter()
+    got = [None] * world
+    if world > 1:
+        dist.all_gather_object(got, mine)
+        dist.barrier()
+    else:
+        got = [mine]
+    el = time.perf_counter() - t0
+    if rank == 0:
+        ranges = sorted(g["range"] for g in got)
+        ok = ranges[0][0] == 0 and all(a[1] == b[0] for a, b in zip(ranges, ranges[1:])) \
+            and ranges[-1][1] == world * args.reads and len({g["pid"] for g in got}) == world
+        if not ok:
+            print(f"bench: bad shards {got}", file=sys.stderr)
+            sys.exit(3)
+        out = result_line(args, cfg, world, None, 0, None, None, "u8",
+                          {"dry_run": True, "shards": [g["range"] for g in sorted(got, key=lambda g: g["rank"])],
+                           "rendezvous_s": round(el, 4)})
+        out["dry_run"] = True
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    world, rank, local = rank_env(args)
+    if args.launch_dry_run:
+        return dry_run_rank(args, world, rank)
+    _load_hpgfastq()
     if args.config == "dropin":
+        if world > 1:
+            print("bench: --config dropin is a one-GPU host-path harness", file=sys.stderr)
+            sys.exit(2)
         return dropin_main(args)
     cfg = CONFIGS[args.config]
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    if local >= ndev and not args.share_device:
+        print(f"bench: rank {rank} needs device {local} but {ndev} are visible", file=sys.stderr)
+        sys.exit(2)
+    local_dev = local % max(ndev, 1)
+    if world > 1:   # rank control on gloo; the data path's exchange is libhpgq's RCCL
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
 
     L = args.read_length
     cgr = args.config in ("c5", "c5_valid")
@@ -495,18 +676,18 @@ def main():
     if kmers:
         # the engine's C2 masks once (setup), then each step counts the passed
         # reads' 5-mers: the k-mer kernel alone is what the step times
-        eng = H.Engine(params, device=local)
+        eng = H.Engine(params, device=local_dev)
         for i, (n, mm, _nb) in enumerate(batches):
             sq, ql, ix = mm[0]
             eng.run_device(H.engine.device_batch(n, sq.data_ptr(), ql.data_ptr(), ix.data_ptr()), None,
                            d_mask.data_ptr() + int(offs[i]), None)
         eng.sync()
-        km = H.Kmers(L, device=local, stream=eng.stream)
+        km = H.Kmers(L, device=local_dev, stream=eng.stream)
         kernel_name = "hpgq::kmers::kmer_tile_kernel (+kmer_reduce_kernel; +kmer_maxlen_kernel above 8 tiles)"
         # seq + offsets + the mask (quality is not read)
         alg = [(nb - 4 * (n + 1)) // 2 + 4 * (n + 1) + n for (n, _m, nb) in batches]
     elif cgr:
-        eng = H.ChaosGame(7, 33, device=local)
+        eng = H.ChaosGame(7, 33, device=local_dev)
         kernel_name = f"hpgq::cgr::stream::cgr_stream_kernel<7, {'true' if valid else 'false'}> (+span_first)"
         # algorithmic bytes per read: seq + quality + offset (tables stay in LDS)
         # (+ 1 status byte per read; the skipped reads' bytes are streamed too)
@@ -518,15 +699,20 @@ def main():
                 lo += n
             torch.cuda.synchronize()
     else:
-        eng = H.Engine(params, device=local)
+        eng = H.Engine(params, device=local_dev, route=args.route)
         kernel_name = eng.kernel_name
         # + 1 B mask per read (pair), + 4 B trim per read when editing
         alg = [nb + n + (4 * n * mates if params.edit_on else 0) for (n, _m, nb) in batches]
+    rccl_ranks = None
     if world > 1:   # one RCCL communicator inside libhpgq (counters / CGR tables)
         uid = H.engine.comm_unique_id() if rank == 0 else b"\0" * 128
         obj = [uid]
         dist.broadcast_object_list(obj, src=0)
         eng.comm_init(world, rank, obj[0])
+        rccl_ranks = eng.comm_count()
+        if rccl_ranks != world:
+            print(f"bench: RCCL communicator has {rccl_ranks} ranks, world is {world}", file=sys.stderr)
+            sys.exit(3)
     ext = torch.cuda.ExternalStream(eng.stream, device=dev)
     hb = [[H.engine.device_batch(n, sq.data_ptr(), ql.data_ptr(), ix.data_ptr())
            for (sq, ql, ix) in mm] for (n, mm, _nb) in batches]
@@ -560,7 +746,7 @@ def main():
                                d_trim.data_ptr() + 4 * int(offs[i]) if params.edit_on else None)
             if s is not None and i == nb - 1 and (per_step or s == args.steps - 1):
                 ev[s][1].record(ext)
-        if world > 1:   # the one exchange step: RCCL sum of the counters / u32 CGR tables
+        if world > 1 and not kmers:   # the one exchange step: RCCL sum of the counters / u32 CGR tables
             eng.allreduce()
 
     for _ in range(args.warmup):
@@ -583,16 +769,16 @@ def main():
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    t = torch.tensor([el], dtype=torch.float64, device=dev)
-    if world > 1:
+    if world > 1:   # max over ranks (gloo, host tensor)
+        t = torch.tensor([el], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    el = float(t.item())
+        el = float(t.item())
     if per_step:
         timed_ms = sum(a.elapsed_time(b) for a, b in ev)
     else:
         timed_ms = ev[0][0].elapsed_time(ev[-1][1])
 
-    # sanity: every read accounted for
+    # sanity: every read accounted for (after the all-reduce: every rank's reads)
     if kmers:
         assert int(km.by_pos().sum()) > 0 or os.environ.get("HPGQ_BENCH_NOCHECK")   # (timing probes)
     elif cgr:
@@ -600,54 +786,44 @@ def main():
         assert wc > 0 or os.environ.get("HPGQ_BENCH_NOCHECK")   # (timing-probe builds add nothing)
     else:
         ctr = eng.counters()
-        expect = args.reads * (world if world > 1 else 1)
+        expect = args.reads * world
         assert int(ctr[H.S_NUM_INPUT]) == expect, (int(ctr[H.S_NUM_INPUT]), expect)
 
     total = args.reads * world * args.steps
-    value = total / el / 1e6
     avg_launch_s = timed_ms / (args.steps * nb) / 1e3
     bytes_per_launch = float(np.mean(alg))
     achieved = bytes_per_launch / avg_launch_s / 1e9
 
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", f"pmc_engine_{args.config}.json")
+    # HBM bytes per launch: NOT measured in this run (PMC counters need their
+    # own rocprofv3 passes); taken from the committed PMC profile of the same
+    # kernel and batch size, and labelled with its file
+    traffic, traffic_src = None, None
+    pmc_rel = os.path.join("profiles", f"pmc_engine_{args.config}.json")
+    pmc = os.path.join(ROOT, pmc_rel)
     if os.path.exists(pmc):
         try:
             rec = json.load(open(pmc))
             if rec.get("kernel") == kernel_name and rec.get("batch_reads") == args.batch_reads:
                 traffic = rec.get("hbm_bytes_per_launch")
+                traffic_src = pmc_rel + " (committed rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes, not this run)"
         except (OSError, ValueError):
             traffic = None
 
-    out = {
-        "metric": cfg["metric"],
-        "value": round(value, 2),
-        "unit": cfg["unit"],
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(el / args.steps * 1e3, 3),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "f64" if cgr else "u8",
-        "data": "synthetic (counter-based generator, resident in HBM)",
-        "config": {"workload": cfg["workload"], "reads_per_gpu": args.reads, "read_length": L,
-                   "batch_reads": args.batch_reads,
-                   "parallelism": f"read-sharded x{world}, RCCL all-reduce of "
-                                  + ("the u32 CGR tables" if cgr else "the counters")},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic, "kernel": kernel_name,
-                     "avg_launch_us": round(avg_launch_s * 1e6, 1),
-                     "alg_bytes_per_launch": int(bytes_per_launch)},
-    }
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic, "traffic_source": traffic_src, "kernel": kernel_name,
+                "avg_launch_us": round(avg_launch_s * 1e6, 1),
+                "alg_bytes_per_launch": int(bytes_per_launch)}
+    extra = {"route": args.route} if args.route else {}
+    if args.share_device:
+        extra["shared_device"] = f"{world} ranks on {ndev} device(s): functional run, not a scaling number"
+    out = result_line(args, cfg, world, el, total, roofline, rccl_ranks, "f64" if cgr else "u8", extra)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, params)
     if rank == 0 and world == 1 and args.config == "c2" and not args.no_e2e:
         eng.close()   # (the CLI runs in its own process)
         eng = None
-        out["e2e"] = e2e_leg(args, local)
+        out["e2e"] = e2e_leg(args, local_dev)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if km is not None:

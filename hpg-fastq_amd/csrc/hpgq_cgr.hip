@@ -990,4 +990,11 @@ int hpgq_cgr_allreduce(hpgq_cgr_t *c) {
 
 uint32_t *hpgq_cgr_global_device(hpgq_cgr_t *c) { return c ? c->d_global : nullptr; }
 
+int hpgq_cgr_comm_count(hpgq_cgr_t *c, int *count) {
+  if (!c || !count) return HPGQ_E_INVALID;
+  *count = 0;
+  if (!c->comm) return HPGQ_E_STATE;
+  return ncclCommCount(c->comm, count) == ncclSuccess ? HPGQ_OK : HPGQ_E_RCCL;
+}
+
 }  // extern "C"

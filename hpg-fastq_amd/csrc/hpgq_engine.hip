@@ -64,10 +64,15 @@ struct hpgq_ctx {
   bool adaptive = false;
   int mode = 0;              // chain of the next call
   int wide_calls = 0;        // calls since the last probe in wide-first mode
-  uint32_t *h_report = nullptr, *d_report = nullptr;   // mapped host words (deferred, reads, seq)
+  // mapped host word: deferred count | call sequence number << 32 (one 8-byte
+  // store by the follow-up stage); the call's read count stays on the host
+  uint32_t *h_report = nullptr, *d_report = nullptr;
   uint32_t seq = 0;          // sequence number of the last call's report
+  int64_t rep_reads[16] = {0};   // reads of call `seq`, by seq & 15
   uint32_t min_seq = 0;      // reports older than this (before a probe) are ignored
   int parity = 0;
+  int route = HPGQ_ROUTE_AUTO;   // hpgq_debug_set_route (tests, A/B); never from the environment
+  int cus = 0;
   uint64_t *d_bits1 = nullptr, *d_bits2 = nullptr;   // deferred reads per s1 unit
   size_t bits_cap = 0;
   // host path (hpgq_run_host): two staging slots, each a pinned host buffer
@@ -270,14 +275,12 @@ static int plan_chain(hpgq_ctx *c, Chain &ch, int cus, int geo_force) {
   // extra per-step scans: N / out-of-range counts, window sums
   const int xm = (nx ? hpgq::X_NOOR : 0) | (lr ? hpgq::X_LR : 0);
   const bool edit = fl & hpgq::F_EDIT;
-  const char *force = std::getenv("HPGQ_KERNEL");   // "single": the catch-all alone (tests)
-  const bool seg = !(force && std::strcmp(force, "single") == 0);
-  if (!seg) {
+  if ((c->route & 0xF) == HPGQ_ROUTE_CATCH_ALL) {   // the catch-all alone (tests)
     catch_all(ch.s1, c->nm, p.lmax, needs_generic(fl), false);
     return finish_stage(c, ch.s1, catch_all_lds(p, c->nm), cus);
   }
   // first geometry: hex for short reads; wide when the counters say reads are
-  // 157..252 long (or when forced: adaptive wide-first chain, HPGQ_TRI_GEO)
+  // 157..252 long (or when forced: adaptive wide-first chain, hpgq_debug_set_route)
   int geo = (stats && p.lmax > hpgq::Geo<hpgq::GEO_HEX>::kPos && p.lmax <= posw) ? hpgq::GEO_WIDE
                                                                                  : hpgq::GEO_HEX;
   if (geo_force >= 0) geo = geo_force;
@@ -301,25 +304,23 @@ static int plan_chain(hpgq_ctx *c, Chain &ch, int cus, int geo_force) {
 }
 
 static int plan(hpgq_ctx *c, int cus) {
-  int geo_force = -1;
-  if (const char *g = std::getenv("HPGQ_TRI_GEO")) {   // tests, A/B: one fixed first geometry
-    if (!std::strcmp(g, "tri")) geo_force = hpgq::GEO_TRI;
-    else if (!std::strcmp(g, "hex")) geo_force = hpgq::GEO_HEX;
-    else if (!std::strcmp(g, "wide")) geo_force = hpgq::GEO_WIDE;
-  }
+  // a fixed first geometry only when hpgq_debug_set_route asks for one (tests, A/B)
+  const int r = c->route & 0xF;
+  const int geo_force = r == HPGQ_ROUTE_FIRST_TRI ? hpgq::GEO_TRI
+                        : r == HPGQ_ROUTE_FIRST_HEX ? hpgq::GEO_HEX
+                        : r == HPGQ_ROUTE_FIRST_WIDE ? hpgq::GEO_WIDE : -1;
   int rc = plan_chain(c, c->ch[0], cus, geo_force);
   if (rc) return rc;
   // hex first with a wide follow-up: batches of mostly long reads run better
   // wide first, so keep that chain too and choose per call
-  const char *ad = std::getenv("HPGQ_ADAPTIVE");   // "0": off (tests, A/B)
-  c->adaptive = c->ch[0].has2 && geo_force < 0 && !(ad && std::atoi(ad) == 0);
+  c->adaptive = c->ch[0].has2 && geo_force < 0 && !(c->route & HPGQ_ROUTE_NO_ADAPTIVE);
   if (!c->adaptive) return HPGQ_OK;
   rc = plan_chain(c, c->ch[1], cus, hpgq::GEO_WIDE);
   if (rc) return rc;
   void *h = nullptr;
   HPGQ_HIP_TRY(hipHostMalloc(&h, 64, hipHostMallocMapped));
   c->h_report = static_cast<uint32_t *>(h);
-  c->h_report[0] = c->h_report[1] = c->h_report[2] = 0;
+  *reinterpret_cast<volatile uint64_t *>(c->h_report) = 0;
   void *d = nullptr;
   HPGQ_HIP_TRY(hipHostGetDevicePointer(&d, h, 0));
   c->d_report = static_cast<uint32_t *>(d);
@@ -331,10 +332,12 @@ static int plan(hpgq_ctx *c, int cus) {
 // kProbeEvery wide-first calls (its report clears the way back)
 static int pick_chain(hpgq_ctx *c) {
   if (!c->adaptive) return 0;
-  volatile uint32_t *r = c->h_report;
-  const uint32_t deferred = r[0], reads = r[1];
-  // (a report from before the last probe may still land after it: ignored)
-  const bool known = reads != 0 && (int32_t)(r[2] - c->min_seq) >= 0;
+  const uint64_t r = *reinterpret_cast<volatile uint64_t *>(c->h_report);
+  const uint32_t deferred = (uint32_t)r, rseq = (uint32_t)(r >> 32);
+  const int64_t reads = c->rep_reads[rseq & 15];
+  // (a report from before the last probe may still land after it: ignored;
+  // so is one too old for the read-count ring, which cannot happen in practice)
+  const bool known = rseq != 0 && reads > 0 && (int32_t)(rseq - c->min_seq) >= 0 && c->seq - rseq < 16;
   const bool mostly_long = known && (uint64_t)deferred * 2 >= reads;
   if (c->mode == 0) {
     if (mostly_long) {
@@ -458,9 +461,8 @@ int hpgq_open(hpgq_ctx_t **out, int device, const hpgq_params_t *p) {
     HPGQ_HIP_TRY(hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming));
     HPGQ_HIP_TRY(hipEventCreateWithFlags(&sl.used, hipEventDisableTiming));
   }
-  int cus = 0;
-  HPGQ_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-  rc = plan(c, cus);
+  HPGQ_HIP_TRY(hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device));
+  rc = plan(c, c->cus);
   if (rc) {
     hpgq_close(c);
     return rc;
@@ -577,6 +579,8 @@ static int launch(hpgq_ctx *c, hpgq::EngineArgs &A) {
     A2.defer_len = ch.s2.defer_len;
     A2.report = c->d_report;   // how many reads hex deferred: the next call's choice
     A2.report_seq = ++c->seq;
+    if (!c->seq) A2.report_seq = ++c->seq;   // 0 means "no report yet"
+    c->rep_reads[c->seq & 15] = A.num_reads;
     rc = launch_stage(c, ch.s2, A2);
     if (rc) return rc;
     and_bits = c->d_bits1;   // bits2 words are only written for units with bits1 set
@@ -712,6 +716,10 @@ int hpgq_host_batch(hpgq_ctx_t *c, int64_t num_reads, size_t nbytes, size_t nbyt
   return HPGQ_OK;
 }
 
+static int run_host_slot(hpgq_ctx *c, hpgq_ctx::Slot &sl, const hpgq_batch_t *const (&bs)[2], int64_t n,
+                         const size_t (&bytes)[2], const size_t (&off)[2][3], size_t mask_off, size_t trim_off,
+                         bool in_place, uint8_t *mask_out, uint32_t *trim_out);
+
 int hpgq_run_host(hpgq_ctx_t *c, const hpgq_batch_t *b, const hpgq_batch_t *b2,
                   uint8_t *mask_out, uint32_t *trim_out) {
   if (!c || !b) return HPGQ_E_INVALID;
@@ -721,7 +729,7 @@ int hpgq_run_host(hpgq_ctx_t *c, const hpgq_batch_t *b, const hpgq_batch_t *b2,
   if (n < 0) return HPGQ_E_INVALID;
   if (n == 0) return HPGQ_OK;
   HPGQ_HIP_TRY(hipSetDevice(c->device));
-  const hpgq_batch_t *bs[2] = {b, b2};
+  const hpgq_batch_t *const bs[2] = {b, b2};
   size_t bytes[2] = {0, 0}, off[2][3], mask_off, trim_off;
   for (int m = 0; m < c->nm; ++m) {
     const int32_t *ix = bs[m]->data_indices;
@@ -753,7 +761,21 @@ int hpgq_run_host(hpgq_ctx_t *c, const hpgq_batch_t *b, const hpgq_batch_t *b2,
   int rc = HPGQ_OK;
   if (in_place) sp = &c->slot[c->cur_slot];
   else if ((rc = slot_acquire(c, total, sp))) return rc;
-  hpgq_ctx::Slot &sl = *sp;
+  rc = run_host_slot(c, *sp, bs, n, bytes, off, mask_off, trim_off, in_place, mask_out, trim_out);
+  if (rc) {
+    // uploads may already be queued into this slot, which is not marked busy:
+    // let them finish before a later call may refill or reallocate the slot
+    // 
+    (void)hipStreamSynchronize(c->cstream);
+    (void)hipStreamSynchronize(c->stream);
+  }
+  return rc;
+}
+
+static int run_host_slot(hpgq_ctx *c, hpgq_ctx::Slot &sl, const hpgq_batch_t *const (&bs)[2], int64_t n,
+                         const size_t (&bytes)[2], const size_t (&off)[2][3], size_t mask_off, size_t trim_off,
+                         bool in_place, uint8_t *mask_out, uint32_t *trim_out) {
+  int rc = HPGQ_OK;
   hpgq::EngineArgs A{};
   fill_args(c, A);
   A.num_reads = n;
@@ -873,5 +895,43 @@ int hpgq_allreduce(hpgq_ctx_t *c) {
 }
 
 uint64_t *hpgq_global_counters_device(hpgq_ctx_t *c) { return c ? c->d_global : nullptr; }
+
+int hpgq_comm_count(hpgq_ctx_t *c, int *count) {
+  if (!c || !count) return HPGQ_E_INVALID;
+  *count = 0;
+  if (!c->comm) return HPGQ_E_STATE;
+  return ncclCommCount(c->comm, count) == ncclSuccess ? HPGQ_OK : HPGQ_E_RCCL;
+}
+
+// ---------------------------------------------------------------------------
+// routing for tests and A/B runs (never read from the environment)
+// ---------------------------------------------------------------------------
+
+int hpgq_debug_set_route(hpgq_ctx_t *c, int route) {
+  if (!c) return HPGQ_E_INVALID;
+  const int r = route & 0xF;
+  if (r > HPGQ_ROUTE_FIRST_WIDE || (route & ~(0xF | HPGQ_ROUTE_NO_ADAPTIVE))) return HPGQ_E_INVALID;
+  HPGQ_HIP_TRY(hipSetDevice(c->device));
+  HPGQ_HIP_TRY(hipStreamSynchronize(c->stream));   // no call of the old chain in flight
+  if (c->h_report) (void)hipHostFree(c->h_report);
+  c->h_report = nullptr;
+  c->d_report = nullptr;
+  c->ch[0] = Chain{};
+  c->ch[1] = Chain{};
+  c->adaptive = false;
+  c->mode = 0;
+  c->wide_calls = 0;
+  c->min_seq = c->seq + 1;
+  const int old = c->route;
+  c->route = route;
+  const int rc = plan(c, c->cus);
+  if (rc) {   // back to the previous route
+    c->route = old;
+    c->ch[0] = Chain{};
+    c->ch[1] = Chain{};
+    (void)plan(c, c->cus);
+  }
+  return rc;
+}
 
 }  // extern "C"

@@ -16,6 +16,12 @@ NUM_SCALARS = 8
 MEANQ_BINS, GC_BINS = 256, 101
 CGR_ALL_READS, CGR_ONLY_VALID_READS = 0, 1
 CGR_PATH_AUTO, CGR_PATH_EXACT = 0, 1
+# hpgq_debug_set_route (tests / A/B only; the library reads no environment)
+ROUTE_AUTO, ROUTE_CATCH_ALL, ROUTE_FIRST_TRI, ROUTE_FIRST_HEX, ROUTE_FIRST_WIDE = range(5)
+ROUTE_NO_ADAPTIVE = 0x10
+ROUTES = {"auto": ROUTE_AUTO, "single": ROUTE_CATCH_ALL, "tri": ROUTE_FIRST_TRI,
+          "hex": ROUTE_FIRST_HEX, "wide": ROUTE_FIRST_WIDE,
+          "auto_fixed": ROUTE_AUTO | ROUTE_NO_ADAPTIVE}
 
 ERRORS = {0: "ok", -1: "invalid argument", -2: "HIP runtime error", -3: "out of memory",
           -4: "read longer than lmax", -5: "no HIP device", -6: "RCCL error",
@@ -110,6 +116,8 @@ _SIGS = [
     ("hpgq_comm_init", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_char_p]),
     ("hpgq_allreduce", C.c_int, [C.c_void_p]),
     ("hpgq_global_counters_device", C.c_void_p, [C.c_void_p]),
+    ("hpgq_comm_count", C.c_int, [C.c_void_p, C.POINTER(C.c_int)]),
+    ("hpgq_debug_set_route", C.c_int, [C.c_void_p, C.c_int]),
     ("hpgq_cgr_open", C.c_int, [C.POINTER(C.c_void_p), C.c_int, C.c_int, C.c_int]),
     ("hpgq_cgr_close", None, [C.c_void_p]),
     ("hpgq_cgr_fill_device", C.c_int, [C.c_void_p, C.POINTER(Batch), C.c_void_p, C.c_int]),
@@ -123,6 +131,7 @@ _SIGS = [
     ("hpgq_cgr_comm_init", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_char_p]),
     ("hpgq_cgr_allreduce", C.c_int, [C.c_void_p]),
     ("hpgq_cgr_global_device", C.c_void_p, [C.c_void_p]),
+    ("hpgq_cgr_comm_count", C.c_int, [C.c_void_p, C.POINTER(C.c_int)]),
     ("hpgq_cgr_load_gs", C.c_int, [C.c_char_p, C.c_int, C.c_void_p, C.c_void_p]),
     ("hpgq_cgr_write_gs", C.c_int, [C.c_char_p, C.c_int, C.c_void_p, C.c_uint32]),
     ("hpgq_cgr_table_dif", C.c_int, [C.c_int, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32,

@@ -9,7 +9,12 @@ import ctypes as C
 
 import numpy as np
 
-from ._abi import (lib, check, Params, Batch, Summary, counters_len, CGR_ALL_READS)
+from ._abi import (lib, check, Params, Batch, Summary, counters_len, CGR_ALL_READS, ROUTES)
+
+# Kernel route for new Engines (tests / A/B: a key of ROUTES, or None for the
+# library's automatic chain).  Applied through hpgq_debug_set_route: the
+# library itself reads no routing choice from the environment.
+DEFAULT_ROUTE = None
 
 
 def _ptr(a):
@@ -32,7 +37,7 @@ def device_batch(num_reads, seq_ptr, qual_ptr, idx_ptr):
 class Engine:
     """One hpgq_ctx: a HIP stream + device counters on `device`."""
 
-    def __init__(self, params, device=0):
+    def __init__(self, params, device=0, route=None):
         if not isinstance(params, Params):
             raise TypeError("params must be hpgfastq.Params")
         self.params = params
@@ -41,6 +46,14 @@ class Engine:
         h = C.c_void_p()
         check(lib.hpgq_open(C.byref(h), device, C.byref(params)), "hpgq_open")
         self._h = h
+        route = route if route is not None else DEFAULT_ROUTE
+        if route is not None and route != "auto":
+            self.set_route(route)
+
+    def set_route(self, route):
+        """hpgq_debug_set_route: 'auto', 'single' (catch-all alone), 'tri' /
+        'hex' / 'wide' first, 'auto_fixed' (no adaptive first stage)."""
+        check(lib.hpgq_debug_set_route(self._h, ROUTES[route]), "hpgq_debug_set_route")
 
     def close(self):
         if self._h:
@@ -119,6 +132,12 @@ class Engine:
     def allreduce(self):
         check(lib.hpgq_allreduce(self._h), "hpgq_allreduce")
 
+    def comm_count(self):
+        """Ranks in the ctx's RCCL communicator (ncclCommCount)."""
+        n = C.c_int(0)
+        check(lib.hpgq_comm_count(self._h, C.byref(n)), "hpgq_comm_count")
+        return n.value
+
     def process(self, seq, qual, idx, seq2=None, qual2=None, idx2=None):
         """Convenience: one host batch -> (mask, trim); counters accumulate."""
         n = len(idx) - 1
@@ -188,6 +207,11 @@ class ChaosGame:
         """u32 sum of every rank's tables and word count (hpgq_cgr_allreduce);
         tables() returns it until the next fill or reset."""
         check(lib.hpgq_cgr_allreduce(self._h), "hpgq_cgr_allreduce")
+
+    def comm_count(self):
+        n = C.c_int(0)
+        check(lib.hpgq_cgr_comm_count(self._h, C.byref(n)), "hpgq_cgr_comm_count")
+        return n.value
 
     def last_replays(self):
         return int(lib.hpgq_cgr_last_replays(self._h))

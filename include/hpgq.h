@@ -280,6 +280,29 @@ int  hpgq_comm_init(hpgq_ctx_t *ctx, int nranks, int rank, const char id[HPGQ_CO
 int  hpgq_allreduce(hpgq_ctx_t *ctx);
 /* device pointer of the all-reduced counters */
 uint64_t *hpgq_global_counters_device(hpgq_ctx_t *ctx);
+/* ranks in the ctx's communicator (ncclCommCount); HPGQ_E_STATE without one.
+ * The multi-GPU bench reports it next to its own world size
+ * (the old tool's --gpu-num-devices, old/main_hpg_fastq_old.c:113,161). */
+int  hpgq_comm_count(hpgq_ctx_t *ctx, int *count);
+
+/*
+ * Kernel routing for tests and A/B measurements only.  The
+ * library never reads routing choices from the environment: a ctx runs the
+ * automatic chain unless this is called.  It waits for the ctx stream and
+ * re-plans the chain; counters are kept.
+ *   AUTO        segmented kernel first (hex, or wide for lmax 157..252),
+ *               adaptive hex/wide first stage, catch-all for the rest
+ *   CATCH_ALL   the one-read-per-wave catch-all kernel alone
+ *   FIRST_TRI / FIRST_HEX / FIRST_WIDE   that geometry first (not adaptive)
+ * | NO_ADAPTIVE  (with AUTO) keep the first choice for every call
+ */
+#define HPGQ_ROUTE_AUTO        0
+#define HPGQ_ROUTE_CATCH_ALL   1
+#define HPGQ_ROUTE_FIRST_TRI   2
+#define HPGQ_ROUTE_FIRST_HEX   3
+#define HPGQ_ROUTE_FIRST_WIDE  4
+#define HPGQ_ROUTE_NO_ADAPTIVE 0x10
+int  hpgq_debug_set_route(hpgq_ctx_t *ctx, int route);
 
 /* ---------------------------------------------------------------------- */
 /* chaos-game (CGR) accumulator, old/chaos_game.c:165-267                 */
@@ -322,6 +345,8 @@ int64_t hpgq_cgr_last_replays(hpgq_cgr_t *cg);
  */
 int  hpgq_cgr_comm_init(hpgq_cgr_t *cg, int nranks, int rank, const char id[HPGQ_COMM_ID_BYTES]);
 int  hpgq_cgr_allreduce(hpgq_cgr_t *cg);
+/* ranks in the chaos-game communicator (ncclCommCount); HPGQ_E_STATE without one */
+int  hpgq_cgr_comm_count(hpgq_cgr_t *cg, int *count);
 /* device pointer of the all-reduced [table_seq | table_q | word_count] */
 uint32_t *hpgq_cgr_global_device(hpgq_cgr_t *cg);
 

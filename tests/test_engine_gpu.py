@@ -51,26 +51,16 @@ STATS_CASES = {
 def kernel_choice(request, monkeypatch):
     """Run a test with the default kernel chain (the segmented kernel in its
     16-byte-lane "hex" geometry first), with its 8-byte-lane "tri" or its
-    4-segment "wide" geometry forced first (HPGQ_TRI_GEO) and with the
-    one-read-per-wave catch-all alone (HPGQ_KERNEL=single), so every kernel
-    meets the oracle."""
-    monkeypatch.delenv("HPGQ_KERNEL", raising=False)
-    monkeypatch.delenv("HPGQ_TRI_GEO", raising=False)
-    if request.param == "single":
-        monkeypatch.setenv("HPGQ_KERNEL", "single")
-    elif request.param in ("tri", "wide"):
-        monkeypatch.setenv("HPGQ_TRI_GEO", request.param)
+    4-segment "wide" geometry forced first and with the one-read-per-wave
+    catch-all alone (hpgq_debug_set_route), so every kernel meets the oracle."""
+    monkeypatch.setattr(H.engine, "DEFAULT_ROUTE", request.param)
     return request.param
 
 
 @pytest.fixture(params=["auto", "tri", "wide"])
 def geo_choice(request, monkeypatch):
     """The segmented kernel's geometries as the first stage (edit runs on all)."""
-    monkeypatch.delenv("HPGQ_KERNEL", raising=False)
-    if request.param in ("tri", "wide"):
-        monkeypatch.setenv("HPGQ_TRI_GEO", request.param)
-    else:
-        monkeypatch.delenv("HPGQ_TRI_GEO", raising=False)
+    monkeypatch.setattr(H.engine, "DEFAULT_ROUTE", request.param)
     return request.param
 
 

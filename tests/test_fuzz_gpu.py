@@ -22,7 +22,7 @@ import oracle_lib as O
 pytestmark = pytest.mark.gpu
 
 NCASES = 192
-# first stage per case: the default chain, or forced (HPGQ_TRI_GEO / HPGQ_KERNEL=single)
+# first stage per case: the default chain, or forced (hpgq_debug_set_route)
 ROUTES = ["auto", "auto", "tri", "wide", "auto", "auto", "tri", "single"]
 LMAX = [64, 150, 156, 157, 160, 200, 250, 252, 300, 1024]
 BASE_LEN = [1, 20, 63, 100, 149, 150, 151, 156, 157, 160, 161, 200, 250, 252, 253, 300]
@@ -100,13 +100,8 @@ def _params(rng):
 
 @pytest.mark.parametrize("case", range(NCASES))
 def test_random_option_combination(case, monkeypatch):
-    monkeypatch.delenv("HPGQ_KERNEL", raising=False)
-    monkeypatch.delenv("HPGQ_TRI_GEO", raising=False)
     route = ROUTES[case % len(ROUTES)]
-    if route == "single":
-        monkeypatch.setenv("HPGQ_KERNEL", "single")
-    elif route != "auto":
-        monkeypatch.setenv("HPGQ_TRI_GEO", route)
+    monkeypatch.setattr(H.engine, "DEFAULT_ROUTE", route)   # hpgq_debug_set_route
     rng = np.random.default_rng(1000 + case)
     p, cmd, o = _params(rng)
     n = int(rng.integers(1, 6000))

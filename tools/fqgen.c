@@ -2,8 +2,13 @@
  * fqgen.c — synthetic FASTQ file for the end-to-end benchmark (tool, not product).
  * Same counter-based generator as bench.py / the oracle: seed,
  * read length L, 5 % truncated, 5 % bad, 'N' at 1/1024, phred33.
- *   gcc -O2 -fopenmp tools/fqgen.c -o /tmp/fqgen && /tmp/fqgen out.fq 20000000 150 2
+ *   gcc -O2 -fopenmp tools/fqgen.c -o /tmp/fqgen && /tmp/fqgen out.fq 20000000 150 2 [cpus]
+ * cpus: optional comma-separated CPU ids the generator pins itself to before
+ * its threads start (bench.py: the GPU's NUMA node, so the file's pages land
+ * there), instead of the parent pinning the child between fork and exec.
  */
+#define _GNU_SOURCE
+#include <sched.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -23,6 +28,17 @@ int main(int argc, char **argv) {
   const int64_t n = atoll(argv[2]);
   const int L0 = atoi(argv[3]);
   const uint64_t seed = strtoull(argv[4], 0, 10);
+  if (argc > 5 && argv[5][0]) {
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    for (char *t = argv[5]; *t;) {
+      const long c = strtol(t, &t, 10);
+      if (c >= 0 && c < CPU_SETSIZE) CPU_SET((int)c, &set);
+      if (*t == ',') ++t;
+      else if (*t) break;
+    }
+    if (CPU_COUNT(&set) && sched_setaffinity(0, sizeof(set), &set) != 0) perror("fqgen: sched_setaffinity");
+  }
   FILE *f = fopen(argv[1], "wb");
   if (!f) return 1;
   const int64_t block = 1 << 16;
