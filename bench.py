@@ -105,8 +105,8 @@ CONFIGS = {
     "dropin": dict(metric="Mreads/s (150 bp) stats+filter through hpgq_run_host, 10,000-read host batches",
                    unit="Mreads/s", reads=4_000_000, batch=10_000, L=150, seed=2,
                    workload="INTEGRATION.md's fastq_stats_worker: AoS reads packed per 10,000-read batch into the "
-                            "ctx's staging slot (hpgq_host_batch), hpgq_run_host + hpgq_sync, 2 worker threads with "
-                            "one ctx each (src/stats_options.c:21-22)"),
+                            "ctx's staging slot (hpgq_host_batch), hpgq_run_host without a mask, one hpgq_sync per "
+                            "worker at the end, 2 worker threads with one ctx each (src/stats_options.c:21-22)"),
     "c2_kmers": dict(metric="Mreads/s (150 bp) stats --kmers 5-mer counts (passed reads of C2)",
                      unit="Mreads/s", reads=50_000_000, batch=10_000_000, L=150, seed=2,
                      workload="stats --kmers on C2 reads: 5-mers of the reads that pass "
@@ -353,14 +353,18 @@ def numa_cpus(device):
     return cpus & os.sched_getaffinity(0)
 
 
-def e2e_leg(args, device, runs=5):
+def e2e_leg(args, device, runs=5, writer_runs=3):
     """`hpg-fastq stats --read-quality-range 20, --read-length-range 50,` on a
     synthetic FASTQ file in /dev/shm (tools/fqgen.c: the same generator,
     E2E_READS x 150 bp, written by threads on the GPU's NUMA node so the file's
-    pages sit there), one warm-up run and `runs` back-to-back CLI runs on this one GPU; the CLI's
-    own throughput line (text read -> parse -> engine, its clock starting after
+    pages sit there), one warm-up run and `runs` back-to-back CLI runs on this
+    one GPU; then the writing subcommands on the same file (`filter` with the
+    same flags -> passed.fq + failed.fq, `edit` with C4's trims -> edit.fq), their
+    outputs in /dev/shm too, `writer_runs` runs each.  The CLI's own throughput
+    line (text read -> parse -> engine -> outputs written, its clock starting after
     device set-up) per run.  PCIe-inclusive: NOT the bench value."""
     import re
+    import shutil
     import subprocess
     import tempfile
     cli = os.path.join(ROOT, "hpg-fastq_amd", "hpg-fastq")
@@ -370,40 +374,55 @@ def e2e_leg(args, device, runs=5):
     gen = os.path.join(tmp, "fqgen")
     shm = "/dev/shm" if os.path.isdir("/dev/shm") else tmp
     fq = os.path.join(shm, f"hpgq_e2e_{os.getpid()}.fq")
+    outd = os.path.join(shm, f"hpgq_e2e_out_{os.getpid()}")
     cpus = numa_cpus(device)
     share = sorted(cpus)[:omp_threads(len(cpus) or 16)] if cpus else None
-
+    nthr = str(len(share) if share else 16)
     out = {"reads": E2E_READS, "read_length": 150, "runs": runs,
            "command": "hpg-fastq stats -f <file> --read-quality-range 20, --read-length-range 50, "
-                      f"--gpus 1 --num-threads {len(share) if share else 16}",
+                      f"--gpus 1 --num-threads {nthr}",
            "numa_cpus": len(share) if share else None}
+    c2 = ["--read-quality-range", "20,", "--read-length-range", "50,"]
+    c4 = ["--left-length", "10", "--left-quality-range", "20,", "--right-length", "30",
+          "--right-quality-range", "20,"]
+
+    def cli_runs(cmd, flags, n, warm):
+        vals, gbs = [], []
+        for rep in range(n + (1 if warm else 0)):   # a warm-up run (GPU clocks, file pages): not counted
+            shutil.rmtree(outd, ignore_errors=True)
+            os.makedirs(outd)
+            r = subprocess.run([cli, cmd, "-f", fq, "-o", outd, *flags, "--gpus", "1", "--gpu", str(device),
+                                "--num-threads", nthr], check=True, capture_output=True, text=True, timeout=300)
+            m = re.search(r"Throughput: (\d+) reads, ([0-9.]+) GB of FastQ in ([0-9.]+) s = ([0-9.]+) Mreads/s",
+                          r.stdout)
+            if not m:
+                raise RuntimeError(f"{cmd}: no throughput line")
+            if warm and rep == 0:
+                continue
+            vals.append(float(m.group(4)))
+            gbs.append(float(m.group(2)) / float(m.group(3)))
+        return vals, gbs
     try:
         subprocess.run(["gcc", "-O2", "-fopenmp", os.path.join(ROOT, "tools", "fqgen.c"), "-o", gen],
                        check=True, capture_output=True, timeout=120)
         # fqgen pins itself to the GPU's NUMA CPUs (no preexec_fn: this process
         # may already run GPU runtime threads)
         subprocess.run([gen, fq, str(E2E_READS), "150", "2", ",".join(map(str, share or []))], check=True,
-                       capture_output=True, timeout=300,
-                       env=dict(os.environ, OMP_NUM_THREADS=str(len(share) if share else 16)))
+                       capture_output=True, timeout=300, env=dict(os.environ, OMP_NUM_THREADS=nthr))
         out["fastq_gb"] = round(os.path.getsize(fq) / 1e9, 3)
-        vals, gbs = [], []
-        for rep in range(runs + 1):   # run 0 warms the GPU clocks and the file's pages: not counted
-            r = subprocess.run([cli, "stats", "-f", fq, "-o", tmp, "--read-quality-range", "20,",
-                                "--read-length-range", "50,", "--gpus", "1", "--gpu", str(device),
-                                "--num-threads", str(len(share) if share else 16)],
-                               check=True, capture_output=True, text=True, timeout=300)
-            m = re.search(r"Throughput: (\d+) reads, ([0-9.]+) GB of FastQ in ([0-9.]+) s = ([0-9.]+) Mreads/s",
-                          r.stdout)
-            if not m:
-                return dict(out, error="no throughput line")
-            if rep == 0:
-                out["warmup_mreads_s"] = float(m.group(4))
-                continue
-            vals.append(float(m.group(4)))
-            gbs.append(float(m.group(2)) / float(m.group(3)))
+        vals, gbs = cli_runs("stats", c2, runs, True)
         out.update(mreads_s=round(float(np.median(vals)), 2), mreads_s_min=round(min(vals), 2),
                    mreads_s_runs=[round(v, 2) for v in vals], gb_s_fastq=round(float(np.median(gbs)), 2))
-    except (OSError, subprocess.SubprocessError) as e:
+        for cmd, flags in (("filter", c2), ("edit", c4)):
+            if writer_runs <= 0:
+                break
+            vals, gbs = cli_runs(cmd, flags, writer_runs, False)
+            out[cmd] = {"command": f"hpg-fastq {cmd} -f <file> -o /dev/shm/... {' '.join(flags)} --gpus 1 "
+                                   f"--num-threads {nthr}",
+                        "mreads_s": round(float(np.median(vals)), 2), "mreads_s_min": round(min(vals), 2),
+                        "mreads_s_runs": [round(v, 2) for v in vals],
+                        "gb_s_fastq": round(float(np.median(gbs)), 2)}
+    except (OSError, subprocess.SubprocessError, RuntimeError) as e:
         out["error"] = str(e)[:200]
     finally:
         for f in (fq, gen):
@@ -411,16 +430,20 @@ def e2e_leg(args, device, runs=5):
                 os.remove(f)
             except OSError:
                 pass
-        import shutil
+        shutil.rmtree(outd, ignore_errors=True)
         shutil.rmtree(tmp, ignore_errors=True)
     return out
 
 
 def dropin_main(args):
-    """--config dropin: INTEGRATION.md's worker (tools/dropin_bench.c) on 10,000-read
-    batches packed into the ctx's staging slot (hpgq_host_batch; and, beside it,
-    the malloc'd-batch worker), 2 worker threads with one ctx each, over a
-    synthetic FASTQ file (reads loaded as AoS before the clock starts)."""
+    """--config dropin: INTEGRATION.md's stats worker (tools/dropin_bench.c) on
+    10,000-read batches packed into the ctx's staging slot (hpgq_host_batch),
+    2 worker threads with one ctx each, over a synthetic FASTQ file (reads
+    loaded as AoS before the clock starts).  The value is the stats worker as
+    the stats consumer needs it: no mask, no per-batch hpgq_sync, one sync per
+    worker at the end (--no-sync).  Beside it: the worker that waits for each
+    batch's mask (filter-style, hpgq_sync per batch) and the malloc'd-batch
+    worker that hpgq_run_host copies."""
     import subprocess
     import tempfile
     harness = os.path.join(ROOT, "tools", "dropin_bench")
@@ -434,12 +457,13 @@ def dropin_main(args):
         subprocess.run([gen, fq, str(n), "150", "2"], check=True, capture_output=True, timeout=300)
         base = [harness, fq, "--threads", "2", "--batch", str(args.batch_reads), "--c2",
                 "--lmax", "1024", "--repeat", str(args.steps)]
-        # the worker packs into the ctx's staging slot (hpgq_host_batch); the
-        # malloc'd-batch worker (hpgq_run_host copies it) is reported beside it
-        r = subprocess.run(base, check=True, capture_output=True, text=True, timeout=600)
-        rec = json.loads(r.stdout.strip().splitlines()[-1])
-        r = subprocess.run(base + ["--copy"], check=True, capture_output=True, text=True, timeout=600)
-        rec_copy = json.loads(r.stdout.strip().splitlines()[-1])
+
+        def harness_run(extra):
+            r = subprocess.run(base + extra, check=True, capture_output=True, text=True, timeout=600)
+            return json.loads(r.stdout.strip().splitlines()[-1])
+        rec = harness_run(["--no-sync"])
+        rec_sync = harness_run([])
+        rec_copy = harness_run(["--copy"])
     finally:
         for f in (fq, gen):
             try:
@@ -453,10 +477,12 @@ def dropin_main(args):
            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
            "data": "synthetic FASTQ (tools/fqgen.c), host memory",
            "config": {"workload": cfg["workload"], "reads": rec["reads"], "batch_reads": rec["batch_reads"],
-                      "threads": rec["threads"], "lmax": 1024, "staging": rec["staging"]},
+                      "threads": rec["threads"], "lmax": 1024, "staging": rec["staging"], "sync": rec["sync"]},
            "harness": rec,
+           "sync_per_batch": {"mreads_s": rec_sync["mreads_s"], "mreads_s_mean": rec_sync["mreads_s_mean"],
+                              "note": "the worker waits for each batch's mask (hpgq_sync per batch)"},
            "copy_path": {"mreads_s": rec_copy["mreads_s"], "mreads_s_mean": rec_copy["mreads_s_mean"],
-                         "note": "worker packs into malloc'd buffers; hpgq_run_host copies them"}}
+                         "note": "worker packs into malloc'd buffers; hpgq_run_host copies them; sync per batch"}}
     print(json.dumps(out), flush=True)
 
 

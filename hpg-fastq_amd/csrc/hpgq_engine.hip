@@ -211,10 +211,11 @@ static size_t seg_lds(const hpgq_params_t &p, int nm, int xm, int pos) {
   const size_t mate_words = (size_t)6 * lp + ((hlen + 1) & ~(size_t)1) + 2 * HPGQ_NUM_SCALARS;
   // per mate [6][lmax] + hist + scalars, 16 B alignment, the byte-mask table,
   // per wave and mate two read tables (2 x 1 KB) + segment ends (+ one list per
-  // extra scan), per wave a compaction scratch and a deferral word
+  // extra scan) + the per-lane mean-quality sums, per wave a compaction scratch
+  // and a deferral word
   const size_t lists = 1 + ((xm & hpgq::X_NOOR) ? 1 : 0) + ((xm & hpgq::X_LR) ? 1 : 0);
   return (size_t)nm * mate_words * 4 + 16 + 17 * 16 +
-         (size_t)hpgq::kWaves * ((size_t)nm * (2 * 256 + 64 * lists) + 64 + 4) * 4;
+         (size_t)hpgq::kWaves * ((size_t)nm * (2 * 256 + 64 * lists + hpgq::kFxWords) + 64 + 4) * 4;
 }
 
 static size_t catch_all_lds(const hpgq_params_t &p, int nm) {

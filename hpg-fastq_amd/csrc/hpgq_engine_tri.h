@@ -48,6 +48,28 @@ namespace hpgq {
 
 constexpr int kTriSlack = 8;    // readable bytes past the data end the loads may touch
 
+// The unit epilogue reads each read's length and trim word back from the read
+// table (LDS) instead of holding them in VGPRs across the unit's steps (4 per
+// mate: current and next unit), which the paired-end edit kernel spilled.
+#ifndef HPGQ_TAB_LEN
+#define HPGQ_TAB_LEN 1
+#endif
+// Paired-end edit, usual windows: both mates' trim loads in flight at once
+// (1), or one mate's loads issued and finished before the other's (0: no
+// TrimLoads of two mates live together).
+#ifndef HPGQ_PE_TRIM_OVERLAP
+#define HPGQ_PE_TRIM_OVERLAP 1
+#endif
+// The exact mean-quality sum (u64 per lane and mate) accumulates in per-lane
+// LDS slots (one no-return ds_add_u64 per unit) instead of a VGPR pair held
+// across the loop: the paired-end edit kernel spilled exactly those pairs,
+// a scratch load + store per unit and mate (~200 MB of scratch writes per
+// 10 M pairs).
+#ifndef HPGQ_FX_LDS
+#define HPGQ_FX_LDS 1
+#endif
+constexpr int kFxWords = HPGQ_FX_LDS ? 128 : 0;   // per wave and mate: 64 u64
+
 constexpr int GEO_TRI = 0, GEO_HEX = 1, GEO_WIDE = 2;
 constexpr int X_NOOR = 1, X_LR = 2;   // extra filter scans (engine_tri_x_kernel)
 
@@ -328,6 +350,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   // fails few reads and ran 4 % slower with it: 692 vs 665 us per 10 M reads)
   constexpr bool PF = NM == 1 && !EDIT && !FOLLOW && XM != X_LR;
   constexpr bool LATE = EDIT;   // the unit prologue's place (see the unit loop)
+  constexpr bool TABLEN = HPGQ_TAB_LEN && !FOLLOW;   // epilogue lengths / trims from the read table
   // PEU (paired-end): a group is ONE step of both mates (grp[slot][m]); both
   // are added, the pair is decided from both scans at once (ds_bpermute), and
   // a failed pair is taken back out of the nibble counters from the registers
@@ -403,7 +426,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     return reinterpret_cast<unsigned long long *>(base + m * mate_words + 6 * lp + hist_words);
   };
   constexpr int kMateWaveWords = 2 * 256 + 64 * (1 + (NX ? 1 : 0) + (LR ? 1 : 0));
-  constexpr int kWaveWords = NM * kMateWaveWords + 64 + 4;   // (multiple of 4: 16 B tables)
+  constexpr int kWaveWords = NM * kMateWaveWords + 64 + 4 + NM * kFxWords;   // (multiple of 4: 16 B tables)
   const int tab_words = (NM * mate_words + 3) & ~3;   // 16 B aligned (host: + 16 B)
   uint32_t *wtab = base + tab_words + wave * kWaveWords;
   auto tab = [&](int m, int tb) __attribute__((always_inline)) { return wtab + m * kMateWaveWords + tb * 256; };
@@ -414,6 +437,14 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   };
   uint32_t *scratch = wtab + NM * kMateWaveWords;
   unsigned long long *dword = reinterpret_cast<unsigned long long *>(scratch + 64);   // 8 B aligned
+  // per-lane exact mean-quality sums (HPGQ_FX_LDS), 8 B aligned
+  auto fxs = [&](int m) __attribute__((always_inline)) {
+    return reinterpret_cast<unsigned long long *>(scratch + 64 + 4 + m * kFxWords);
+  };
+  if (HPGQ_FX_LDS) {
+#pragma unroll
+    for (int m = 0; m < NM; ++m) fxs(m)[lane] = 0ull;
+  }
   // byte masks by valid-byte count c = clamp(n - p0, 0, 4 NW): mtab[c][w]
   // (one LDS read per step instead of a clamp and a 64-bit shift per word)
   uint32_t *mtab = base + tab_words + kWaves * kWaveWords;   // 16 B aligned
@@ -499,7 +530,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     // per mate; single-end keeps trim_word, whose registers fit better)
     TrimLoads tl[NM];
     const ColdParams &cold = cold_all;
-    const bool usual = EDIT && NM == 2 && trim_usual(cold);
+    const bool usual = HPGQ_PE_TRIM_OVERLAP && EDIT && NM == 2 && trim_usual(cold);
     if (usual) {
 #pragma unroll
       for (int m = 0; m < NM; ++m)
@@ -519,8 +550,10 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       const uint32_t n = live ? (uint32_t)(e - a) : 0u;
       const uint32_t xs = live ? (uint32_t)(bs[m] + a) : 0x80000000u;
       const uint32_t xq = live ? (uint32_t)(bq[m] + a) : 0x80000000u;
-      // (FOLLOW: the read id rides in the record's spare dword, for the epilogue)
-      const v4u rec = v4u{xs & ~3u, xq & ~3u, n | ((xs & 3u) << 16) | ((xq & 3u) << 20), rid};
+      // (FOLLOW: the read id rides in the record's spare dword, for the
+      // epilogue; else the trim word, when the epilogue reads it back)
+      const uint32_t spare = FOLLOW || !HPGQ_TAB_LEN ? rid : tw[m];
+      const v4u rec = v4u{xs & ~3u, xq & ~3u, n | ((xs & 3u) << 16) | ((xq & 3u) << 20), spare};
       *reinterpret_cast<v4u *>(tab(m, tb) + 4 * lane) = rec;
       len[m] = n;
     }
@@ -895,6 +928,14 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     const bool inb = lane < nr;
     const bool valid = inb && !((dm >> lane) & 1ull);
     const int my_read = FOLLOW ? (int)tab(0, tb)[4 * lane + 3] : cur.u * ublock + lane;
+    if (TABLEN) {   // this unit's lengths and trim words from its read table
+#pragma unroll
+      for (int m = 0; m < NM; ++m) {
+        const v2u r = *reinterpret_cast<const v2u *>(tab(m, tb) + 4 * lane + 2);
+        len[m] = r.x & 0xFFFFu;
+        tw[m] = EDIT ? r.y : 0u;
+      }
+    }
     __builtin_amdgcn_wave_barrier();
     uint32_t r1[NM];
     bool pass = valid;
@@ -948,7 +989,8 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
             meanq_terms(s, wn, bin, fx);
             atomicAdd(&h[lp + 1 + bin], 1u);
             atomicAdd(&h[lp + 1 + HPGQ_MEANQ_BINS + (100 * gc) / wn], 1u);
-            fx16[m] += fx;
+            if (HPGQ_FX_LDS) atomicAdd(&fxs(m)[lane], (unsigned long long)fx);   // (no return: ds_add_u64)
+            else fx16[m] += fx;
           }
         }
       }
@@ -987,10 +1029,12 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
         }
       }
     }
+    if (!TABLEN) {
 #pragma unroll
-    for (int m = 0; m < NM; ++m) {
-      len[m] = lenn[m];
-      tw[m] = twn[m];
+      for (int m = 0; m < NM; ++m) {
+        len[m] = lenn[m];
+        tw[m] = twn[m];
+      }
     }
     dm = dmn;
     tb ^= 1;
@@ -1004,7 +1048,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   for (int m = 0; m < NM; ++m) {
     acc[m].widen();
     acc[m].flush(pos_acc(m), lp, p0);
-    const uint64_t tot = wave_sum64(fx16[m]);
+    const uint64_t tot = wave_sum64(HPGQ_FX_LDS ? (uint64_t)fxs(m)[lane] : fx16[m]);   // (LDS: in order per wave)
     if (lane == 0) {
       unsigned long long *s = sc(m);
       if (cnt[m][0]) atomicAdd(&s[HPGQ_S_NUM_INPUT], (unsigned long long)cnt[m][0]);

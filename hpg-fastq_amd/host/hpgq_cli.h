@@ -53,6 +53,7 @@ typedef struct {
   char *kmers_out;          /* raw u64 k-mer table dump (tests) */
   char *cg_out;             /* raw u32 chaos-game tables dump (tests) */
   int quiet;
+  int stream_writer;        /* filter / edit: one writer thread instead of mapped outputs */
 } cli_options_t;
 
 /* parse + validate (exits with the reference's messages on errors) */

@@ -102,6 +102,9 @@ static void usage(const cli_options_t *o) {
     printf("  --kmers-out=<file>              Write the raw u64 k-mer table [1024][lmax-4]\n");
   if (o->command == CMD_STATS)
     printf("  --cg-out=<file>                 Write the raw u32 chaos-game tables + word count\n");
+  if (o->command != CMD_STATS)
+    printf("  --stream-writer                 Write the FastQ outputs through one writer thread\n"
+           "                                  (default: mapped output files filled in parallel)\n");
   printf("  --quiet                         No parameter / result display\n");
   exit(-1);
 }
@@ -114,7 +117,7 @@ static int exists(const char *path) {
 enum {
   O_THREADS = 1000, O_BATCH, O_QENC, O_KMERS, O_LRANGE, O_QRANGE, O_LLEN, O_LQRANGE, O_RLEN,
   O_RQRANGE, O_MAXN, O_MAXOOQ, O_GPU, O_LMAX, O_CHUNK, O_PRINT, O_COUNTERS, O_QUIET,
-  O_KMERSOUT, O_CG, O_KCG, O_GS, O_GPUS, O_CGBATCH, O_CGOUT, O_GPUW
+  O_KMERSOUT, O_CG, O_KCG, O_GS, O_GPUS, O_CGBATCH, O_CGOUT, O_GPUW, O_STREAMW
 };
 
 cli_options_t *cli_parse(int command, const char *exec_name, int argc, char **argv) {
@@ -166,6 +169,7 @@ cli_options_t *cli_parse(int command, const char *exec_name, int argc, char **ar
       {"counters-out", required_argument, 0, O_COUNTERS},
       {"kmers-out", required_argument, 0, O_KMERSOUT},
       {"quiet", no_argument, 0, O_QUIET},
+      {"stream-writer", no_argument, 0, O_STREAMW},
       {0, 0, 0, 0}};
   if (argc < 2) usage(o);
   optind = 1;
@@ -207,6 +211,7 @@ cli_options_t *cli_parse(int command, const char *exec_name, int argc, char **ar
       case O_KMERSOUT: o->kmers_out = strdup(optarg); break;
       case O_CGOUT: o->cg_out = strdup(optarg); break;
       case O_QUIET: o->quiet = 1; break;
+      case O_STREAMW: o->stream_writer = 1; break;
       default: usage(o);
     }
   }

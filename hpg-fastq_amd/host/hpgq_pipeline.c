@@ -24,10 +24,19 @@
  *              state starts afresh, old/chaos_game.c:180-181) do not depend on
  *              --chunk-mb or --gpus; the reader then cuts every chunk at a
  *              batch end.
- *   writer     (filter / edit) passed.fq / failed.fq / edit.fq in input
+ *   outputs    (filter / edit) passed.fq / failed.fq / edit.fq in input
  *              order: filter copies whole input records; edit writes the
  *              header and '+' lines as read and the trimmed sequence /
- *              quality.
+ *              quality.  Regular output files are mapped shared, sized to the
+ *              bound (each output is at most the input), and every chunk is
+ *              placed in input order from its per-class byte counts and then
+ *              copied into the maps by its worker's copy threads in parallel
+ *              (one writer thread through write() capped filter at 18 and edit
+ *              at 15-17 Mreads/s: a tmpfs or page-cache file takes one write()
+ *              at a time, page stores from many threads at once); the files
+ *              are truncated to their final sizes at the end.  Otherwise
+ *              (--stream-writer, or a map that fails) one writer thread
+ *              writes the chunks in order.
  * Stats never leave the device until the end (hpgq_read_counters).
  */
 #define _GNU_SOURCE
@@ -38,6 +47,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <sys/uio.h>
 #include <time.h>
@@ -83,6 +93,12 @@ typedef struct {
   int64_t chunks;
   FILE *out_pass, *out_fail;
   uint64_t written_pass, written_fail;
+  /* mapped outputs: [0] passed / edit.fq, [1] failed.fq (NULL: not written) */
+  int mmap_out;
+  char *map[2];
+  size_t map_cap;
+  uint64_t out_off[2];   /* bytes placed so far per output */
+  int64_t placed;        /* chunks placed (in input order) */
   int64_t cg_batch;   /* --cg: bytes of FASTQ text per chaos-game call (0: off) */
   /* HPGQ_TRACE=1: per chunk (the first TRACE_MAX) the reader's and the worker's
    * start / end times, printed to stderr at the end (diagnostics only) */
@@ -478,6 +494,180 @@ static int ensure_results(slot_t *s, int64_t n) {
              : -1;
 }
 
+/* ---- mapped outputs: placement in input order, parallel copy -------------- */
+
+/* output class of record i (0: passed / edit.fq, 1: failed.fq) and its output
+ * bytes: the whole input record (filter) or the trimmed one (edit) */
+static inline int rec_class(const pipe_t *P, const slot_t *s, int64_t i) {
+  return s->mask[i] != 0 || !P->o->filter_on ? 0 : 1;
+}
+
+static inline uint64_t rec_out_bytes(const pipe_t *P, const slot_t *s, int64_t i) {
+  if (P->o->command != CMD_EDIT) {
+    const uint32_t ee = i + 1 < s->nreads ? s->rec_start[i + 1] : (uint32_t)s->use;
+    return ee - s->rec_start[i];
+  }
+  const uint32_t ts = s->trim[i] & 0xFFFFu, te = s->trim[i] >> 16;
+  const uint32_t keep = (uint32_t)(s->idx[i + 1] - s->idx[i]) - ts - te;
+  return (uint64_t)(s->seq_start[i] - s->rec_start[i]) + (s->qual_start[i] - s->plus_start[i]) + 2u * keep + 2u;
+}
+
+#define MAX_COPIERS 64
+typedef struct {
+  pipe_t *P;
+  slot_t *s;
+  int64_t i0, i1;      /* records of this part */
+  uint64_t bytes[2];   /* its output bytes per class */
+  char *dst[2];        /* where its records go */
+  pthread_t th;
+  int started;
+} copy_part_t;
+
+/* records [i0, i1) into the maps at dst[class] */
+static void copy_records(pipe_t *P, slot_t *s, int64_t i0, int64_t i1, char *dst[2]) {
+  const int edit = P->o->command == CMD_EDIT;
+  for (int64_t i = i0; i < i1; ++i) {
+    const int c = rec_class(P, s, i);
+    if (!P->map[c]) continue;
+    if (!edit) {   /* a run of same-class records is one contiguous span */
+      int64_t j = i + 1;
+      while (j < i1 && rec_class(P, s, j) == c) ++j;
+      const uint32_t a = s->rec_start[i];
+      const uint32_t ee = j < s->nreads ? s->rec_start[j] : (uint32_t)s->use;
+      memcpy(dst[c], s->buf + a, ee - a);
+      dst[c] += ee - a;
+      i = j - 1;
+      continue;
+    }
+    const uint32_t a = s->rec_start[i];
+    const uint32_t ts = s->trim[i] & 0xFFFFu, te = s->trim[i] >> 16;
+    const uint32_t keep = (uint32_t)(s->idx[i + 1] - s->idx[i]) - ts - te;
+    const uint32_t hl = s->seq_start[i] - a, pl = s->qual_start[i] - s->plus_start[i];
+    char *o = dst[c];
+    memcpy(o, s->buf + a, hl);                              /* header line */
+    o += hl;
+    memcpy(o, s->buf + s->seq_start[i] + ts, keep);
+    o += keep;
+    *o++ = '\n';
+    memcpy(o, s->buf + s->plus_start[i], pl);                /* '+' line */
+    o += pl;
+    memcpy(o, s->buf + s->qual_start[i] + ts, keep);
+    o += keep;
+    *o++ = '\n';
+    dst[c] = o;
+  }
+}
+
+static void *size_part(void *arg) {
+  copy_part_t *cp = arg;
+  cp->bytes[0] = cp->bytes[1] = 0;
+  for (int64_t i = cp->i0; i < cp->i1; ++i) cp->bytes[rec_class(cp->P, cp->s, i)] += rec_out_bytes(cp->P, cp->s, i);
+  return NULL;
+}
+
+static void *copy_part(void *arg) {
+  copy_part_t *cp = arg;
+  copy_records(cp->P, cp->s, cp->i0, cp->i1, cp->dst);
+  return NULL;
+}
+
+/* fn over the parts: part 0 on this thread, the others on threads of their own
+ * (a part whose thread cannot start runs here too) */
+static void run_parts(void *(*fn)(void *), copy_part_t *part, int n) {
+  for (int t = 1; t < n; ++t) part[t].started = pthread_create(&part[t].th, NULL, fn, &part[t]) == 0;
+  fn(&part[0]);
+  for (int t = 1; t < n; ++t) {
+    if (part[t].started) pthread_join(part[t].th, NULL);
+    else fn(&part[t]);
+  }
+}
+
+/* a processed chunk into the mapped outputs: size its records per class (in
+ * parallel), place it after chunk k-1 (which only needs k-1's sizes, not its
+ * copies), copy its records at those offsets (in parallel) */
+static int place_and_copy(pipe_t *P, slot_t *s) {
+  static __thread copy_part_t part[MAX_COPIERS];
+  int n = P->o->num_threads;
+  const int64_t per_min = 16384;   /* records per copier at least */
+  if (n > MAX_COPIERS) n = MAX_COPIERS;
+  if ((int64_t)n > s->nreads / per_min + 1) n = (int)(s->nreads / per_min + 1);
+  if (n < 1) n = 1;
+  const int64_t per = (s->nreads + n - 1) / n;
+  for (int t = 0; t < n; ++t) {
+    copy_part_t *cp = &part[t];
+    cp->P = P;
+    cp->s = s;
+    cp->i0 = (int64_t)t * per < s->nreads ? (int64_t)t * per : s->nreads;
+    cp->i1 = cp->i0 + per < s->nreads ? cp->i0 + per : s->nreads;
+  }
+  run_parts(size_part, part, n);
+  uint64_t sz[2] = {0, 0}, base[2] = {0, 0}, npass = 0, nfail = 0;
+  for (int t = 0; t < n; ++t) {
+    sz[0] += part[t].bytes[0];
+    sz[1] += part[t].bytes[1];
+  }
+  int rc = 0;
+  pthread_mutex_lock(&P->mu);
+  while (P->placed != s->chunk && !P->error) pthread_cond_wait(&P->cv, &P->mu);
+  if (P->error) {
+    rc = -1;
+  } else if (P->out_off[0] + sz[0] > P->map_cap || P->out_off[1] + sz[1] > P->map_cap) {
+    rc = HPGQ_E_IO;   /* (cannot happen: each output is at most the input) */
+  } else {
+    for (int c = 0; c < 2; ++c) {
+      base[c] = P->out_off[c];
+      P->out_off[c] += sz[c];
+    }
+    P->placed++;
+  }
+  pthread_cond_broadcast(&P->cv);
+  pthread_mutex_unlock(&P->mu);
+  if (rc) return rc;
+  for (int t = 0; t < n; ++t) {
+    for (int c = 0; c < 2; ++c) {
+      part[t].dst[c] = P->map[c] ? P->map[c] + base[c] : NULL;
+      base[c] += part[t].bytes[c];
+    }
+  }
+  run_parts(copy_part, part, n);
+  for (int64_t i = 0; i < s->nreads; ++i) {
+    if (rec_class(P, s, i)) ++nfail;
+    else ++npass;
+  }
+  pthread_mutex_lock(&P->mu);
+  P->written_pass += npass;
+  P->written_fail += nfail;
+  pthread_mutex_unlock(&P->mu);
+  return 0;
+}
+
+/* map the outputs for the parallel writer: each is at most the input (+ the
+ * final newline the reader may add); 0 when mapped, else the stream writer runs */
+static int map_outputs(pipe_t *P) {
+  FILE *f[2] = {P->out_pass, P->out_fail};
+  P->map_cap = (size_t)P->size + 4096;
+  for (int c = 0; c < 2; ++c) {
+    if (!f[c]) continue;
+    const int fd = fileno(f[c]);
+    struct stat st;
+    if (fstat(fd, &st) || !S_ISREG(st.st_mode) || ftruncate(fd, (off_t)P->map_cap)) return -1;
+    void *m = mmap(NULL, P->map_cap, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    if (m == MAP_FAILED) return -1;
+    P->map[c] = m;
+  }
+  P->mmap_out = 1;
+  return 0;
+}
+
+static void unmap_outputs(pipe_t *P, int *rc) {
+  FILE *f[2] = {P->out_pass, P->out_fail};
+  for (int c = 0; c < 2; ++c) {
+    if (P->map[c]) munmap(P->map[c], P->map_cap);
+    P->map[c] = NULL;
+    if (f[c] && P->mmap_out && ftruncate(fileno(f[c]), (off_t)P->out_off[c]) && *rc == 0) *rc = HPGQ_E_IO;
+  }
+}
+
 /* one GPU worker: its own ctx, parser, k-mer and CGR accumulators on one device */
 typedef struct {
   pipe_t *P;
@@ -555,7 +745,7 @@ static int worker_chunk(worker_t *W, slot_t *s) {
   }
   trace_at(W->P, s->chunk, 3, -1);
   if (rc == 0) rc = hpgq_sync(W->ctx);
-  if (rc == 0 && edit) rc = assemble_edit(W->P, s);
+  if (rc == 0 && edit && !W->P->mmap_out) rc = assemble_edit(W->P, s);
   if (rc == 0 && W->cg) {   /* after the parse and the mask; settled before the next parse reuses b */
     rc = hpgq_cgr_fill_device(W->cg, &b, o->filter_on ? W->d_mask : NULL,
                               o->filter_on ? HPGQ_CGR_ONLY_VALID_READS : HPGQ_CGR_ALL_READS);
@@ -579,12 +769,15 @@ static void *worker_main(void *arg) {
     pthread_mutex_unlock(&P->mu);
     if (stop) break;
     trace_at(P, k, 2, W->w);
-    const int rc = worker_chunk(W, s);
+    int rc = worker_chunk(W, s);
+    if (rc == 0 && writes && P->mmap_out) {
+      rc = place_and_copy(P, s);   /* (an empty chunk is placed too: input order) */
+    }
     trace_at(P, k, 4, -1);
     W->fastq_bytes += (double)s->use;
     pthread_mutex_lock(&P->mu);
     if (rc && !P->error) P->error = rc;
-    s->state = writes && rc == 0 ? 2 : 0;
+    s->state = writes && rc == 0 && !P->mmap_out ? 2 : 0;
     pthread_cond_broadcast(&P->cv);
     pthread_mutex_unlock(&P->mu);
     if (rc) {
@@ -662,6 +855,14 @@ int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, 
     if (!P.out_pass || ((!edit || o->filter_on) && !P.out_fail)) rc = HPGQ_E_INVALID;
     if (P.out_pass) setvbuf(P.out_pass, NULL, _IOFBF, 16 << 20);
     if (P.out_fail) setvbuf(P.out_fail, NULL, _IOFBF, 16 << 20);
+    if (rc == 0 && !o->stream_writer && map_outputs(&P)) {   /* not mappable: the writer thread */
+      for (int c = 0; c < 2; ++c)
+        if (P.map[c]) munmap(P.map[c], P.map_cap);
+      P.map[0] = P.map[1] = NULL;
+      P.mmap_out = 0;
+      if (P.out_pass && ftruncate(fileno(P.out_pass), 0)) rc = HPGQ_E_IO;
+      if (P.out_fail && ftruncate(fileno(P.out_fail), 0)) rc = HPGQ_E_IO;
+    }
   }
   if (rc) goto done;
 
@@ -669,7 +870,8 @@ int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, 
   P.t0 = t0;
   pthread_t reader, writer;
   pthread_create(&reader, NULL, reader_main, &P);
-  if (writes) pthread_create(&writer, NULL, writer_main, &P);
+  const int writer_thread = writes && !P.mmap_out;
+  if (writer_thread) pthread_create(&writer, NULL, writer_main, &P);
   for (int w = 0; w < G; ++w) pthread_create(&W[w].th, NULL, worker_main, &W[w]);
   for (int w = 0; w < G; ++w) pthread_join(W[w].th, NULL);
   /* (a worker that stopped on an error left P.error set: reader and writer end) */
@@ -677,7 +879,7 @@ int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, 
   pthread_cond_broadcast(&P.cv);
   pthread_mutex_unlock(&P.mu);
   pthread_join(reader, NULL);
-  if (writes) pthread_join(writer, NULL);
+  if (writer_thread) pthread_join(writer, NULL);
   for (int w = 0; w < G && rc == 0; ++w) rc = W[w].rc;
   if (rc == 0 && P.error) rc = P.error < 0 && P.error != HPGQ_E_FORMAT ? HPGQ_E_INVALID : P.error;
 
@@ -726,6 +928,7 @@ int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, 
     free(ts);
     free(tq);
   }
+  if (P.mmap_out) unmap_outputs(&P, &rc);   /* the files at their final sizes (inside the clock) */
   res->seconds = now_s() - t0;
   res->num_gpus = G;
   for (int64_t k = 0; P.trace && k < P.chunks && k < TRACE_MAX; ++k)
@@ -738,6 +941,7 @@ int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, 
   }
 
 done:
+  if (P.mmap_out) unmap_outputs(&P, &rc);
   if (P.out_pass) fclose(P.out_pass);
   if (P.out_fail) fclose(P.out_fail);
   for (int i = 0; i < P.nslots; ++i) {

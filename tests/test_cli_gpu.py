@@ -78,12 +78,18 @@ def test_cli_report_golden(tmp_path, case):
         assert filecmp.cmp(os.path.join(want_dir, name), tmp_path / name, shallow=False), name
 
 
+WRITERS = {"mmap": [], "stream": ["--stream-writer"]}
+
+
+@pytest.mark.parametrize("writer", sorted(WRITERS))
 @pytest.mark.parametrize("crlf", [False, True])
-def test_cli_filter_outputs(tmp_path, crlf):
+def test_cli_filter_outputs(tmp_path, crlf, writer):
+    """passed.fq / failed.fq byte for byte, with the mapped parallel writer
+    (default) and the one-thread stream writer."""
     reads = O.synth(15000, seed=22, L=150)
     fq = _write(tmp_path, reads, crlf=crlf)
     run_cli(["filter", "-f", fq, "-o", tmp_path, "--read-quality-range", "20,",
-             "--read-length-range", "50,", "--max-N", "1", "--chunk-mb", 1, "--quiet"])
+             "--read-length-range", "50,", "--max-N", "1", "--chunk-mb", 1, "--quiet", *WRITERS[writer]])
     p = H.filter_params(lmax=1024, read_quality_range="20,", read_length_range="50,", max_N=1)
     mask, _, _ = O.run(p, reads)
     recs = [h + sq + nl + plus + q + nl for (h, sq, plus, q, nl) in _records(reads, crlf)]
@@ -93,12 +99,13 @@ def test_cli_filter_outputs(tmp_path, crlf):
     assert (tmp_path / "failed.fq").read_bytes() == failed
 
 
-def test_cli_edit_outputs(tmp_path):
+@pytest.mark.parametrize("writer", sorted(WRITERS))
+def test_cli_edit_outputs(tmp_path, writer):
     reads = O.synth(12000, seed=24, L=150)
     fq = _write(tmp_path, reads)
     run_cli(["edit", "-f", fq, "-o", tmp_path, "--left-length", 10, "--left-quality-range", "20,",
              "--right-length", 30, "--right-quality-range", "20,", "--read-length-range", "60,",
-             "--chunk-mb", 1, "--quiet"])
+             "--chunk-mb", 1, "--quiet", *WRITERS[writer]])
     p = H.edit_params(lmax=1024, left_length=10, left_quality_range="20,", right_length=30,
                       right_quality_range="20,", read_length_range="60,")
     mask, trim, _ = O.run(p, reads)
@@ -109,6 +116,47 @@ def test_cli_edit_outputs(tmp_path):
         (ok if m else bad).append(rec)
     assert (tmp_path / "edit.fq").read_bytes() == b"".join(ok)
     assert (tmp_path / "failed.fq").read_bytes() == b"".join(bad)
+
+
+@pytest.mark.parametrize("writer", sorted(WRITERS))
+@pytest.mark.parametrize("case", ["empty", "all_fail", "all_pass", "no_final_newline"])
+def test_cli_writer_edges(tmp_path, case, writer):
+    """Output files at the edges: an empty input, every read failing (empty
+    passed.fq), every read passing (empty failed.fq), a file whose last line
+    lacks its newline (the reader adds it); edit the same way."""
+    reads = O.synth(3000, seed=31, L=150)
+    text, _ = to_fastq(reads)
+    if case == "empty":
+        text = b""
+    elif case == "no_final_newline":
+        text = text[:-1]
+    fq = tmp_path / "in.fq"
+    fq.write_bytes(text)
+    q = {"all_fail": "60,", "all_pass": "0,"}.get(case, "20,")
+    for cmd in ("filter", "edit"):
+        d = tmp_path / cmd
+        d.mkdir()
+        extra = ["--left-length", 10, "--left-quality-range", "20,"] if cmd == "edit" else []
+        run_cli([cmd, "-f", fq, "-o", d, "--read-quality-range", q, "--chunk-mb", 1, "--quiet", *extra,
+                 *WRITERS[writer]])
+        if cmd == "filter":
+            p = H.filter_params(lmax=1024, read_quality_range=q)
+        else:
+            p = H.edit_params(lmax=1024, left_length=10, left_quality_range="20,", read_quality_range=q)
+        mask, trim, _ = O.run(p, reads) if case != "empty" else (np.zeros(0), np.zeros(0), None)
+        ok, bad = [], []
+        for (h, sq, plus, qq, nl), m, t in zip(_records(reads) if case != "empty" else [], mask, trim):
+            ts, te = (int(t) & 0xFFFF, int(t) >> 16) if cmd == "edit" else (0, 0)
+            rec = h + sq[ts:len(sq) - te] + nl + plus + qq[ts:len(qq) - te] + nl
+            (ok if m else bad).append(rec)
+        # (to_fastq writes the same records as _records; the reader restores a
+        # missing final newline)
+        assert (d / ("passed.fq" if cmd == "filter" else "edit.fq")).read_bytes() == b"".join(ok)
+        assert (d / "failed.fq").read_bytes() == b"".join(bad)
+        if case == "all_fail":
+            assert not ok
+        if case == "all_pass":
+            assert not bad
 
 
 def test_cli_kat_stats(tmp_path):
@@ -290,7 +338,7 @@ def test_cli_workers_merge(tmp_path, cmd):
         np.testing.assert_array_equal(np.fromfile(b / "ctr.bin", np.uint64), want)
 
 
-@pytest.mark.parametrize("cmd", ["stats", "filter", "edit"])
+@pytest.mark.parametrize("cmd", ["stats", "filter", "edit", "filter_stream", "edit_stream"])
 def test_cli_threads_under_tsan(tmp_path, cmd):
     """The threaded host pipeline (reader threads, 2 GPU x 2 worker threads,
     writer; hpg-fastq_amd/host/hpgq_pipeline.c) built with ThreadSanitizer
@@ -302,6 +350,7 @@ def test_cli_threads_under_tsan(tmp_path, cmd):
     reads = O.synth(20000, seed=29, L=150, n_per_1024=6)
     fq = _write(tmp_path, reads)
     outs = []
+    cmd, _, mode = cmd.partition("_")
     for exe in (CLI, tsan):
         d = tmp_path / os.path.basename(exe)
         d.mkdir()
@@ -310,6 +359,8 @@ def test_cli_threads_under_tsan(tmp_path, cmd):
                 "--read-length-range", "50,"]
         if cmd == "edit":
             args += ["--left-length", 10, "--left-quality-range", "20,"]
+        if mode == "stream":
+            args += ["--stream-writer"]
         supp = os.path.join(os.path.dirname(os.path.abspath(__file__)), "sanitize", "tsan.supp")
         env = dict(os.environ, TSAN_OPTIONS=f"halt_on_error=1:second_deadlock_stack=1:suppressions={supp}")
         # (TSan's shadow layout needs the address-space randomisation off:

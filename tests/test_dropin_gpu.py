@@ -1,7 +1,8 @@
 """The drop-in binding as INTEGRATION.md writes it (tools/dropin_bench.c):
 SoA batches of the reference's 10,000 reads (src/stats_options.c:22), packed
 into the ctx's staging slot (hpgq_host_batch) or into malloc'd buffers,
-packed from AoS reads, hpgq_run_host + hpgq_sync per batch, one ctx per worker
+packed from AoS reads, hpgq_run_host + hpgq_sync per batch (or, for the stats
+worker that needs no mask, one hpgq_sync per worker at the end), one ctx per worker
 thread (src/stats_options.c:21: 2 threads) -- the summed counters and every
 mask equal the oracle's over the same FASTQ file.  Also the host path's
 contract: several hpgq_run_host calls in flight before one hpgq_sync."""
@@ -32,23 +33,30 @@ def fastq(tmp_path_factory):
     return path
 
 
-@pytest.mark.parametrize("threads,batch,copy", [(2, 10000, False), (1, 997, False), (3, 4096, False),
-                                               (2, 10000, True), (3, 4096, True)])
-def test_dropin_worker_matches_oracle(fastq, tmp_path, threads, batch, copy):
+@pytest.mark.parametrize("threads,batch,copy,nosync", [
+    (2, 10000, False, False), (1, 997, False, False), (3, 4096, False, False),
+    (2, 10000, True, False), (3, 4096, True, False),
+    (2, 10000, False, True), (1, 997, False, True), (3, 4096, True, True)])
+def test_dropin_worker_matches_oracle(fastq, tmp_path, threads, batch, copy, nosync):
     """copy=False: the worker packs into the ctx's staging slot (hpgq_host_batch);
-    copy=True: into malloc'd buffers that hpgq_run_host copies."""
+    copy=True: into malloc'd buffers that hpgq_run_host copies.  nosync: the
+    stats worker without a mask or a per-batch hpgq_sync (one sync per worker
+    at the end; bench --config dropin's value) -- counters only."""
     assert os.path.exists(HARNESS), "build with make -C hpg-fastq_amd"
     ctr, msk = str(tmp_path / "ctr.bin"), str(tmp_path / "mask.bin")
     out = subprocess.run([HARNESS, fastq, "--batch", str(batch), "--threads", str(threads), "--c2",
-                          "--counters", ctr, "--mask", msk, "--repeat", "2"] + (["--copy"] if copy else []),
+                          "--counters", ctr, "--repeat", "2"] + (["--mask", msk] if not nosync else [])
+                         + (["--copy"] if copy else []) + (["--no-sync"] if nosync else []),
                          check=True, capture_output=True, text=True, timeout=300)
     rec = json.loads(out.stdout.strip().splitlines()[-1])
     assert rec["staging"] == ("copy" if copy else "in_place")
+    assert rec["sync"] == ("once per worker at the end" if nosync else "per batch")
     reads = read_fastq(fastq)
     assert rec["reads"] == reads.n
     p = H.stats_params(lmax=1024, read_quality_range="20,", read_length_range="50,")
     m_o, _t, c_o = O.run(p, reads)
-    np.testing.assert_array_equal(np.fromfile(msk, np.uint8), m_o)
+    if not nosync:
+        np.testing.assert_array_equal(np.fromfile(msk, np.uint8), m_o)
     np.testing.assert_array_equal(np.fromfile(ctr, np.uint64), c_o)
 
 

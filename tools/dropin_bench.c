@@ -14,12 +14,17 @@
  *             fastq_stats_worker of INTEGRATION.md (src/stats_fastq.c:202-250);
  *             the SoA buffers are the ctx's staging slot (hpgq_host_batch),
  *             or with --copy malloc'd ones that hpgq_run_host copies.
+ *             --no-sync: the stats worker as the stats consumer needs it -- no
+ *             mask (the engine merges the passed reads itself), so no
+ *             hpgq_sync per batch: hpgq_host_batch waits for the slot's
+ *             previous batch (two in flight per ctx), and each worker syncs
+ *             its ctx once after its last batch (inside the clock).
  *   consumer  nothing per read; the ctxs' counters are summed at the end.
  * Prints one JSON line.  --counters F / --mask F write the summed u64 counter
  * set and the per-read masks (input order) for tests/test_dropin_gpu.py.
  *
  *   dropin_bench in.fq [--batch 10000] [--threads 2] [--lmax 1024] [--c2] [--copy]
- *                      [--counters F] [--mask F] [--repeat R]
+ *                      [--no-sync] [--counters F] [--mask F] [--repeat R]
  * --c2: the C2 filter (--read-quality-range 20, --read-length-range 50,).
  */
 #define _GNU_SOURCE
@@ -104,7 +109,8 @@ typedef struct {
   hpgq_ctx_t *ctx;
 } worker_t;
 
-static int g_copy;   /* --copy: the malloc'd-batch worker (hpgq_run_host copies it) */
+static int g_copy;     /* --copy: the malloc'd-batch worker (hpgq_run_host copies it) */
+static int g_nosync;   /* --no-sync: no mask, one hpgq_sync per worker at the end */
 
 /* INTEGRATION.md fastq_stats_worker, once per batch: the reads are packed
  * straight into the ctx's staging slot (hpgq_host_batch), or with --copy into
@@ -139,14 +145,14 @@ static void *worker(void *arg) {
         memcpy(qual + idx[i], bt->reads[i].quality, len);
       }
     }
-    uint8_t *mask = malloc(n);
+    uint8_t *mask = g_nosync ? NULL : malloc(n);
     if (rc == HPGQ_OK) rc = hpgq_run_host(w->ctx, &b, NULL, mask, NULL);
-    if (rc == HPGQ_OK) rc = hpgq_sync(w->ctx);   /* mask valid, buffers reusable */
+    if (rc == HPGQ_OK && !g_nosync) rc = hpgq_sync(w->ctx);   /* mask valid, buffers reusable */
     if (rc != HPGQ_OK) {
       fprintf(stderr, "hpgq: %s\n", hpgq_strerror(rc));
       g_fail = 1;
     }
-    if (g_mask) memcpy(g_mask + bt->first, mask, n);
+    if (g_mask && mask) memcpy(g_mask + bt->first, mask, n);
     free(mask);
     if (g_copy) {
       free(seq);
@@ -154,13 +160,20 @@ static void *worker(void *arg) {
     }
     free(idx);
   }
+  if (g_nosync) {   /* the workflow's end: this worker's batches are done */
+    const int rc = hpgq_sync(w->ctx);
+    if (rc != HPGQ_OK) {
+      fprintf(stderr, "hpgq: %s\n", hpgq_strerror(rc));
+      g_fail = 1;
+    }
+  }
   return NULL;
 }
 
 int main(int argc, char **argv) {
   if (argc < 2) {
     fprintf(stderr, "usage: dropin_bench in.fq [--batch N] [--threads T] [--lmax L] [--c2] [--copy] "
-                    "[--counters F] [--mask F] [--repeat R]\n");
+                    "[--no-sync] [--counters F] [--mask F] [--repeat R]\n");
     return 2;
   }
   size_t batch = 10000;
@@ -173,6 +186,7 @@ int main(int argc, char **argv) {
     else if (!strcmp(argv[i], "--repeat") && i + 1 < argc) repeat = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--c2")) c2 = 1;
     else if (!strcmp(argv[i], "--copy")) g_copy = 1;
+    else if (!strcmp(argv[i], "--no-sync")) g_nosync = 1;
     else if (!strcmp(argv[i], "--counters") && i + 1 < argc) ctr_path = argv[++i];
     else if (!strcmp(argv[i], "--mask") && i + 1 < argc) mask_path = argv[++i];
     else {
@@ -181,6 +195,10 @@ int main(int argc, char **argv) {
     }
   }
   if (batch < 1 || threads < 1 || repeat < 1) return 2;
+  if (g_nosync && mask_path) {
+    fprintf(stderr, "--no-sync takes no mask (the stats consumer needs none)\n");
+    return 2;
+  }
   const double t_load = now();
   if (load(argv[1], batch)) {
     fprintf(stderr, "cannot read %s\n", argv[1]);
@@ -242,10 +260,11 @@ int main(int argc, char **argv) {
   }
   printf("{\"reads\": %zu, \"batches\": %zu, \"batch_reads\": %zu, \"threads\": %d, \"gpus\": %d, "
          "\"repeat\": %d, \"best_s\": %.6f, \"mean_s\": %.6f, \"mreads_s\": %.3f, \"mreads_s_mean\": %.3f, "
-         "\"load_s\": %.3f, \"num_input\": %llu, \"num_passed\": %llu, \"staging\": \"%s\"}\n",
+         "\"load_s\": %.3f, \"num_input\": %llu, \"num_passed\": %llu, \"staging\": \"%s\", "
+         "\"sync\": \"%s\"}\n",
          g_total, g_nbatches, batch, threads, threads < ndev ? threads : ndev, repeat, best, sum / repeat,
          g_total / best / 1e6, g_total / (sum / repeat) / 1e6, load_s,
          (unsigned long long)tot[HPGQ_S_NUM_INPUT], (unsigned long long)tot[HPGQ_S_NUM_PASSED],
-         g_copy ? "copy" : "in_place");
+         g_copy ? "copy" : "in_place", g_nosync ? "once per worker at the end" : "per batch");
   return 0;
 }
