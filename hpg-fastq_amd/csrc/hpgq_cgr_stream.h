@@ -69,6 +69,16 @@
 // for only when its bound would decide.
 #pragma once
 
+// Timing-only ablations of the per-byte loop (tools/gpu_c5_ablation_r04.sh;
+// the tables they leave are wrong, never built into the product):
+//   1: no table add (a VALU xor into a register instead of the ds_add_u64)
+//   2: the quality window chain replaced by a constant
+//   3: no emission mask (every byte adds to its word's cell)
+//   4: a 32-bit ds_add_u32 of the count only
+#ifndef HPGQ_C5_ABLATION
+#define HPGQ_C5_ABLATION 0
+#endif
+
 namespace hpgq {
 namespace cgr {
 namespace stream {
@@ -474,6 +484,7 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
   const int32_t ns = (int32_t)nspans(a0, b1);
   const int32_t gw = (int32_t)blockIdx.x * kWaves + wid, nwav = (int32_t)gridDim.x * kWaves;
   bool risky = false;
+  uint32_t abl_sink = 0;   // (HPGQ_C5_ABLATION 1)
 
   // one descriptor pair per call: offsets past b1 + slack read zeros without
   // memory traffic (the context loads of tiles that enter no span, the
@@ -668,15 +679,24 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
                                      : c.p1 >> (sh - 64);
         const uint32_t w = win & M;   // M: the cell byte-address mask
         const int jo = j - K;   // the byte leaving the quality window
-        const uint32_t qold = jo >= 0 ? __builtin_amdgcn_ubfe(qw[jo >> 2], 8 * (jo & 3), 8)
-                                      : __builtin_amdgcn_ubfe(jo + kLaneBytes < kLaneBytes - 4 ? nq6 : nq7, 8 * (jo & 3), 8);
-        acc = acc + __builtin_amdgcn_ubfe(qw[j >> 2], 8 * (j & 3), 8) - qold;
+        if (HPGQ_C5_ABLATION == 2) {
+          acc = 0x55u;
+        } else {
+          const uint32_t qold = jo >= 0 ? __builtin_amdgcn_ubfe(qw[jo >> 2], 8 * (jo & 3), 8)
+                                        : __builtin_amdgcn_ubfe(jo + kLaneBytes < kLaneBytes - 4 ? nq6 : nq7, 8 * (jo & 3), 8);
+          acc = acc + __builtin_amdgcn_ubfe(qw[j >> 2], 8 * (j & 3), 8) - qold;
+        }
         // addr = E bit j ? w : spare (v_bfe_i32 + v_bitop3; left to itself the
         // compiler spends three instructions on it)
         const uint32_t e = (uint32_t)__builtin_amdgcn_sbfe((int)E, j, 1);
-        const uint32_t addr = __builtin_amdgcn_bitop3_b32(e, w, spare, 0xCA);   // e ? w : spare
+        const uint32_t addr = HPGQ_C5_ABLATION == 3 ? w : __builtin_amdgcn_bitop3_b32(e, w, spare, 0xCA);   // e ? w : spare
         const unsigned long long inc = ((unsigned long long)acc << 32) | 1ull;
-        atomicAdd(reinterpret_cast<unsigned long long *>(reinterpret_cast<char *>(tab) + addr), inc);
+        if (HPGQ_C5_ABLATION == 1)
+          abl_sink ^= addr + (uint32_t)(inc >> 32);
+        else if (HPGQ_C5_ABLATION == 4)
+          atomicAdd(reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(tab) + addr), 1u);
+        else
+          atomicAdd(reinterpret_cast<unsigned long long *>(reinterpret_cast<char *>(tab) + addr), inc);
       }
       // carry the last lane to the next tile's lane 0
       // (rotated by one lane: lane 0 holds lane 63's, the "old" operand of
@@ -763,6 +783,7 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
     }
   }
   if (__ballot(risky) && lane == 0) atomicOr(A.gate, GATE_EXACT);
+  if (HPGQ_C5_ABLATION == 1 && abl_sink == 0x9E3779B9u) tab[lane] = 1ull;   // (keeps the sink live)
   __syncthreads();
   for (int i = threadIdx.x; i < cells; i += kWG) {
     const unsigned long long v = tab[i];

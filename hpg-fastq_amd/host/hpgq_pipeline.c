@@ -104,7 +104,9 @@ typedef struct {
    * start / end times, printed to stderr at the end (diagnostics only) */
   int trace;
   double t0;
-  double tr[TRACE_MAX][5];   /* read start, read end, worker start, sync start, worker end */
+  /* read start, read end, worker start, sync start, worker end, parsed,
+   * synced, placed */
+  double tr[TRACE_MAX][8];
   int tw[TRACE_MAX];
 } pipe_t;
 
@@ -623,6 +625,7 @@ static int place_and_copy(pipe_t *P, slot_t *s) {
   pthread_cond_broadcast(&P->cv);
   pthread_mutex_unlock(&P->mu);
   if (rc) return rc;
+  trace_at(P, s->chunk, 7, -1);
   for (int t = 0; t < n; ++t) {
     for (int c = 0; c < 2; ++c) {
       part[t].dst[c] = P->map[c] ? P->map[c] + base[c] : NULL;
@@ -718,6 +721,7 @@ static int worker_chunk(worker_t *W, slot_t *s) {
   const int need_mask = writes || ((W->km || W->cg) && o->filter_on);
   hpgq_batch_t b;
   int rc = hpgq_parse_host(W->ps, s->buf, (int64_t)s->use, &b);
+  trace_at(W->P, s->chunk, 5, -1);
   if (rc || b.num_reads == 0) {
     s->nreads = 0;
     return rc;
@@ -745,6 +749,7 @@ static int worker_chunk(worker_t *W, slot_t *s) {
   }
   trace_at(W->P, s->chunk, 3, -1);
   if (rc == 0) rc = hpgq_sync(W->ctx);
+  trace_at(W->P, s->chunk, 6, -1);
   if (rc == 0 && edit && !W->P->mmap_out) rc = assemble_edit(W->P, s);
   if (rc == 0 && W->cg) {   /* after the parse and the mask; settled before the next parse reuses b */
     rc = hpgq_cgr_fill_device(W->cg, &b, o->filter_on ? W->d_mask : NULL,
@@ -932,8 +937,10 @@ int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, 
   res->seconds = now_s() - t0;
   res->num_gpus = G;
   for (int64_t k = 0; P.trace && k < P.chunks && k < TRACE_MAX; ++k)
-    fprintf(stderr, "trace chunk %lld: read %.1f-%.1f ms, worker %d %.1f-%.1f (sync from %.1f) ms\n", (long long)k,
-            1e3 * P.tr[k][0], 1e3 * P.tr[k][1], P.tw[k], 1e3 * P.tr[k][2], 1e3 * P.tr[k][4], 1e3 * P.tr[k][3]);
+    fprintf(stderr,
+            "trace chunk %lld: read %.1f-%.1f ms, worker %d %.1f-%.1f (parsed %.1f, sync %.1f-%.1f, placed %.1f) ms\n",
+            (long long)k, 1e3 * P.tr[k][0], 1e3 * P.tr[k][1], P.tw[k], 1e3 * P.tr[k][2], 1e3 * P.tr[k][4],
+            1e3 * P.tr[k][5], 1e3 * P.tr[k][3], 1e3 * P.tr[k][6], 1e3 * P.tr[k][7]);
   if (rc == 0) {
     res->num_passed = counters[HPGQ_S_NUM_PASSED];
     res->num_failed = counters[HPGQ_S_NUM_FAILED];
