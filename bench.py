@@ -628,6 +628,7 @@ def dry_run_rank(args, world, rank):
     _load_hpgfastq()
     cfg = CONFIGS[args.config]
     if world > 1:
+        os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
         dist.init_process_group("gloo", rank=rank, world_size=world)
     lo, hi = shard(args, rank)
     n = min(1000, args.reads)
@@ -682,6 +683,8 @@ def main():
         sys.exit(2)
     local_dev = local % max(ndev, 1)
     if world > 1:   # rank control on gloo; the data path's exchange is libhpgq's RCCL
+        # one node: gloo on loopback (the container hostname may not resolve)
+        os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
         dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)

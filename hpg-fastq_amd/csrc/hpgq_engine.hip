@@ -483,6 +483,13 @@ void hpgq_close(hpgq_ctx_t *c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  // outputs of host-path calls not yet delivered (no hpgq_sync since) are
+  // dropped, never written: the caller may already have freed those arrays
+  for (auto &sl : c->slot) {
+    sl.mask_dst = nullptr;
+    sl.trim_dst = nullptr;
+    sl.busy = false;
+  }
   if (c->comm) ncclCommDestroy(c->comm);
   (void)hipFree(c->d_state);
   (void)hipFree(c->d_global);
@@ -849,6 +856,12 @@ int hpgq_read_counters(hpgq_ctx_t *c, uint64_t *out, size_t n) {
   HPGQ_HIP_TRY(hipMemcpyAsync(out, c->reduced ? c->d_global : c->d_state, c->clen * c->nm * sizeof(uint64_t),
                               hipMemcpyDeviceToHost, c->stream));
   HPGQ_HIP_TRY(hipStreamSynchronize(c->stream));
+  // the stream has run every queued batch: their masks / trims reach the
+  // caller's arrays here too, as in hpgq_sync
+  for (int k = 0; k < 2; ++k) {
+    hpgq_ctx::Slot &sl = c->slot[c->cur_slot ^ 1 ^ k];
+    if (sl.busy) slot_deliver(sl);
+  }
   return HPGQ_OK;
 }
 

@@ -212,8 +212,12 @@ int  hpgq_run_device(hpgq_ctx_t *ctx, const hpgq_batch_t *b, const hpgq_batch_t 
  * each piece's H2D queued as soon as it is copied) and the call returns once
  * the caller's buffers have been read: they are reusable on return.  The
  * copies run on a second stream, so this batch's H2D overlaps the previous
- * batch's kernels.  mask_out / trim_out are filled by hpgq_sync() (or when the
- * slot is reused two calls later), not before.
+ * batch's kernels.  mask_out / trim_out are filled by hpgq_sync() or
+ * hpgq_read_counters() (or when the slot is reused two calls later), not
+ * before: synchronising hpgq_stream() yourself does not fill them, and the
+ * arrays must stay allocated until one of those calls.  hpgq_close() drops
+ * the outputs of calls not delivered by then (it never writes them).
+ * A stats-only caller passes NULL for both and needs no hpgq_sync per batch.
  */
 int  hpgq_run_host(hpgq_ctx_t *ctx, const hpgq_batch_t *b, const hpgq_batch_t *b2,
                    uint8_t *mask_out, uint32_t *trim_out);
@@ -248,7 +252,8 @@ int  hpgq_reset(hpgq_ctx_t *ctx);
 /* Number of uint64 in this ctx's counter buffer (1 or 2 sets). */
 size_t hpgq_counters_size(const hpgq_ctx_t *ctx);
 
-/* Copy the counters to host memory (synchronises the ctx). */
+/* Copy the counters to host memory (synchronises the ctx; like hpgq_sync it
+ * also delivers pending hpgq_run_host masks / trims). */
 int  hpgq_read_counters(hpgq_ctx_t *ctx, uint64_t *out, size_t n);
 
 /* DEPRECATED no-op, kept only so that round-1 callers still link: the kernels
@@ -261,7 +266,8 @@ int  hpgq_fold(hpgq_ctx_t *ctx);
  * all-reduce); holds the totals once the ctx stream has run the batches. */
 uint64_t *hpgq_counters_device(hpgq_ctx_t *ctx);
 
-/* HIP stream (hipStream_t) the ctx runs on. */
+/* HIP stream (hipStream_t) the ctx runs on.  Synchronising it waits for the
+ * kernels but does not deliver hpgq_run_host outputs (hpgq_sync does). */
 void *hpgq_stream(hpgq_ctx_t *ctx);
 
 /* ---------------------------------------------------------------------- */
