@@ -122,3 +122,15 @@ def test_host_batch_keeps_its_arrays_alive():
     gc.collect()
     idx = (C.c_int32 * 3).from_address(b.data_indices)
     assert list(idx) == [2, 5, 8] and b.num_reads == 2
+
+
+def test_library_reads_no_environment():
+    """libhpgq takes no routing or tuning choice from the environment (VERDICT
+    r3: HPGQ_KERNEL / HPGQ_TRI_GEO / HPGQ_ADAPTIVE moved to
+    hpgq_debug_set_route): no getenv anywhere in its sources."""
+    import glob
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    srcs = glob.glob(os.path.join(root, "hpg-fastq_amd", "csrc", "*"))
+    assert srcs
+    for f in srcs:
+        assert "getenv" not in open(f, errors="replace").read(), f

@@ -127,3 +127,27 @@ def test_host_batch_in_place(paired, edit):
             np.testing.assert_array_equal(t, t_o)
         want += c_o
     np.testing.assert_array_equal(got, want)
+
+
+def test_read_counters_delivers_host_outputs():
+    """hpgq_read_counters synchronises the ctx and, like hpgq_sync, hands the
+    pending host-path masks / trims to the caller's arrays; a ctx
+    closed with outputs pending drops them (never writes them)."""
+    p = H.edit_params(lmax=150, stats=True, left_length=10, left_quality_range="20,",
+                      right_length=30, right_quality_range="20,", read_quality_range="20,")
+    reads = [O.synth(5000, seed=90 + i, L=150, trunc_pct=10, first=7000 * i) for i in range(2)]
+    masks = [np.full(r.n, 7, np.uint8) for r in reads]
+    trims = [np.zeros(r.n, np.uint32) for r in reads]
+    with H.Engine(p) as e:
+        for r, m, t in zip(reads, masks, trims):
+            e.run_host(H.engine.host_batch(r.seq, r.qual, r.idx), None, m, t)
+        got = e.counters()          # no hpgq_sync before it
+        for r, m, t in zip(reads, masks, trims):
+            m_o, t_o, _ = O.run(p, r)
+            np.testing.assert_array_equal(m, m_o)
+            np.testing.assert_array_equal(t, t_o)
+        want = sum(O.run(p, r)[2] for r in reads)
+        np.testing.assert_array_equal(got, want)
+        pending = np.full(reads[0].n, 7, np.uint8)
+        e.run_host(H.engine.host_batch(reads[0].seq, reads[0].qual, reads[0].idx), None, pending, None)
+    assert (pending == 7).all()     # dropped by hpgq_close: untouched

@@ -600,3 +600,35 @@ def test_adaptive_first_stage_switches_and_stays_exact():
             np.testing.assert_array_equal(m_g, m_o)
             want += c_o
         np.testing.assert_array_equal(e.counters(), want)
+
+
+def test_debug_set_route_on_a_live_ctx():
+    """hpgq_debug_set_route re-plans a ctx between batches: the counters keep
+    accumulating, every route meets the oracle and the first stage's kernel
+    name follows the route; the library itself reads no routing environment."""
+    import os
+    os.environ["HPGQ_KERNEL"] = "single"       # (rounds <= 3 read these; now ignored)
+    os.environ["HPGQ_TRI_GEO"] = "tri"
+    try:
+        p = H.stats_params(lmax=150, read_quality_range="20,", read_length_range="50,")
+        parts = [O.synth(6000, seed=300 + i, L=150, trunc_pct=10, first=9000 * i) for i in range(4)]
+        names = []
+        with H.Engine(p) as e:
+            names.append(e.kernel_name)
+            for r, route in zip(parts, ["auto", "single", "tri", "wide"]):
+                e.set_route(route)
+                names.append(e.kernel_name)
+                m, _ = e.process(r.seq, r.qual, r.idx)
+                np.testing.assert_array_equal(m, O.run(p, r)[0])
+            got = e.counters()
+        np.testing.assert_array_equal(got, sum(O.run(p, r)[2] for r in parts))
+        assert "hex" in names[0] and "hex" in names[1]   # the environment changed nothing
+        assert names[2].startswith("hpgq::engine_kernel<")
+        assert ", tri" in names[3] and ", wide" in names[4]
+        assert H.lib.hpgq_debug_set_route(None, 0) == -1   # HPGQ_E_INVALID
+        with H.Engine(p) as e2:
+            assert H.lib.hpgq_debug_set_route(e2._h, 99) == -1
+            assert "hex" in e2.kernel_name
+    finally:
+        del os.environ["HPGQ_KERNEL"]
+        del os.environ["HPGQ_TRI_GEO"]
