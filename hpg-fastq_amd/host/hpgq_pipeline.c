@@ -472,28 +472,32 @@ static int assemble_edit(pipe_t *P, slot_t *s) {
   return 0;
 }
 
+/* the per-chunk results come back by DMA: page-locked buffers (pageable
+ * destinations are staged through the runtime's bounce buffer, synchronously) */
+static void free_results(slot_t *s) {
+  void **b[7] = {(void **)&s->mask, (void **)&s->trim, (void **)&s->rec_start, (void **)&s->seq_start,
+                 (void **)&s->plus_start, (void **)&s->qual_start, (void **)&s->idx};
+  for (int i = 0; i < 7; ++i) {
+    hpgq_host_free(*b[i]);
+    *b[i] = NULL;
+  }
+  s->res_cap = 0;
+}
+
 static int ensure_results(slot_t *s, int64_t n) {
   if ((size_t)n <= s->res_cap) return 0;
-  free(s->mask);
-  free(s->trim);
-  free(s->rec_start);
-  free(s->seq_start);
-  free(s->plus_start);
-  free(s->qual_start);
-  free(s->idx);
+  free_results(s);
   const size_t c = (size_t)n + (size_t)n / 4 + 1024;
-  s->mask = malloc(c);
-  s->trim = malloc(c * 4);
-  s->rec_start = malloc(c * 4);
-  s->seq_start = malloc(c * 4);
-  s->plus_start = malloc(c * 4);
-  s->qual_start = malloc(c * 4);
-  s->idx = malloc((c + 1) * 4);
+  void **b[7] = {(void **)&s->mask, (void **)&s->trim, (void **)&s->rec_start, (void **)&s->seq_start,
+                 (void **)&s->plus_start, (void **)&s->qual_start, (void **)&s->idx};
+  const size_t sz[7] = {c, c * 4, c * 4, c * 4, c * 4, c * 4, (c + 1) * 4};
+  for (int i = 0; i < 7; ++i)
+    if (hpgq_host_alloc(b[i], sz[i])) {
+      free_results(s);
+      return -1;
+    }
   s->res_cap = c;
-  return s->mask && s->trim && s->rec_start && s->seq_start && s->plus_start && s->qual_start &&
-                 s->idx
-             ? 0
-             : -1;
+  return 0;
 }
 
 /* ---- mapped outputs: placement in input order, parallel copy -------------- */
@@ -953,15 +957,9 @@ done:
   if (P.out_fail) fclose(P.out_fail);
   for (int i = 0; i < P.nslots; ++i) {
     hpgq_host_free(P.slot[i].buf);
-    free(P.slot[i].mask);
-    free(P.slot[i].trim);
-    free(P.slot[i].rec_start);
-    free(P.slot[i].seq_start);
-    free(P.slot[i].plus_start);
-    free(P.slot[i].qual_start);
+    free_results(&P.slot[i]);
     free(P.slot[i].out[0]);
     free(P.slot[i].out[1]);
-    free(P.slot[i].idx);
   }
   free(P.carry);
   for (int w = 0; w < G; ++w) worker_close(&W[w]);
