@@ -99,6 +99,8 @@ int main(int argc, char **argv) {
         printf("\tNum. failed reads : %lu (%s/failed.fq)\n", (unsigned long)r.num_failed, o->out_dirname);
       }
     }
+    if (r.writer)
+      printf("Output writer     : %s\n", r.writer == 1 ? "mapped files, parallel copy" : "one stream writer thread");
     printf("\nThroughput: %lu reads, %.3f GB of FastQ in %.3f s = %.2f Mreads/s (%d GPU worker%s)\n",
            (unsigned long)r.num_reads, r.fastq_bytes / 1e9, r.seconds,
            r.seconds > 0 ? r.num_reads / r.seconds / 1e6 : 0.0, r.num_gpus, r.num_gpus == 1 ? "" : "s");

@@ -76,6 +76,7 @@ typedef struct {
   uint32_t cg_words;        /* fq_word_count */
   int cg_exact_calls;       /* chaos-game calls the exact simulation redid */
   int num_gpus;             /* GPU worker threads that ran */
+  int writer;               /* filter / edit outputs: 1 mapped files (parallel copy), 2 stream writer */
 } cli_result_t;
 
 int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, cli_result_t *res);

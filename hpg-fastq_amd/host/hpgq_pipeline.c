@@ -855,23 +855,33 @@ int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, 
   const int edit = o->command == CMD_EDIT;
   if (rc == 0 && writes) {
     char path[4096];
+    /* "w+": read + write, which a shared writable mapping needs (an O_WRONLY
+     * descriptor cannot be mapped) */
     snprintf(path, sizeof(path), "%s/%s.fq", o->out_dirname, edit ? "edit" : "passed");
-    P.out_pass = fopen(path, "w");
+    P.out_pass = fopen(path, "w+");
     if (!edit || o->filter_on) {
       snprintf(path, sizeof(path), "%s/failed.fq", o->out_dirname);
-      P.out_fail = fopen(path, "w");
+      P.out_fail = fopen(path, "w+");
     }
     if (!P.out_pass || ((!edit || o->filter_on) && !P.out_fail)) rc = HPGQ_E_INVALID;
     if (P.out_pass) setvbuf(P.out_pass, NULL, _IOFBF, 16 << 20);
     if (P.out_fail) setvbuf(P.out_fail, NULL, _IOFBF, 16 << 20);
     if (rc == 0 && !o->stream_writer && map_outputs(&P)) {   /* not mappable: the writer thread */
-      for (int c = 0; c < 2; ++c)
+      FILE *f[2] = {P.out_pass, P.out_fail};
+      for (int c = 0; c < 2; ++c) {
         if (P.map[c]) munmap(P.map[c], P.map_cap);
+        struct stat fs;
+        /* (a regular file map_outputs may have extended: back to empty) */
+        if (f[c] && fstat(fileno(f[c]), &fs) == 0 && S_ISREG(fs.st_mode) && ftruncate(fileno(f[c]), 0))
+          rc = HPGQ_E_IO;
+      }
       P.map[0] = P.map[1] = NULL;
       P.mmap_out = 0;
-      if (P.out_pass && ftruncate(fileno(P.out_pass), 0)) rc = HPGQ_E_IO;
-      if (P.out_fail && ftruncate(fileno(P.out_fail), 0)) rc = HPGQ_E_IO;
     }
+    res->writer = P.mmap_out ? 1 : 2;
+    if (P.trace)
+      fprintf(stderr, "hpg-fastq: writer: %s\n", P.mmap_out ? "mapped output files, parallel copy"
+                                                            : "one stream writer thread");
   }
   if (rc) goto done;
 

@@ -6,9 +6,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CLI = os.path.join(ROOT, "hpg-fastq_amd", "hpg-fastq")
 
 
-def run_cli(args, check=True, timeout=300):
+def run_cli(args, check=True, timeout=300, env=None):
     r = subprocess.run([CLI] + [str(a) for a in args], capture_output=True, text=True,
-                       timeout=timeout)
+                       timeout=timeout, env=None if env is None else dict(os.environ, **env))
     if check and r.returncode != 0:
         raise AssertionError(f"hpg-fastq {args} -> {r.returncode}\n{r.stdout}\n{r.stderr}")
     return r

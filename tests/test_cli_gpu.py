@@ -79,6 +79,15 @@ def test_cli_report_golden(tmp_path, case):
 
 
 WRITERS = {"mmap": [], "stream": ["--stream-writer"]}
+WRITER_LINE = {"mmap": "writer: mapped output files, parallel copy", "stream": "writer: one stream writer thread"}
+
+
+def run_writer(args, writer):
+    """run_cli with the writer choice; asserts the pipeline used that writer
+    (HPGQ_TRACE=1 prints it: a failed mapping falls back to the stream writer)"""
+    r = run_cli(list(args) + WRITERS[writer], env={"HPGQ_TRACE": "1"})
+    assert WRITER_LINE[writer] in r.stderr, r.stderr[-2000:]
+    return r
 
 
 @pytest.mark.parametrize("writer", sorted(WRITERS))
@@ -88,8 +97,8 @@ def test_cli_filter_outputs(tmp_path, crlf, writer):
     (default) and the one-thread stream writer."""
     reads = O.synth(15000, seed=22, L=150)
     fq = _write(tmp_path, reads, crlf=crlf)
-    run_cli(["filter", "-f", fq, "-o", tmp_path, "--read-quality-range", "20,",
-             "--read-length-range", "50,", "--max-N", "1", "--chunk-mb", 1, "--quiet", *WRITERS[writer]])
+    run_writer(["filter", "-f", fq, "-o", tmp_path, "--read-quality-range", "20,",
+                "--read-length-range", "50,", "--max-N", "1", "--chunk-mb", 1, "--quiet"], writer)
     p = H.filter_params(lmax=1024, read_quality_range="20,", read_length_range="50,", max_N=1)
     mask, _, _ = O.run(p, reads)
     recs = [h + sq + nl + plus + q + nl for (h, sq, plus, q, nl) in _records(reads, crlf)]
@@ -103,9 +112,9 @@ def test_cli_filter_outputs(tmp_path, crlf, writer):
 def test_cli_edit_outputs(tmp_path, writer):
     reads = O.synth(12000, seed=24, L=150)
     fq = _write(tmp_path, reads)
-    run_cli(["edit", "-f", fq, "-o", tmp_path, "--left-length", 10, "--left-quality-range", "20,",
-             "--right-length", 30, "--right-quality-range", "20,", "--read-length-range", "60,",
-             "--chunk-mb", 1, "--quiet", *WRITERS[writer]])
+    run_writer(["edit", "-f", fq, "-o", tmp_path, "--left-length", 10, "--left-quality-range", "20,",
+                "--right-length", 30, "--right-quality-range", "20,", "--read-length-range", "60,",
+                "--chunk-mb", 1, "--quiet"], writer)
     p = H.edit_params(lmax=1024, left_length=10, left_quality_range="20,", right_length=30,
                       right_quality_range="20,", read_length_range="60,")
     mask, trim, _ = O.run(p, reads)
@@ -116,6 +125,20 @@ def test_cli_edit_outputs(tmp_path, writer):
         (ok if m else bad).append(rec)
     assert (tmp_path / "edit.fq").read_bytes() == b"".join(ok)
     assert (tmp_path / "failed.fq").read_bytes() == b"".join(bad)
+
+
+def test_cli_writer_to_devices(tmp_path):
+    """Outputs that cannot be mapped (here: symlinks to /dev/null) take the
+    stream writer, and the run succeeds."""
+    reads = O.synth(3000, seed=33, L=150)
+    fq = _write(tmp_path, reads)
+    d = tmp_path / "out"
+    d.mkdir()
+    for n in ("passed.fq", "failed.fq", "edit.fq"):
+        os.symlink("/dev/null", d / n)
+    for cmd, extra in (("filter", ["--read-quality-range", "20,"]), ("edit", ["--left-length", 10, "--left-quality-range", "20,"])):
+        r = run_cli([cmd, "-f", fq, "-o", d, "--chunk-mb", 1, "--quiet", *extra], env={"HPGQ_TRACE": "1"})
+        assert WRITER_LINE["stream"] in r.stderr
 
 
 @pytest.mark.parametrize("writer", sorted(WRITERS))
@@ -137,8 +160,7 @@ def test_cli_writer_edges(tmp_path, case, writer):
         d = tmp_path / cmd
         d.mkdir()
         extra = ["--left-length", 10, "--left-quality-range", "20,"] if cmd == "edit" else []
-        run_cli([cmd, "-f", fq, "-o", d, "--read-quality-range", q, "--chunk-mb", 1, "--quiet", *extra,
-                 *WRITERS[writer]])
+        run_writer([cmd, "-f", fq, "-o", d, "--read-quality-range", q, "--chunk-mb", 1, "--quiet", *extra], writer)
         if cmd == "filter":
             p = H.filter_params(lmax=1024, read_quality_range=q)
         else:
