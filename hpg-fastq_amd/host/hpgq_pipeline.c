@@ -77,6 +77,10 @@ typedef struct {
   char *out[2];
   size_t out_cap[2], out_len[2];
   uint64_t out_n[2];
+  /* mapped outputs: this chunk's copy parts (copy_part_t[MAX_COPIERS]) and
+   * how many are still being copied (state 3 until the last one is done) */
+  void *parts;
+  int parts_left;
 } slot_t;
 
 typedef struct {
@@ -99,6 +103,14 @@ typedef struct {
   size_t map_cap;
   uint64_t out_off[2];   /* bytes placed so far per output */
   int64_t placed;        /* chunks placed (in input order) */
+  /* the copy pool: placed chunks' parts, copied into the maps by --num-threads
+   * copier threads while the GPU workers go on with the next chunks */
+  void **cq;             /* ring of copy_part_t * */
+  int cq_cap, cq_head, cq_tail, cq_exit, ncopiers;
+  pthread_mutex_t cq_mu;
+  pthread_cond_t cq_cv;
+  int copies_pending;    /* slots in state 3 (under mu) */
+  pthread_t copier[64];
   int64_t cg_batch;   /* --cg: bytes of FASTQ text per chaos-game call (0: off) */
   /* HPGQ_TRACE=1: per chunk (the first TRACE_MAX) the reader's and the worker's
    * start / end times, printed to stderr at the end (diagnostics only) */
@@ -571,12 +583,6 @@ static void *size_part(void *arg) {
   return NULL;
 }
 
-static void *copy_part(void *arg) {
-  copy_part_t *cp = arg;
-  copy_records(cp->P, cp->s, cp->i0, cp->i1, cp->dst);
-  return NULL;
-}
-
 /* fn over the parts: part 0 on this thread, the others on threads of their own
  * (a part whose thread cannot start runs here too) */
 static void run_parts(void *(*fn)(void *), copy_part_t *part, int n) {
@@ -588,11 +594,69 @@ static void run_parts(void *(*fn)(void *), copy_part_t *part, int n) {
   }
 }
 
+/* copier thread: takes parts off the queue; the last part of a chunk frees its
+ * slot for the reader */
+static void *copier_main(void *arg) {
+  pipe_t *P = arg;
+  for (;;) {
+    pthread_mutex_lock(&P->cq_mu);
+    while (P->cq_head == P->cq_tail && !P->cq_exit) pthread_cond_wait(&P->cq_cv, &P->cq_mu);
+    if (P->cq_head == P->cq_tail) {
+      pthread_mutex_unlock(&P->cq_mu);
+      break;
+    }
+    copy_part_t *cp = P->cq[P->cq_head % P->cq_cap];
+    P->cq_head++;
+    pthread_mutex_unlock(&P->cq_mu);
+    copy_records(cp->P, cp->s, cp->i0, cp->i1, cp->dst);
+    pthread_mutex_lock(&P->mu);
+    if (--cp->s->parts_left == 0) {
+      cp->s->state = 0;
+      P->copies_pending--;
+      pthread_cond_broadcast(&P->cv);
+    }
+    pthread_mutex_unlock(&P->mu);
+  }
+  return NULL;
+}
+
+static int start_copiers(pipe_t *P) {
+  int n = P->o->num_threads;
+  if (n > 64) n = 64;
+  if (n < 1) n = 1;
+  P->cq_cap = P->nslots * MAX_COPIERS;
+  P->cq = calloc((size_t)P->cq_cap, sizeof(void *));
+  if (!P->cq) return HPGQ_E_NOMEM;
+  for (int i = 0; i < P->nslots; ++i) {
+    P->slot[i].parts = calloc(MAX_COPIERS, sizeof(copy_part_t));
+    if (!P->slot[i].parts) return HPGQ_E_NOMEM;
+  }
+  for (int t = 0; t < n; ++t) {
+    if (pthread_create(&P->copier[t], NULL, copier_main, P)) break;
+    P->ncopiers++;
+  }
+  return P->ncopiers ? 0 : HPGQ_E_NOMEM;
+}
+
+/* every placed chunk copied, then the copiers end */
+static void stop_copiers(pipe_t *P) {
+  pthread_mutex_lock(&P->mu);
+  while (P->copies_pending > 0) pthread_cond_wait(&P->cv, &P->mu);
+  pthread_mutex_unlock(&P->mu);
+  pthread_mutex_lock(&P->cq_mu);
+  P->cq_exit = 1;
+  pthread_cond_broadcast(&P->cq_cv);
+  pthread_mutex_unlock(&P->cq_mu);
+  for (int t = 0; t < P->ncopiers; ++t) pthread_join(P->copier[t], NULL);
+  P->ncopiers = 0;
+}
+
 /* a processed chunk into the mapped outputs: size its records per class (in
  * parallel), place it after chunk k-1 (which only needs k-1's sizes, not its
- * copies), copy its records at those offsets (in parallel) */
+ * copies), queue its parts for the copier threads (the slot stays busy, state
+ * 3, until they are copied) */
 static int place_and_copy(pipe_t *P, slot_t *s) {
-  static __thread copy_part_t part[MAX_COPIERS];
+  copy_part_t *part = s->parts;
   int n = P->o->num_threads;
   const int64_t per_min = 16384;   /* records per copier at least */
   if (n > MAX_COPIERS) n = MAX_COPIERS;
@@ -636,7 +700,6 @@ static int place_and_copy(pipe_t *P, slot_t *s) {
       base[c] += part[t].bytes[c];
     }
   }
-  run_parts(copy_part, part, n);
   for (int64_t i = 0; i < s->nreads; ++i) {
     if (rec_class(P, s, i)) ++nfail;
     else ++npass;
@@ -644,7 +707,18 @@ static int place_and_copy(pipe_t *P, slot_t *s) {
   pthread_mutex_lock(&P->mu);
   P->written_pass += npass;
   P->written_fail += nfail;
+  if (s->nreads > 0) {   /* busy until copied (set before the parts can finish) */
+    s->state = 3;
+    s->parts_left = n;
+    P->copies_pending++;
+  }
   pthread_mutex_unlock(&P->mu);
+  if (s->nreads > 0) {
+    pthread_mutex_lock(&P->cq_mu);
+    for (int t = 0; t < n; ++t) P->cq[P->cq_tail++ % P->cq_cap] = &part[t];
+    pthread_cond_broadcast(&P->cq_cv);
+    pthread_mutex_unlock(&P->cq_mu);
+  }
   return 0;
 }
 
@@ -786,7 +860,7 @@ static void *worker_main(void *arg) {
     W->fastq_bytes += (double)s->use;
     pthread_mutex_lock(&P->mu);
     if (rc && !P->error) P->error = rc;
-    s->state = writes && rc == 0 && !P->mmap_out ? 2 : 0;
+    if (s->state != 3) s->state = writes && rc == 0 && !P->mmap_out ? 2 : 0;   /* (3: the copiers free it) */
     pthread_cond_broadcast(&P->cv);
     pthread_mutex_unlock(&P->mu);
     if (rc) {
@@ -810,6 +884,8 @@ int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, 
   P.size = st.st_size;
   pthread_mutex_init(&P.mu, NULL);
   pthread_cond_init(&P.cv, NULL);
+  pthread_mutex_init(&P.cq_mu, NULL);
+  pthread_cond_init(&P.cq_cv, NULL);
 
   /* GPU workers: --gpu-workers per device on --gpus devices (0: every visible
    * one); worker w on device (gpu + w mod ngpus) mod ndev */
@@ -887,6 +963,7 @@ int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, 
 
   const double t0 = now_s();
   P.t0 = t0;
+  if (P.mmap_out && (rc = start_copiers(&P))) goto done;
   pthread_t reader, writer;
   pthread_create(&reader, NULL, reader_main, &P);
   const int writer_thread = writes && !P.mmap_out;
@@ -899,6 +976,7 @@ int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, 
   pthread_mutex_unlock(&P.mu);
   pthread_join(reader, NULL);
   if (writer_thread) pthread_join(writer, NULL);
+  if (P.mmap_out) stop_copiers(&P);   /* every placed chunk is in the maps */
   for (int w = 0; w < G && rc == 0; ++w) rc = W[w].rc;
   if (rc == 0 && P.error) rc = P.error < 0 && P.error != HPGQ_E_FORMAT ? HPGQ_E_INVALID : P.error;
 
@@ -962,16 +1040,19 @@ int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, 
   }
 
 done:
+  if (P.ncopiers) stop_copiers(&P);
   if (P.mmap_out) unmap_outputs(&P, &rc);
   if (P.out_pass) fclose(P.out_pass);
   if (P.out_fail) fclose(P.out_fail);
   for (int i = 0; i < P.nslots; ++i) {
     hpgq_host_free(P.slot[i].buf);
     free_results(&P.slot[i]);
+    free(P.slot[i].parts);
     free(P.slot[i].out[0]);
     free(P.slot[i].out[1]);
   }
   free(P.carry);
+  free(P.cq);
   for (int w = 0; w < G; ++w) worker_close(&W[w]);
   close(P.fd);
   return rc;

@@ -4,9 +4,10 @@
 # the engine configs, the drop-in harness, then the C5 ablation
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-bash tools/gpu_r04_trace.sh || exit $?
 O=gpurun_out/r04c
 mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_cli_gpu.py tests/test_dropin_gpu.py tests/test_engine_gpu.py -k "writer or outputs or tsan or dropin or read_counters or route or host" -x -q --timeout 200 --timeout-method thread > $O/tests.log 2>&1 || exit 6
+bash tools/gpu_r04_trace.sh || exit $?
 for cfg in c2 c3 c4 c4_pe c4_noor; do
   for v in new base new base; do
     if [ $v = base ]; then L=$PWD/hpg-fastq_amd/ab/r3base/libhpgq.so; else L=$PWD/hpg-fastq_amd/libhpgq.so; fi
