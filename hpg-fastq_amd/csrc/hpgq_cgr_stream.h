@@ -75,6 +75,8 @@
 //   2: the quality window chain replaced by a constant
 //   3: no emission mask (every byte adds to its word's cell)
 //   4: a 32-bit ds_add_u32 of the count only
+//   5: (exact) bytes that end no word skip the add by EXEC masking instead of
+//      adding to the lane's spare cell
 #ifndef HPGQ_C5_ABLATION
 #define HPGQ_C5_ABLATION 0
 #endif
@@ -693,6 +695,10 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
         const unsigned long long inc = ((unsigned long long)acc << 32) | 1ull;
         if (HPGQ_C5_ABLATION == 1)
           abl_sink ^= addr + (uint32_t)(inc >> 32);
+        else if (HPGQ_C5_ABLATION == 5) {
+          if ((E >> j) & 1u)
+            atomicAdd(reinterpret_cast<unsigned long long *>(reinterpret_cast<char *>(tab) + w), inc);
+        }
         else if (HPGQ_C5_ABLATION == 4)
           atomicAdd(reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(tab) + addr), 1u);
         else

@@ -17,6 +17,7 @@ VARIANTS = {
     "2": "the quality window chain replaced by a constant",
     "3": "no emission mask: every byte adds to its word's cell",
     "4": "a 32-bit ds_add_u32 of the count only",
+    "5": "(exact) bytes that end no word skip the add by EXEC masking, no spare-cell adds",
 }
 
 
