@@ -49,6 +49,7 @@
 #include <string.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
+#include <sys/statvfs.h>
 #include <sys/uio.h>
 #include <time.h>
 #include <unistd.h>
@@ -727,6 +728,13 @@ static int place_and_copy(pipe_t *P, slot_t *s) {
 static int map_outputs(pipe_t *P) {
   FILE *f[2] = {P->out_pass, P->out_fail};
   P->map_cap = (size_t)P->size + 4096;
+  /* a store into a mapped page the file system cannot back is a SIGBUS, not
+   * an error return: map only when the outputs (together at most the input)
+   * surely fit, else the stream writer reports ENOSPC as an I/O error */
+  struct statvfs vs;
+  if (!f[0] || fstatvfs(fileno(f[0]), &vs) ||
+      (unsigned long long)vs.f_bavail * vs.f_frsize < (unsigned long long)P->map_cap + (64ull << 20))
+    return -1;
   for (int c = 0; c < 2; ++c) {
     if (!f[c]) continue;
     const int fd = fileno(f[c]);
