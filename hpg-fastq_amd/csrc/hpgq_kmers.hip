@@ -49,9 +49,7 @@ namespace kmers {
 
 constexpr int kK = 5;
 constexpr int kNum = 1 << (2 * kK);   // 1024
-constexpr int kP = 32;                // table row pitch: start positions per row (one LDS bank each)
-constexpr int kTW = 28;               // start positions a tile counts: its 32-byte window is ONE
-                                      // 16-byte load per lane of a read's lane pair
+constexpr int kP = 32;                // start positions per tile (one LDS bank each)
 constexpr int kWG = 1024;
 constexpr int kReadsPerWave = 32;     // two lanes per read
 constexpr int kGroup = kWG / 2;       // reads per workgroup step
@@ -120,26 +118,25 @@ __global__ void __launch_bounds__(1024) kmer_maxlen_kernel(const int32_t *idx, i
   }
 }
 
-// the 14 starts of one half-tile of a lane: its 20-byte code stream (hi8:lo32,
-// byte 0's code highest; positions base + h for stream byte h, base = 0 for
-// the even lane of a pair, 12 for the odd one) shifted for the alignbit cuts
-// (t1:t0 = the 40-bit stream << 7: the 5-mer at stream byte h is bits
-// [2(15 - h) + 7, + 10)), and its count mask rotated to the lane's visiting
-// order (bit j = the start the lane visits at step j).  The lane's starts are
-// stream bytes h0 .. h0 + 13 (h0 = 0 even, 2 odd: positions 0-13 / 14-27).
+// the 16 starts of one half-tile of a lane's window: its code stream shifted
+// for the alignbit cuts (t1:t0 = the 20 bytes' codes << 7, first byte
+// highest: the 5-mer at half position h is bits [2(15 - h) + 7, + 10)) and
+// its count mask rotated to the lane's visiting order (bit j = the start the
+// lane visits at step j)
 struct Half {
   uint32_t t1, t0, er;
 };
 
-__device__ __forceinline__ Half half_of(uint32_t hi8, uint32_t lo32, uint32_t bad20, int lim, int h0, int q) {
-  // the 5-mer at h counts iff bytes h..h+4 are A/C/G/T and h <= lim
-  uint32_t e = ~(bad20 | (bad20 >> 1) | (bad20 >> 2) | (bad20 >> 3) | (bad20 >> 4));
-  e &= lim >= 15 ? 0xFFFFu : lim >= 0 ? (2u << lim) - 1u : 0u;
-  const uint32_t e14 = (e >> h0) & 0x3FFFu;
+__device__ __forceinline__ Half half_of(const uint32_t (&pk)[5], const uint32_t (&bd)[5], int last, int q) {
+  const uint32_t s0 = (pk[1] << 24) | (pk[2] << 16) | (pk[3] << 8) | pk[4];
+  const uint32_t b = bd[0] | (bd[1] << 4) | (bd[2] << 8) | (bd[3] << 12) | (bd[4] << 16);
+  // the 5-mer at h counts iff bytes h..h+4 are A/C/G/T and h <= last
+  uint32_t e = ~(b | (b >> 1) | (b >> 2) | (b >> 3) | (b >> 4));
+  e &= last >= 15 ? 0xFFFFu : last >= 0 ? (2u << last) - 1u : 0u;
   Half H;
-  H.t1 = __builtin_amdgcn_alignbit(hi8, lo32, 25);
-  H.t0 = lo32 << 7;
-  H.er = (e14 | (e14 << 14)) >> q;
+  H.t1 = __builtin_amdgcn_alignbit(pk[0], s0, 25);
+  H.t0 = s0 << 7;
+  H.er = (e | (e << 16)) >> q;
   return H;
 }
 
@@ -149,21 +146,20 @@ __global__ void __launch_bounds__(kWG) kmer_tile_kernel(const char *seq, const i
   __shared__ uint32_t t[kNum * kP];   // [id][position]
   // tiles with a start position some counted read reaches
   const int last_start = min(npos, (maxlen ? *maxlen : npos + kK - 1) - (kK - 1));   // starts 0 .. last_start-1
-  const int T = last_start > 0 ? (last_start + kTW - 1) / kTW : 0;
+  const int T = last_start > 0 ? (last_start + kP - 1) / kP : 0;
   const int b = (int)blockIdx.x, xcd = b & 7, slot = b >> 3;
   const int classes = T ? (int)(gridDim.x >> 3) / T : 0;   // read-group classes per XCD
   if (T == 0 || slot >= classes * T) return;
   const int tile = slot % T, cls = slot / T;
-  const int p0 = tile * kTW;
+  const int p0 = tile * kP;
   for (int i = threadIdx.x; i < kP * kNum; i += kWG) t[i] = 0;
   __syncthreads();
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  // lanes 2i, 2i + 1 take read i's half-tiles hl = 0, 1 (starts 14 hl + [0,
-  // 14)); the lane visits start 14 hl + (q + j) mod 14 at step j, so the 32
-  // lanes of a group (lanes 0-31, 32-63: one LDS cycle each) sit on 28
-  // distinct positions at every step (two pairs of reads share their q: a
-  // group takes two LDS cycles per add instead of one)
-  const int q = ((lane >> 1) & 15) % 14, hl = lane & 1;
+  // lanes 2i, 2i + 1 take read i's half-tiles hl = 0, 1 (starts 16 hl + [0,
+  // 16)); the lane visits start 16 hl + (q + j) mod 16 at step j, so the 32
+  // lanes of a group (lanes 0-31, 32-63: one LDS cycle each) sit on 32
+  // distinct positions at every step
+  const int q = (lane >> 1) & 15, hl = lane & 1;
   const int32_t data_end = __builtin_amdgcn_readfirstlane(idx[n]);
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
       (void *)seq, (short)0, data_end + HPGQ_DEVICE_SLACK, 0x00020000);
@@ -176,72 +172,85 @@ __global__ void __launch_bounds__(kWG) kmer_tile_kernel(const char *seq, const i
   const int64_t ngroups = (n + kGroup - 1) / kGroup;
   const int64_t gstride = 8 * (int64_t)classes;
   const int64_t g0 = xcd + 8 * (int64_t)cls;
-  // a read's offsets and mask byte (unconditional loads: past the end they
-  // read 0, so the compiler counts the loads in flight exactly)
+  // a read's offsets and mask byte.  The wave's 32 reads take ONE coalesced
+  // load of their 33 offsets (lane l: idx[rb + l]) and one of their 32 mask
+  // bytes (lane l: mask[rb + l]), handed to the read's lane pair by
+  // ds_bpermute when the group is used (per-lane loads of idx[r], idx[r + 1]
+  // and mask[r] were three addresser passes per wave and tile visit).
+  // Unconditional loads: past the end they read 0, so the compiler counts the
+  // loads in flight exactly.
   struct Meta {
     int32_t a, e;
     uint32_t m;
   };
-  auto meta = [&](int64_t g) __attribute__((always_inline)) {
-    const int64_t r = g * kGroup + wave * kReadsPerWave + (lane >> 1);
-    const uint32_t ro = r < n ? (uint32_t)r : 0x3FFFFFF0u;
+  struct Raw {
+    int32_t ix;
+    uint32_t mk;
+    int64_t rb;
+  };
+  auto meta_raw = [&](int64_t g) __attribute__((always_inline)) {
+    Raw R;
+    R.rb = g * kGroup + wave * kReadsPerWave;
+    const int64_t r = R.rb + lane;
+    const uint32_t ro = r <= n && lane <= kReadsPerWave ? (uint32_t)r : 0x3FFFFFF0u;
+    R.ix = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(ri, ro * 4u, 0, 0);
+    const bool on = r < n && lane < kReadsPerWave;
+    R.mk = mask ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rm, on ? (uint32_t)r : 0x3FFFFFF0u, 0, 0)
+                : (on ? 1u : 0u);
+    return R;
+  };
+  auto resolve = [&](const Raw &R) __attribute__((always_inline)) {
+    const int i = lane >> 1;
     Meta M;
-    M.a = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(ri, ro * 4u, 0, 0);
-    M.e = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(ri, ro * 4u + 4u, 0, 0);
-    M.m = mask ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rm, ro, 0, 0) : (r < n ? 1u : 0u);
+    M.a = __builtin_amdgcn_ds_bpermute(4 * i, R.ix);
+    M.e = __builtin_amdgcn_ds_bpermute(4 * (i + 1), R.ix);
+    M.m = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * i, (int)R.mk);
     return M;
   };
-  // the lane's 16 bytes: a read's two lanes read its 32-byte tile window with
-  // ONE 16-byte load each (the 5-mers across the halves take the partner's
-  // codes by DPP); a lane's pieces of one read share cache lines, so the
-  // addresser sees about one line per read and load instead of the two
-  // unaligned 20-byte pieces (b128 + b32) of 32-position tiles
-  auto window = [&](const Meta &M) __attribute__((always_inline)) {
-    return __builtin_amdgcn_raw_buffer_load_b128(rs, (uint32_t)(M.a + p0 + 16 * hl), 0, 0);
+  // the lane's 20 bytes (16 starts + 4): a read's two lanes read 36
+  // contiguous bytes
+  struct Win {
+    v4u a;
+    uint32_t c;
   };
-  typedef v4u Win;
-  // per step j: the alignbit shift of the visited start (stream byte h = h0 +
-  // (q + j) mod 14; 30 - 2h, alignbit reads 5 bits) and its cell's position bits
-  const int h0 = hl ? 2 : 0, base = hl ? 12 : 0;
-  uint32_t sh[14], row[14];
+  auto window = [&](const Meta &M) __attribute__((always_inline)) {
+    const uint32_t o = (uint32_t)(M.a + p0 + 16 * hl);
+    Win W;
+    W.a = __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0);
+    W.c = __builtin_amdgcn_raw_buffer_load_b32(rs, o + 16u, 0, 0);
+    return W;
+  };
+  // per step j: the alignbit shift of the visited start (30 - 2 (q + j mod
+  // 16); alignbit reads 5 bits) and its cell's position bits
+  uint32_t sh[16], row[16];
 #pragma unroll
-  for (int j = 0; j < 14; ++j) {
-    const uint32_t hv = (uint32_t)((q + j) % 14);
-    sh[j] = 30u - 2u * (hv + (uint32_t)h0);
-    row[j] = 4u * (hv + 14u * (uint32_t)hl);
+  for (int j = 0; j < 16; ++j) {
+    const uint32_t h = (uint32_t)((q + j) & 15);
+    sh[j] = 30u - 2u * h;
+    row[j] = 4u * (h + 16u * (uint32_t)hl);
   }
   constexpr uint32_t kIdBits = (uint32_t)(kNum - 1) << 7;   // id * 128 = id * kP * 4
   // software pipeline: group g counted while g + stride's window and
   // g + 2 stride's offsets are in flight
-  Meta cur = meta(g0);
+  Meta cur = resolve(meta_raw(g0));
   Win w = window(cur);
-  Meta nxt = meta(g0 + gstride);
+  Raw nxt_raw = meta_raw(g0 + gstride);
   for (int64_t g = g0; g < ngroups; g += gstride) {
     // the read's last start, relative to the tile's first (< 0: none here;
     // masked-out reads: none)
-    const int last = cur.m == 1u ? min(min(cur.e - cur.a - kK, npos - 1) - p0, kTW - 1) : -1;
-    uint32_t pk[4], bd[4];
+    const int last = cur.m == 1u ? min(cur.e - cur.a - kK, npos - 1) - p0 : -1;
+    uint32_t pk[5], bd[5];
+    const uint32_t wd[5] = {w.a[0], w.a[1], w.a[2], w.a[3], w.c};
 #pragma unroll
-    for (int i = 0; i < 4; ++i) codes4(w[i], pk[i], bd[i]);
-    w = window(nxt);   // next group's window (its offsets arrived during this group)
+    for (int i = 0; i < 5; ++i) codes4(wd[i], pk[i], bd[i]);
+    const Meta nxt = resolve(nxt_raw);   // (its loads were issued a group ago)
+    w = window(nxt);   // next group's window
     cur = nxt;
-    nxt = meta(g + 2 * gstride);
+    nxt_raw = meta_raw(g + 2 * gstride);
     if (__ballot(last >= 0) == 0ull) continue;   // the whole wave's reads end before these starts
-    // own codes (16 bytes, first highest) and bad bits; the partner's edge
-    // dword (even lane: the odd lane's first, odd: the even lane's last) by
-    // one DPP quad_perm [1, 0, 3, 2]
-    const uint32_t o32 = (pk[0] << 24) | (pk[1] << 16) | (pk[2] << 8) | pk[3];
-    const uint32_t ob = bd[0] | (bd[1] << 4) | (bd[2] << 8) | (bd[3] << 12);
-    const uint32_t send = hl ? (pk[0] | (bd[0] << 8)) : (pk[3] | (bd[3] << 8));
-    const uint32_t recv = (uint32_t)__builtin_amdgcn_mov_dpp((int)send, 0xB1, 0xF, 0xF, true);
-    const uint32_t rp = recv & 0xFFu, rb = (recv >> 8) & 0xFu;
-    // 20-byte stream: even = own 16 + the partner's first 4, odd = the partner's last 4 + own 16
-    const uint32_t hi8 = hl ? rp : pk[0];
-    const uint32_t lo32 = hl ? o32 : ((o32 << 8) | rp);
-    const uint32_t bad20 = hl ? (rb | (ob << 4)) : (ob | (rb << 16));
-    const Half hf = half_of(hi8, lo32, bad20, last - base, h0, q);
+    const Half hf = half_of(pk, bd, last - 16 * hl, q);
 #pragma unroll
-    for (int j = 0; j < 14; ++j) {
+    for (int j = 0; j < 16; ++j) {
       // cell byte address id * 128 + position * 4: the id cut out at bits
       // 7..16 by one v_alignbit, the position's bits from row (v_bitop3);
       // a start that does not count adds 0
@@ -265,12 +274,12 @@ __global__ void __launch_bounds__(kWG) kmer_tile_kernel(const char *seq, const i
 __global__ void __launch_bounds__(256) kmer_reduce_kernel(const uint32_t *slab, int npos, const int *maxlen, int grid,
                                                           unsigned long long *out) {
   const int last_start = min(npos, (maxlen ? *maxlen : npos + kK - 1) - (kK - 1));
-  const int T = last_start > 0 ? (last_start + kTW - 1) / kTW : 0;
+  const int T = last_start > 0 ? (last_start + kP - 1) / kP : 0;
   const int64_t f = (int64_t)blockIdx.x * 256 + threadIdx.x;   // tile * kP * kNum + id * kP + row
   const int tile = (int)(f / (kP * kNum)), cell = (int)(f % (kP * kNum));
   const int classes = T ? (grid >> 3) / T : 0;
-  if (tile >= T || cell % kP >= kTW) return;
-  const int p = tile * kTW + cell % kP;
+  if (tile >= T) return;
+  const int p = tile * kP + cell % kP;
   if (p >= npos) return;
   uint32_t sum = 0;
   for (int cls = 0; cls < classes; ++cls)
@@ -332,7 +341,7 @@ int hpgq_kmers_open(hpgq_kmers_t **km, int device, int lmax, void *stream) {
     // allows) x read-group classes, so every tile of a class has its
     // workgroup on each XCD (the kernel takes the tiles the longest read
     // needs and idles the rest)
-    const int tmax = std::max(1, (k->npos + kTW - 1) / kTW);
+    const int tmax = std::max(1, (k->npos + kP - 1) / kP);
     k->grid = 8 * tmax * std::max(1, k->cus / (8 * tmax));
     if (k->npos > 0 && hipMalloc(&k->d_slab, (size_t)k->grid * kP * kNum * sizeof(uint32_t)) != hipSuccess) {
       hpgq_kmers_close(k);
@@ -360,7 +369,7 @@ int hpgq_kmers_count_device(hpgq_kmers_t *k, const hpgq_batch_t *b, const uint8_
   if (!b->seq || !b->data_indices) return HPGQ_E_INVALID;
   HPGQ_HIP_TRY(hipSetDevice(k->device));
   using namespace hpgq::kmers;
-  const int tmax = (k->npos + kTW - 1) / kTW;
+  const int tmax = (k->npos + kP - 1) / kP;
   constexpr int64_t kPart = (int64_t)1 << 28;   // reads per launch (32-bit offsets into idx)
   for (int64_t lo = 0; lo < b->num_reads; lo += kPart) {
     const int64_t n = std::min(kPart, b->num_reads - lo);
