@@ -81,6 +81,12 @@
 #define HPGQ_C5_ABLATION 0
 #endif
 
+// tiles of bytes in flight per wave: 2 (fetch the next tile while this one
+// is counted) or 3 (fetch the one after it)
+#ifndef HPGQ_C5_DEPTH
+#define HPGQ_C5_DEPTH 3
+#endif
+
 namespace hpgq {
 namespace cgr {
 namespace stream {
@@ -465,6 +471,8 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
   constexpr uint32_t SPARE = (uint32_t)cells << 3;      // the spare cells (one per lane: bytes
                                                         // that end no word do not collide)
   constexpr uint32_t kRun = 48 - K;
+  // (VALID: the third tile's registers spill; it stays at 2)
+  constexpr int kDepth = !VALID && HPGQ_C5_DEPTH == 3 ? 3 : 2;
   // per wave: start bitmaps of two tiles (this, next) + context; VALID: the
   // validity toggles of the two tiles
   constexpr int kBm = VALID ? 5 : 3;
@@ -739,13 +747,39 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
     if (VALID) tgA = take_bits(&tcb[lane]);
     load32(rs, (uint32_t)(tA + kLaneBytes * lane), sA);
     load32(rq, (uint32_t)(tA + kLaneBytes * lane), qA);
+    // the load cursor (wave-uniform) walks the same tile stream one tile
+    // ahead of the start cursor: tile z = y's successor is fetched while x is
+    // counted, so a tile's bytes have two tiles' work to arrive
+    int32_t ls = s, lt = tA, le = eA;
+    bool lfin = false;
+    auto lnext = [&] {
+      if (lfin) return;
+      lt += kTile;
+      if (lt >= le) {
+        ls += nwav;
+        if (ls < ns) {
+          lt = (int32_t)(a0 + ((int64_t)ls << kSpanLog));
+          le = (int32_t)min((int64_t)lt + kSpan, (int64_t)b1);
+        } else {
+          lfin = true;
+        }
+      }
+    };
+    uint32_t sC[kNdw], qC[kNdw], soC, tgC = 0, skC = 0;
+    int32_t tC, eC, rfC = 0;
+    if constexpr (kDepth == 3) {
+      lnext();
+      load32(rs, lfin ? kPast : (uint32_t)(lt + kLaneBytes * lane), sB);
+      load32(rq, lfin ? kPast : (uint32_t)(lt + kLaneBytes * lane), qB);
+    }
     // count tile x while fetching tile y (straight-line: the loads are
     // unconditional, so the compiler counts the loads in flight exactly and
-    // a tile waits only for its own bytes); false past the wave's last tile
+    // a tile waits only for its own bytes); false past the wave's last tile.
+    // (kDepth 3: y's bytes are in flight already; the loads go to z)
     auto half = [&](const int32_t tx, const int32_t ex, uint32_t (&sx)[kNdw], uint32_t (&qx)[kNdw], const uint32_t sox,
                     const uint32_t skx, const uint32_t tgx, const int32_t rfx, uint32_t *scpy, uint32_t *tcpy,
                     int32_t &ty, int32_t &ey, uint32_t (&sy)[kNdw], uint32_t (&qy)[kNdw], uint32_t &soy,
-                    uint32_t &sky, uint32_t &tgy, int32_t &rfy) {
+                    uint32_t &sky, uint32_t &tgy, int32_t &rfy, uint32_t (&sz)[kNdw], uint32_t (&qz)[kNdw]) {
       ty = tx + kTile;
       ey = ex;
       bool entering = false, fin = false;
@@ -765,9 +799,16 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
       const int32_t rv = r - 1;   // entering: the read holding byte ty - 1
       const v4u a = __builtin_amdgcn_raw_buffer_load_b128(rs, entering ? (uint32_t)ty - 16u : kPast, 0, 0);
       const v2u q = __builtin_amdgcn_raw_buffer_load_b64(rq, entering ? (uint32_t)ty - 8u : kPast, 0, 0);
-      const uint32_t oy = fin ? kPast : (uint32_t)(ty + kLaneBytes * lane);
-      load32(rs, oy, sy);
-      load32(rq, oy, qy);
+      if constexpr (kDepth == 3) {
+        lnext();
+        const uint32_t oz = lfin ? kPast : (uint32_t)(lt + kLaneBytes * lane);
+        load32(rs, oz, sz);
+        load32(rq, oz, qz);
+      } else {
+        const uint32_t oy = fin ? kPast : (uint32_t)(ty + kLaneBytes * lane);
+        load32(rs, oy, sy);
+        load32(rq, oy, qy);
+      }
       const uint32_t par = tile(tx, ex, sx, qx, sox, skx, tgx, rfx, [&] {
         rfy = r;
         scatter_starts<VALID, VALID>(A, rt, scpy, tcpy, r, iw, itg, ty, fin ? INT32_MIN : ty + kTile, lane,
@@ -783,9 +824,22 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
       }
       return true;
     };
+    if constexpr (kDepth == 3) {
+    // (the start bitmaps alternate between the two halves of sc / tcb: tile x
+    // reads its own before scattering y's into the other)
     for (;;) {
-      if (!half(tA, eA, sA, qA, soA, skA, tgA, rfA, sc + 64, tcb + 64, tB, eB, sB, qB, soB, skB, tgB, rfB)) break;
-      if (!half(tB, eB, sB, qB, soB, skB, tgB, rfB, sc, tcb, tA, eA, sA, qA, soA, skA, tgA, rfA)) break;
+      if (!half(tA, eA, sA, qA, soA, skA, tgA, rfA, sc + 64, tcb + 64, tB, eB, sB, qB, soB, skB, tgB, rfB, sC, qC)) break;
+      if (!half(tB, eB, sB, qB, soB, skB, tgB, rfB, sc, tcb, tC, eC, sC, qC, soC, skC, tgC, rfC, sA, qA)) break;
+      if (!half(tC, eC, sC, qC, soC, skC, tgC, rfC, sc + 64, tcb + 64, tA, eA, sA, qA, soA, skA, tgA, rfA, sB, qB)) break;
+      if (!half(tA, eA, sA, qA, soA, skA, tgA, rfA, sc, tcb, tB, eB, sB, qB, soB, skB, tgB, rfB, sC, qC)) break;
+      if (!half(tB, eB, sB, qB, soB, skB, tgB, rfB, sc + 64, tcb + 64, tC, eC, sC, qC, soC, skC, tgC, rfC, sA, qA)) break;
+      if (!half(tC, eC, sC, qC, soC, skC, tgC, rfC, sc, tcb, tA, eA, sA, qA, soA, skA, tgA, rfA, sB, qB)) break;
+    }
+    } else {
+    for (;;) {
+      if (!half(tA, eA, sA, qA, soA, skA, tgA, rfA, sc + 64, tcb + 64, tB, eB, sB, qB, soB, skB, tgB, rfB, sA, qA)) break;
+      if (!half(tB, eB, sB, qB, soB, skB, tgB, rfB, sc, tcb, tA, eA, sA, qA, soA, skA, tgA, rfA, sB, qB)) break;
+    }
     }
   }
   if (__ballot(risky) && lane == 0) atomicOr(A.gate, GATE_EXACT);

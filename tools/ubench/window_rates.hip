@@ -10,6 +10,8 @@
 //           (150 bytes per read and tile: what staging whole reads costs)
 //   lane1_68x3  one lane per read, 64-position tiles: 68-byte windows, 3 tiles
 //           (window_TB_s still counts 5 x 36 bytes per read: the same work)
+//   lane2_68x3, lane2_68x2_36  two lanes per read, 64-position tiles (36
+//           bytes per lane), three of them / two and a 32-position tail
 // Each lane XOR-folds what it loads (kept alive through one store per lane).
 // The tiles of a read are visited back to back, so tiles 1..4 hit the cache:
 // the time is the load path (TA, L1/L2), not HBM.
@@ -83,6 +85,36 @@ __global__ void __launch_bounds__(kWG) k_lane1_68(const char *s, uint32_t nreads
   out[blockIdx.x * kWG + threadIdx.x] = x;
 }
 
+// two lanes per read, 64-position tiles (round 4): lane k of a read takes
+// starts 32k..32k+31 of a tile, a 36-byte window (two 16-byte loads and one
+// 4-byte load); TAIL: the 150 bp read's third visit is a 32-position tile
+// (a 16-byte and a 4-byte load per lane, as k_lanes<2>) instead of a third
+// 64-position one
+template <bool TAIL>
+__global__ void __launch_bounds__(kWG) k_lane2_64(const char *s, uint32_t nreads, uint32_t *out) {
+  const auto rs = rsrc(s, nreads * kL + 128);
+  const int lane = threadIdx.x & 63, part = lane & 1;
+  uint32_t x = 0;
+  const uint32_t nw = gridDim.x * (kWG / 64);
+  for (uint32_t g = blockIdx.x * (kWG / 64) + (threadIdx.x >> 6); g * 32 < nreads; g += nw) {
+    const uint32_t r = g * 32 + (lane >> 1);
+    const uint32_t a = (r < nreads ? r : 0) * kL;
+#pragma unroll
+    for (int t = 0; t < (TAIL ? 2 : 3); ++t) {
+      const uint32_t o = a + 64 * t + 32 * part;
+      const v4u p = __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0);
+      const v4u q = __builtin_amdgcn_raw_buffer_load_b128(rs, o + 16, 0, 0);
+      x ^= p.x ^ p.y ^ p.z ^ p.w ^ q.x ^ q.y ^ q.z ^ q.w ^ __builtin_amdgcn_raw_buffer_load_b32(rs, o + 32, 0, 0);
+    }
+    if (TAIL) {
+      const uint32_t o = a + 128 + 16 * part;
+      const v4u p = __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0);
+      x ^= p.x ^ p.y ^ p.z ^ p.w ^ __builtin_amdgcn_raw_buffer_load_b32(rs, o + 16, 0, 0);
+    }
+  }
+  out[blockIdx.x * kWG + threadIdx.x] = x;
+}
+
 // nine lanes per read (lanes 63 idle), one dword each
 __global__ void __launch_bounds__(kWG) k_dword9(const char *s, uint32_t nreads, uint32_t *out) {
   const auto rs = rsrc(s, nreads * kL + 64);
@@ -148,6 +180,8 @@ int main() {
   run("dword9", [&] { hipLaunchKernelGGL(k_dword9, dim3(grid), dim3(kWG), 0, 0, d, nreads, o); });
   run("flat", [&] { hipLaunchKernelGGL(k_flat, dim3(grid), dim3(kWG), 0, 0, d, nreads, o); });
   run("lane1_68x3", [&] { hipLaunchKernelGGL(k_lane1_68, dim3(grid), dim3(kWG), 0, 0, d, nreads, o); });
+  run("lane2_68x3", [&] { hipLaunchKernelGGL(k_lane2_64<false>, dim3(grid), dim3(kWG), 0, 0, d, nreads, o); });
+  run("lane2_68x2_36", [&] { hipLaunchKernelGGL(k_lane2_64<true>, dim3(grid), dim3(kWG), 0, 0, d, nreads, o); });
   hipFree(d);
   hipFree(o);
   return 0;
