@@ -57,12 +57,6 @@ constexpr int kTriSlack = 8;    // readable bytes past the data end the loads ma
 // Paired-end edit, usual windows: both mates' trim loads in flight at once
 // (1), or one mate's loads issued and finished before the other's (0: no
 // TrimLoads of two mates live together).
-// cache policy (buffer-load aux bits) of the stream's byte loads: 0 default,
-// 2 nt (non-temporal: read once, so the lines the trim prologue gathered stay
-// in L2 until the unit's steps stream them)
-#ifndef HPGQ_STREAM_CPOL
-#define HPGQ_STREAM_CPOL 0
-#endif
 #ifndef HPGQ_PE_TRIM_OVERLAP
 #define HPGQ_PE_TRIM_OVERLAP 1
 #endif
@@ -574,12 +568,12 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     const v4u rec = *reinterpret_cast<const v4u *>(tab(m, tb) + 4 * src);
     pd.n = rec.z;
     if (NW == 2) {
-      const v2u a = __builtin_amdgcn_raw_buffer_load_b64(rs[m], rec.x + lane8, 0, HPGQ_STREAM_CPOL);
-      const v2u b = __builtin_amdgcn_raw_buffer_load_b64(rq[m], rec.y + lane8, 0, HPGQ_STREAM_CPOL);
+      const v2u a = __builtin_amdgcn_raw_buffer_load_b64(rs[m], rec.x + lane8, 0, 0);
+      const v2u b = __builtin_amdgcn_raw_buffer_load_b64(rq[m], rec.y + lane8, 0, 0);
       pd.s[0] = a.x; pd.s[1] = a.y; pd.q[0] = b.x; pd.q[1] = b.y;
     } else {
-      const v4u a = __builtin_amdgcn_raw_buffer_load_b128(rs[m], rec.x + lane8, 0, HPGQ_STREAM_CPOL);
-      const v4u b = __builtin_amdgcn_raw_buffer_load_b128(rq[m], rec.y + lane8, 0, HPGQ_STREAM_CPOL);
+      const v4u a = __builtin_amdgcn_raw_buffer_load_b128(rs[m], rec.x + lane8, 0, 0);
+      const v4u b = __builtin_amdgcn_raw_buffer_load_b128(rq[m], rec.y + lane8, 0, 0);
 #pragma unroll
       for (int w = 0; w < NW; ++w) {
         pd.s[w] = a[w & 3];
