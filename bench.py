@@ -386,7 +386,7 @@ def e2e_leg(args, device, runs=5, writer_runs=3):
     c4 = ["--left-length", "10", "--left-quality-range", "20,", "--right-length", "30",
           "--right-quality-range", "20,"]
 
-    def cli_runs(cmd, flags, n, warm):
+    def cli_runs(cmd, flags, n, warm, writers=None):
         vals, gbs = [], []
         for rep in range(n + (1 if warm else 0)):   # a warm-up run (GPU clocks, file pages): not counted
             shutil.rmtree(outd, ignore_errors=True)
@@ -399,6 +399,9 @@ def e2e_leg(args, device, runs=5, writer_runs=3):
                 raise RuntimeError(f"{cmd}: no throughput line")
             if warm and rep == 0:
                 continue
+            w = re.search(r"Output writer\s*:\s*(.+)", r.stdout)
+            if writers is not None and w:
+                writers.add(w.group(1).strip())
             vals.append(float(m.group(4)))
             gbs.append(float(m.group(2)) / float(m.group(3)))
         return vals, gbs
@@ -416,8 +419,9 @@ def e2e_leg(args, device, runs=5, writer_runs=3):
         for cmd, flags in (("filter", c2), ("edit", c4)):
             if writer_runs <= 0:
                 break
-            vals, gbs = cli_runs(cmd, flags, writer_runs, False)
-            out[cmd] = {"command": f"hpg-fastq {cmd} -f <file> -o /dev/shm/... {' '.join(flags)} --gpus 1 "
+            writers = set()
+            vals, gbs = cli_runs(cmd, flags, writer_runs, False, writers)
+            out[cmd] = {"writer": ", ".join(sorted(writers)) or None,"command": f"hpg-fastq {cmd} -f <file> -o /dev/shm/... {' '.join(flags)} --gpus 1 "
                                    f"--num-threads {nthr}",
                         "mreads_s": round(float(np.median(vals)), 2), "mreads_s_min": round(min(vals), 2),
                         "mreads_s_runs": [round(v, 2) for v in vals],
