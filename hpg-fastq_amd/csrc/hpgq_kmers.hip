@@ -56,6 +56,7 @@ constexpr int kGroup = kWG / 2;       // reads per workgroup step
 constexpr int kSpill = 8;             // tiles above which the maxlen prepass runs
 static_assert(kWG == kNum, "the flush gives each thread one id");
 
+typedef unsigned v2u __attribute__((ext_vector_type(2)));
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
 // byte & 7 is one-to-one on A(1) C(3) T(4) G(7).  kEx*: the expected byte per
@@ -208,16 +209,21 @@ __global__ void __launch_bounds__(kWG) kmer_tile_kernel(const char *seq, const i
     return M;
   };
   // the lane's 20 bytes (16 starts + 4): a read's two lanes read 36
-  // contiguous bytes
+  // contiguous bytes.  The loads are dword-aligned: 24 bytes from the dword
+  // at or below the window (a b128 and a b64), shifted into place by
+  // v_alignbyte when the group is counted.  Reads start at any byte (150-byte
+  // reads back to back: every other one at 2 mod 4), and a 16-byte load that
+  // is not dword-aligned costs the addresser far more than an aligned one
+  // (tools/ubench/window_rates.hip: 405 vs 248 us for the same windows).
   struct Win {
     v4u a;
-    uint32_t c;
+    v2u c;
   };
   auto window = [&](const Meta &M) __attribute__((always_inline)) {
-    const uint32_t o = (uint32_t)(M.a + p0 + 16 * hl);
+    const uint32_t o = (uint32_t)(M.a + p0 + 16 * hl) & ~3u;
     Win W;
     W.a = __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0);
-    W.c = __builtin_amdgcn_raw_buffer_load_b32(rs, o + 16u, 0, 0);
+    W.c = __builtin_amdgcn_raw_buffer_load_b64(rs, o + 16u, 0, 0);
     return W;
   };
   // per step j: the alignbit shift of the visited start (30 - 2 (q + j mod
@@ -240,7 +246,11 @@ __global__ void __launch_bounds__(kWG) kmer_tile_kernel(const char *seq, const i
     // masked-out reads: none)
     const int last = cur.m == 1u ? min(cur.e - cur.a - kK, npos - 1) - p0 : -1;
     uint32_t pk[5], bd[5];
-    const uint32_t wd[5] = {w.a[0], w.a[1], w.a[2], w.a[3], w.c};
+    const uint32_t ab = (uint32_t)cur.a & 3u;   // the window's byte offset in its first dword
+                                                // (p0 and 16 hl are multiples of 4)
+    const uint32_t wd[5] = {__builtin_amdgcn_alignbyte(w.a[1], w.a[0], ab), __builtin_amdgcn_alignbyte(w.a[2], w.a[1], ab),
+                            __builtin_amdgcn_alignbyte(w.a[3], w.a[2], ab), __builtin_amdgcn_alignbyte(w.c[0], w.a[3], ab),
+                            __builtin_amdgcn_alignbyte(w.c[1], w.c[0], ab)};
 #pragma unroll
     for (int i = 0; i < 5; ++i) codes4(wd[i], pk[i], bd[i]);
     const Meta nxt = resolve(nxt_raw);   // (its loads were issued a group ago)

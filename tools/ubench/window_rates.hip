@@ -10,6 +10,8 @@
 //           (150 bytes per read and tile: what staging whole reads costs)
 //   lane1_68x3  one lane per read, 64-position tiles: 68-byte windows, 3 tiles
 //           (window_TB_s still counts 5 x 36 bytes per read: the same work)
+//   lane2_same, lane2_aligned  k_lanes<2> again, and with dword-aligned loads
+//           (b128 + b64 from the dword below, v_alignbyte into place)
 //   lane2_68x3, lane2_68x2_36  two lanes per read, 64-position tiles (36
 //           bytes per lane), three of them / two and a 32-position tail
 // Each lane XOR-folds what it loads (kept alive through one store per lane).
@@ -21,6 +23,7 @@
 #include <cstdint>
 #include <vector>
 
+typedef unsigned v2u __attribute__((ext_vector_type(2)));
 typedef unsigned v4u __attribute__((ext_vector_type(4)));
 
 constexpr int kWG = 1024;
@@ -115,6 +118,38 @@ __global__ void __launch_bounds__(kWG) k_lane2_64(const char *s, uint32_t nreads
   out[blockIdx.x * kWG + threadIdx.x] = x;
 }
 
+// k_lanes<2> with dword-aligned loads: the 150-byte reads start at even
+// offsets only, so a window's 16-byte load is misaligned by 2 bytes half the
+// time; ALIGN loads the 24 bytes from the dword below instead (a b128 and a
+// b64) and shifts them into place with v_alignbyte (what the kernel would do)
+template <bool ALIGN>
+__global__ void __launch_bounds__(kWG) k_lane2_al(const char *s, uint32_t nreads, uint32_t *out) {
+  const auto rs = rsrc(s, nreads * kL + 64);
+  const int lane = threadIdx.x & 63, part = lane & 1;
+  uint32_t x = 0;
+  const uint32_t nw = gridDim.x * (kWG / 64);
+  for (uint32_t g = blockIdx.x * (kWG / 64) + (threadIdx.x >> 6); g * 32 < nreads; g += nw) {
+    const uint32_t r = g * 32 + (lane >> 1);
+    const uint32_t a = (r < nreads ? r : 0) * kL;
+#pragma unroll
+    for (int t = 0; t < kTiles; ++t) {
+      const uint32_t o = a + 32 * t + 16 * part;
+      if (ALIGN) {
+        const uint32_t sh = o & 3u;
+        const v4u p = __builtin_amdgcn_raw_buffer_load_b128(rs, o & ~3u, 0, 0);
+        const v2u q = __builtin_amdgcn_raw_buffer_load_b64(rs, (o & ~3u) + 16, 0, 0);
+        const uint32_t w[6] = {p.x, p.y, p.z, p.w, q.x, q.y};
+#pragma unroll
+        for (int i = 0; i < 5; ++i) x ^= __builtin_amdgcn_alignbyte(w[i + 1], w[i], sh);
+      } else {
+        const v4u p = __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0);
+        x ^= p.x ^ p.y ^ p.z ^ p.w ^ __builtin_amdgcn_raw_buffer_load_b32(rs, o + 16, 0, 0);
+      }
+    }
+  }
+  out[blockIdx.x * kWG + threadIdx.x] = x;
+}
+
 // nine lanes per read (lanes 63 idle), one dword each
 __global__ void __launch_bounds__(kWG) k_dword9(const char *s, uint32_t nreads, uint32_t *out) {
   const auto rs = rsrc(s, nreads * kL + 64);
@@ -181,6 +216,8 @@ int main() {
   run("flat", [&] { hipLaunchKernelGGL(k_flat, dim3(grid), dim3(kWG), 0, 0, d, nreads, o); });
   run("lane1_68x3", [&] { hipLaunchKernelGGL(k_lane1_68, dim3(grid), dim3(kWG), 0, 0, d, nreads, o); });
   run("lane2_68x3", [&] { hipLaunchKernelGGL(k_lane2_64<false>, dim3(grid), dim3(kWG), 0, 0, d, nreads, o); });
+  run("lane2_same", [&] { hipLaunchKernelGGL(k_lane2_al<false>, dim3(grid), dim3(kWG), 0, 0, d, nreads, o); });
+  run("lane2_aligned", [&] { hipLaunchKernelGGL(k_lane2_al<true>, dim3(grid), dim3(kWG), 0, 0, d, nreads, o); });
   run("lane2_68x2_36", [&] { hipLaunchKernelGGL(k_lane2_64<true>, dim3(grid), dim3(kWG), 0, 0, d, nreads, o); });
   hipFree(d);
   hipFree(o);
