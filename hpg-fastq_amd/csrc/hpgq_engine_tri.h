@@ -218,36 +218,20 @@ using UndoTag = TriTag<2>;   // take back what the same step just added (nibble 
 // the trim windows' quality bytes for the usual windows (left <= 16, right <=
 // 32): three 16-byte loads issued together, the right ones at pb = n - 32 (or
 // 0 for a short read, so no load starts before the read's own offset)
-// (HPGQ_TRIM_ALIGNED: the loads start at the dword at or below each window --
-// 20 and 36 bytes -- and trim_finish shifts them into place with v_alignbyte:
-// reads start at any byte, and a 16-byte load that is not dword-aligned costs
-// the texture addresser far more than an aligned one, tools/ubench/window_rates.hip)
-#ifndef HPGQ_TRIM_ALIGNED
-#define HPGQ_TRIM_ALIGNED 1
-#endif
 struct TrimLoads {
   v4u wl, wr0, wr1;
-  uint32_t wl4, wr8;   // (HPGQ_TRIM_ALIGNED) the dword after wl / wr1
 };
 
 __device__ __forceinline__ bool trim_usual(const ColdParams &C) { return C.e_left_len <= 16 && C.e_right_len <= 32; }
 
 __device__ __forceinline__ TrimLoads trim_issue(const ColdParams &C, __amdgpu_buffer_rsrc_t rq, int off, int n) {
   const int pb = n >= 32 ? n - 32 : 0;
-  const uint32_t am = HPGQ_TRIM_ALIGNED ? ~3u : ~0u;
   TrimLoads T;
-  T.wl = v4u{0u, 0u, 0u, 0u};
-  T.wl4 = T.wr8 = 0u;
-  if (C.e_left_len > 0) {
-    T.wl = __builtin_amdgcn_raw_buffer_load_b128(rq, (uint32_t)off & am, 0, 0);
-    if (HPGQ_TRIM_ALIGNED) T.wl4 = __builtin_amdgcn_raw_buffer_load_b32(rq, ((uint32_t)off & am) + 16u, 0, 0);
-  }
+  T.wl = C.e_left_len > 0 ? __builtin_amdgcn_raw_buffer_load_b128(rq, (uint32_t)off, 0, 0) : v4u{0u, 0u, 0u, 0u};
   T.wr0 = T.wr1 = v4u{0u, 0u, 0u, 0u};
   if (C.e_right_len > 0) {
-    const uint32_t o = (uint32_t)(off + pb) & am;
-    T.wr0 = __builtin_amdgcn_raw_buffer_load_b128(rq, o, 0, 0);
-    T.wr1 = __builtin_amdgcn_raw_buffer_load_b128(rq, o + 16u, 0, 0);
-    if (HPGQ_TRIM_ALIGNED) T.wr8 = __builtin_amdgcn_raw_buffer_load_b32(rq, o + 32u, 0, 0);
+    T.wr0 = __builtin_amdgcn_raw_buffer_load_b128(rq, (uint32_t)(off + pb), 0, 0);
+    T.wr1 = __builtin_amdgcn_raw_buffer_load_b128(rq, (uint32_t)(off + pb + 16), 0, 0);
   }
   return T;
 }
@@ -267,33 +251,22 @@ __device__ __forceinline__ uint64_t trim_ok(const ColdParams &C, uint32_t x, uin
 
 __device__ __forceinline__ uint64_t trim_low_bytes(int k) { return k >= 8 ? ~0ull : ((1ull << (8 * max(k, 0))) - 1); }
 
-// the trims of a read of length n at quality offset off from its usual-window
-// loads: ts | te << 16
-__device__ __forceinline__ uint32_t trim_finish(const ColdParams &C, const TrimLoads &T, int off, int n) {
+// the trims of a read of length n from its usual-window loads: ts | te << 16
+__device__ __forceinline__ uint32_t trim_finish(const ColdParams &C, const TrimLoads &T, int n) {
   int ts = 0, te = 0;
   const int pb = n >= 32 ? n - 32 : 0;
-  // the windows' dwords (HPGQ_TRIM_ALIGNED: shifted into place)
-  uint32_t L[4] = {T.wl.x, T.wl.y, T.wl.z, T.wl.w};
-  uint32_t R[8] = {T.wr0.x, T.wr0.y, T.wr0.z, T.wr0.w, T.wr1.x, T.wr1.y, T.wr1.z, T.wr1.w};
-  if (HPGQ_TRIM_ALIGNED) {
-    const uint32_t al = (uint32_t)off & 3u, ar = (uint32_t)(off + pb) & 3u;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) L[k] = __builtin_amdgcn_alignbyte(k < 3 ? L[k + 1] : T.wl4, L[k], al);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) R[k] = __builtin_amdgcn_alignbyte(k < 7 ? R[k + 1] : T.wr8, R[k], ar);
-  }
   if (C.e_left_len > 0) {
     const int lim = min(C.e_left_len, n);
-    const uint64_t k0 = trim_ok(C, L[0], L[1], false) & trim_low_bytes(lim);
-    const uint64_t k1 = trim_ok(C, L[2], L[3], false) & trim_low_bytes(lim - 8);
+    const uint64_t k0 = trim_ok(C, T.wl.x, T.wl.y, false) & trim_low_bytes(lim);
+    const uint64_t k1 = trim_ok(C, T.wl.z, T.wl.w, false) & trim_low_bytes(lim - 8);
     ts = k0 ? (__builtin_ctzll(k0) >> 3) : k1 ? 8 + (__builtin_ctzll(k1) >> 3) : lim;
   }
   if (C.e_right_len > 0) {
     const int lim = min(C.e_right_len, n - ts);
     const int lo = n - lim - pb, hi = n - pb;   // positions [lo, hi) of the 32 loaded
     te = lim;
-    const uint64_t ok[4] = {trim_ok(C, R[0], R[1], true), trim_ok(C, R[2], R[3], true),
-                            trim_ok(C, R[4], R[5], true), trim_ok(C, R[6], R[7], true)};
+    const uint64_t ok[4] = {trim_ok(C, T.wr0.x, T.wr0.y, true), trim_ok(C, T.wr0.z, T.wr0.w, true),
+                            trim_ok(C, T.wr1.x, T.wr1.y, true), trim_ok(C, T.wr1.z, T.wr1.w, true)};
 #pragma unroll
     for (int k = 0; k < 4; ++k) {   // the last in-range byte wins (highest k last)
       const uint64_t m = ok[k] & trim_low_bytes(hi - 8 * k) & ~trim_low_bytes(lo - 8 * k);
@@ -310,7 +283,7 @@ __device__ __forceinline__ uint32_t trim_word(const ColdParams &C, __amdgpu_buff
     return trim_ok(C, w.x, w.y, right);
   };
   auto low_bytes = [](int k) -> uint64_t { return trim_low_bytes(k); };
-  if (trim_usual(C)) return trim_finish(C, trim_issue(C, rq, off, n), off, n);
+  if (trim_usual(C)) return trim_finish(C, trim_issue(C, rq, off, n), n);
   int ts = 0, te = 0;
   if (C.e_left_len > 0) {
     const int lim = min(C.e_left_len, n);
@@ -568,7 +541,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       int a = ia[m], e = ie[m];
       tw[m] = 0;
       if (EDIT) {   // trim here, then describe the trimmed window
-        tw[m] = !live ? 0u : usual ? trim_finish(cold, tl[m], bq[m] + a, e - a) : trim_word(cold, rq[m], bq[m] + a, e - a);
+        tw[m] = !live ? 0u : usual ? trim_finish(cold, tl[m], e - a) : trim_word(cold, rq[m], bq[m] + a, e - a);
         if (A.trim && live) A.trim[(size_t)m * (size_t)A.num_reads + rid] = tw[m];
         a += (int)(tw[m] & 0xFFFFu);
         e -= (int)(tw[m] >> 16);
