@@ -379,11 +379,35 @@ __device__ __forceinline__ int32_t idx_window(const SArgs &A, __amdgpu_buffer_rs
   return j <= n ? v : 0x7FFFFFFF;
 }
 
+// the same loads, raw (HPGQ_C5_RAW_WINDOW): the value and the toggle word as
+// loaded, made into the window (idx_at, tog_at) only where scatter_starts uses
+// them.  The window is loop-carried; any operation on a loaded value at the
+// loop's merge point (the select above) makes the wave wait there for that load
+// and, vmcnt being in order, for every load issued before it -- the tile bytes
+// prefetched for the tiles after this one.
+#ifndef HPGQ_C5_RAW_WINDOW
+#define HPGQ_C5_RAW_WINDOW 1
+#endif
+template <bool VALID>
+__device__ __forceinline__ int32_t idx_window_raw(const SArgs &A, __amdgpu_buffer_rsrc_t rt, int32_t r, int lane,
+                                                  uint32_t &tw) {
+  const int32_t j = r + lane, n = (int32_t)A.num_reads;
+  const int32_t v = A.idx[j <= n ? j : n];
+  if (VALID) tw = __builtin_amdgcn_raw_buffer_load_b32(rt, ((uint32_t)j >> 5) * 4u, 0, 0);
+  return v;
+}
+__device__ __forceinline__ int32_t idx_at(const SArgs &A, int32_t r, int lane, int32_t v) {
+  return r + lane <= (int32_t)A.num_reads ? v : 0x7FFFFFFF;
+}
+__device__ __forceinline__ uint32_t tog_at(int32_t r, int lane, uint32_t tw) {
+  return __builtin_amdgcn_ubfe(tw, (uint32_t)(r + lane) & 31u, 1);
+}
+
 // read starts in [base, limit) (limit - base <= 64 * kLaneBytes): bits into
 // the wave's LDS bitmap sc[64] (TOG: the validity toggles into tc[64]),
 // advancing the cursor r past them.  iw / itg are the window at r (loaded
-// ahead by the caller); they come back as the window at the new r, its load
-// in flight.  hop: the tile is its span's last, so the cursor moves on to rn
+// ahead by the caller; HPGQ_C5_RAW_WINDOW: raw, see idx_window_raw); they come
+// back as the window at the new r, its load in flight.  hop: the tile is its span's last, so the cursor moves on to rn
 // (the next span's first read) instead.
 template <bool VALID, bool TOG>
 __device__ __forceinline__ void scatter_starts(const SArgs &A, __amdgpu_buffer_rsrc_t rt, uint32_t *sc, uint32_t *tc,
@@ -400,7 +424,9 @@ __device__ __forceinline__ void scatter_starts(const SArgs &A, __amdgpu_buffer_r
     r += c;
     return c;
   };
-  if (__builtin_expect(put(iw, itg) == 64, 0)) {   // rare: more than 64 starts in the tile
+  const int32_t x0 = HPGQ_C5_RAW_WINDOW ? idx_at(A, r, lane, iw) : iw;
+  const uint32_t tg0 = HPGQ_C5_RAW_WINDOW && VALID ? tog_at(r, lane, itg) : itg;
+  if (__builtin_expect(put(x0, tg0) == 64, 0)) {   // rare: more than 64 starts in the tile
     int c;
     do {
       uint32_t tg = 0;
@@ -409,7 +435,7 @@ __device__ __forceinline__ void scatter_starts(const SArgs &A, __amdgpu_buffer_r
     } while (c == 64);
   }
   if (hop) r = rn;
-  iw = idx_window<VALID>(A, rt, r, lane, itg);
+  iw = HPGQ_C5_RAW_WINDOW ? idx_window_raw<VALID>(A, rt, r, lane, itg) : idx_window<VALID>(A, rt, r, lane, itg);
 }
 
 // a lane's bytes at o (o >= 0) from a buffer descriptor; bytes past the end read 0
@@ -727,7 +753,7 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
     int32_t r = sfirst[s];
     int32_t rn = sfirst[min(s + nwav, ns - 1)];
     uint32_t itg = 0;
-    int32_t iw = idx_window<VALID>(A, rt, r, lane, itg);
+    int32_t iw = HPGQ_C5_RAW_WINDOW ? idx_window_raw<VALID>(A, rt, r, lane, itg) : idx_window<VALID>(A, rt, r, lane, itg);
     uint32_t skA = 0, skB = 0;   // VALID: skip state at the tile starts
     {
       uint32_t cs[4] = {0x4E4E4E4Eu, 0x4E4E4E4Eu, 0x4E4E4E4Eu, 0x4E4E4E4Eu}, cq[2] = {0u, 0u};
