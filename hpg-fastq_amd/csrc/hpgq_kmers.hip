@@ -141,6 +141,9 @@ __device__ __forceinline__ Half half_of(const uint32_t (&pk)[5], const uint32_t 
   return H;
 }
 
+// MASK: mask is not null (a compile-time choice: a runtime one put a branch
+// around the mask load, whose merge made hipcc wait for every load in flight)
+template <bool MASK>
 __global__ void __launch_bounds__(kWG) kmer_tile_kernel(const char *seq, const int32_t *idx, int64_t n,
                                                         const uint8_t *mask, int npos, const int *maxlen,
                                                         uint32_t *slab) {
@@ -196,7 +199,7 @@ __global__ void __launch_bounds__(kWG) kmer_tile_kernel(const char *seq, const i
     const uint32_t ro = r <= n && lane <= kReadsPerWave ? (uint32_t)r : 0x3FFFFFF0u;
     R.ix = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(ri, ro * 4u, 0, 0);
     const bool on = r < n && lane < kReadsPerWave;
-    R.mk = mask ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rm, on ? (uint32_t)r : 0x3FFFFFF0u, 0, 0)
+    R.mk = MASK ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rm, on ? (uint32_t)r : 0x3FFFFFF0u, 0, 0)
                 : (on ? 1u : 0u);
     return R;
   };
@@ -236,28 +239,40 @@ __global__ void __launch_bounds__(kWG) kmer_tile_kernel(const char *seq, const i
     row[j] = 4u * (h + 16u * (uint32_t)hl);
   }
   constexpr uint32_t kIdBits = (uint32_t)(kNum - 1) << 7;   // id * 128 = id * kP * 4
-  // software pipeline: group g counted while g + stride's window and
-  // g + 2 stride's offsets are in flight
-  Meta cur = resolve(meta_raw(g0));
-  Win w = window(cur);
-  Raw nxt_raw = meta_raw(g0 + gstride);
-  for (int64_t g = g0; g < ngroups; g += gstride) {
+  // software pipeline: group g is counted while the windows of g + stride and
+  // g + 2 stride and the offsets of g + 3 stride are in flight.  Two register
+  // sets alternate (unrolled by two), so no loop-carried copy of a register
+  // whose load is pending makes the wave wait for it; each group's offsets
+  // are loaded before the window issued in the same step, so waiting for them
+  // (vmcnt is in order) never waits for that younger window.  (Round 3/4's
+  // one-group pipeline rotated its registers by copies, and the copies drained
+  // every load at the loop latch.)
+  // the starts of one group: c / wc (its offsets and window) are counted, then
+  // refilled with group g + 2 stride (offsets from rin, loaded a step ago);
+  // rout takes the offsets of g + 3 stride
+  auto step = [&](int64_t g, Meta &c, Win &wc, Raw &rin, Raw &rout) __attribute__((always_inline)) {
     // the read's last start, relative to the tile's first (< 0: none here;
     // masked-out reads: none)
-    const int last = cur.m == 1u ? min(cur.e - cur.a - kK, npos - 1) - p0 : -1;
+    const int last = c.m == 1u ? min(c.e - c.a - kK, npos - 1) - p0 : -1;
     uint32_t pk[5], bd[5];
-    const uint32_t ab = (uint32_t)cur.a & 3u;   // the window's byte offset in its first dword
-                                                // (p0 and 16 hl are multiples of 4)
-    const uint32_t wd[5] = {__builtin_amdgcn_alignbyte(w.a[1], w.a[0], ab), __builtin_amdgcn_alignbyte(w.a[2], w.a[1], ab),
-                            __builtin_amdgcn_alignbyte(w.a[3], w.a[2], ab), __builtin_amdgcn_alignbyte(w.c[0], w.a[3], ab),
-                            __builtin_amdgcn_alignbyte(w.c[1], w.c[0], ab)};
+    const uint32_t ab = (uint32_t)c.a & 3u;   // the window's byte offset in its first dword
+                                              // (p0 and 16 hl are multiples of 4)
+    const uint32_t wd[5] = {__builtin_amdgcn_alignbyte(wc.a[1], wc.a[0], ab), __builtin_amdgcn_alignbyte(wc.a[2], wc.a[1], ab),
+                            __builtin_amdgcn_alignbyte(wc.a[3], wc.a[2], ab), __builtin_amdgcn_alignbyte(wc.c[0], wc.a[3], ab),
+                            __builtin_amdgcn_alignbyte(wc.c[1], wc.c[0], ab)};
 #pragma unroll
     for (int i = 0; i < 5; ++i) codes4(wd[i], pk[i], bd[i]);
-    const Meta nxt = resolve(nxt_raw);   // (its loads were issued a group ago)
-    w = window(nxt);   // next group's window
-    cur = nxt;
-    nxt_raw = meta_raw(g + 2 * gstride);
-    if (__ballot(last >= 0) == 0ull) continue;   // the whole wave's reads end before these starts
+    // (the set's registers are dead here: keep the refill below this point, so
+    // the loads reuse them instead of living beside them -- else the loop
+    // latch copies a register whose load is pending, which waits for it)
+    __builtin_amdgcn_sched_barrier(0);
+    rout = meta_raw(g + 3 * gstride);
+    c = resolve(rin);
+    wc = window(c);
+    // (no early exit for a wave whose reads all end before these starts: a
+    // branch here lets hipcc sink the codes below the refill, and the set's
+    // registers then live beside their own refill -- copies that wait; such a
+    // wave adds zeros)
     const Half hf = half_of(pk, bd, last - 16 * hl, q);
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
@@ -268,6 +283,18 @@ __global__ void __launch_bounds__(kWG) kmer_tile_kernel(const char *seq, const i
       const uint32_t addr = __builtin_amdgcn_bitop3_b32(win, kIdBits, row[j], 0xEA);   // (a & b) | c
       atomicAdd(reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(t) + addr), __builtin_amdgcn_ubfe(hf.er, j, 1));
     }
+  };
+  Meta ca = resolve(meta_raw(g0));
+  Win wa = window(ca);
+  Raw ra = meta_raw(g0 + gstride), rb;
+  Meta cb = resolve(ra);
+  Win wb = window(cb);
+  rb = meta_raw(g0 + 2 * gstride);
+  // (no exit between the two steps: a group past the last has no counted
+  // read -- its offsets and mask bytes load as 0 -- and adds nothing)
+  for (int64_t g = g0; g < ngroups; g += 2 * gstride) {
+    step(g, ca, wa, rb, ra);
+    step(g + gstride, cb, wb, ra, rb);
   }
   __syncthreads();
   // the table goes to this workgroup's slab with plain coalesced stores;
@@ -395,8 +422,12 @@ int hpgq_kmers_count_device(hpgq_kmers_t *k, const hpgq_batch_t *b, const uint8_
       HPGQ_HIP_TRY(hipGetLastError());
       ml = k->d_maxlen;
     }
-    hipLaunchKernelGGL(kmer_tile_kernel, dim3((unsigned)k->grid), dim3(kWG), 0, k->stream, b->seq, ix, n, mk,
-                       k->npos, ml, k->d_slab);
+    if (mk)
+      hipLaunchKernelGGL(kmer_tile_kernel<true>, dim3((unsigned)k->grid), dim3(kWG), 0, k->stream, b->seq, ix, n, mk,
+                         k->npos, ml, k->d_slab);
+    else
+      hipLaunchKernelGGL(kmer_tile_kernel<false>, dim3((unsigned)k->grid), dim3(kWG), 0, k->stream, b->seq, ix, n, mk,
+                         k->npos, ml, k->d_slab);
     HPGQ_HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(kmer_reduce_kernel, dim3((unsigned)(((int64_t)tmax * kP * kNum + 255) / 256)), dim3(256), 0,
                        k->stream, (const uint32_t *)k->d_slab, k->npos, ml, k->grid, k->d_out);
