@@ -20,9 +20,13 @@
 // reads) exit at once instead of scanning every read.
 //   kmer_maxlen_kernel  max length over the counted reads (atomicMax)
 //   kmer_tile_kernel    two lanes per read and tile (20 bytes each: 16
-//                       starts + 4), software-pipelined (the next group's
-//                       bytes are fetched while this one is counted, its
-//                       offsets one group earlier still).  Table id-major,
+//                       starts + 4, loaded dword-aligned as 24 and shifted
+//                       into place by v_alignbyte: a misaligned 16-byte
+//                       gather costs the texture addresser far more),
+//                       software-pipelined two groups deep on two
+//                       alternating register sets (the windows of the next
+//                       two groups and the offsets of the one after are in
+//                       flight while a group is counted).  Table id-major,
 //                       cell (p, id) at id * 32 + p: a start position is an
 //                       LDS bank.  The 32 lanes of a group visit their starts
 //                       in rotated orders, so at every step they sit on 32
@@ -33,11 +37,8 @@
 //                       LUT for the 2-bit code and one for the exactness test;
 //                       per start: one v_alignbit (the lane's shift for that
 //                       step), one v_bitop3 (its position's bank), one v_bfe
-//                       (0 or 1) and the add.  Bound: the texture addresser
-//                       (tools/ubench/window_rates.hip: gathering a read's
-//                       36-byte tile window costs ~4.6 TA cycles per read and
-//                       tile in any lane shape, as much as streaming the whole
-//                       150-byte read; one lane per read was as fast but made
+//                       (0 or 1) and the add.  Bound: VALU issue beside the
+//                       window gathers (one lane per read made
 //                       1024-read groups whose L2 re-reads doubled the HBM
 //                       traffic).
 #include "hpgq_common.h"
