@@ -542,6 +542,9 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       tw[m] = 0;
       if (EDIT) {   // trim here, then describe the trimmed window
         tw[m] = !live ? 0u : usual ? trim_finish(cold, tl[m], e - a) : trim_word(cold, rq[m], bq[m] + a, e - a);
+#ifdef HPGQ_EDIT_ABL_NOTRIM   // timing-only ablation (wrong trims): no trim gathers, no trims
+        tw[m] = 0u;
+#endif
         if (A.trim && live) A.trim[(size_t)m * (size_t)A.num_reads + rid] = tw[m];
         a += (int)(tw[m] & 0xFFFFu);
         e -= (int)(tw[m] >> 16);
