@@ -227,6 +227,15 @@ __device__ __forceinline__ bool trim_usual(const ColdParams &C) { return C.e_lef
 __device__ __forceinline__ TrimLoads trim_issue(const ColdParams &C, __amdgpu_buffer_rsrc_t rq, int off, int n) {
   const int pb = n >= 32 ? n - 32 : 0;
   TrimLoads T;
+#if defined(HPGQ_EDIT_ABL_NOTRIM) && HPGQ_EDIT_ABL_NOTRIM == 3   // (timing-only: the windows made up, no loads)
+  {
+    const uint32_t x = (uint32_t)off * 0x9E3779B1u, y = (uint32_t)n * 0x85EBCA6Bu;
+    T.wl = v4u{x, y, x ^ y, x + y};
+    T.wr0 = v4u{y, x, x - y, x | y};
+    T.wr1 = v4u{x & y, ~x, ~y, x * 3u};
+    return T;
+  }
+#endif
   T.wl = C.e_left_len > 0 ? __builtin_amdgcn_raw_buffer_load_b128(rq, (uint32_t)off, 0, 0) : v4u{0u, 0u, 0u, 0u};
   T.wr0 = T.wr1 = v4u{0u, 0u, 0u, 0u};
   if (C.e_right_len > 0) {
@@ -542,7 +551,10 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       tw[m] = 0;
       if (EDIT) {   // trim here, then describe the trimmed window
         tw[m] = !live ? 0u : usual ? trim_finish(cold, tl[m], e - a) : trim_word(cold, rq[m], bq[m] + a, e - a);
-#ifdef HPGQ_EDIT_ABL_NOTRIM   // timing-only ablation (wrong trims): no trim gathers, no trims
+#ifdef HPGQ_EDIT_ABL_NOTRIM   // timing-only ablations (wrong trims): 1 no trim gathers, no trims;
+                              // 2 the trims computed (gathers and all), then not applied;
+                              // 3 computed from made-up windows (no gathers), not applied
+        if (HPGQ_EDIT_ABL_NOTRIM >= 2) asm volatile("" ::"v"(tw[m]));
         tw[m] = 0u;
 #endif
         if (A.trim && live) A.trim[(size_t)m * (size_t)A.num_reads + rid] = tw[m];
