@@ -193,11 +193,11 @@ def native_oracle():
     whose CPU is not the GPU box's.  Falls back to the portable build."""
     import subprocess
     import tempfile
-    src = os.path.join(ROOT, "oracle", "hpgq_oracle.c")
+    src = [os.path.join(ROOT, "oracle", f) for f in ("hpgq_oracle.c", "refarch.c")]
     tmp = tempfile.mkdtemp(prefix="hpgq_oracle_")
     out = os.path.join(tmp, "liboracle_native.so")
-    cmd = ["gcc", "-O3", "-march=native", "-std=c99", "-fopenmp", "-fPIC", "-ffp-contract=off",
-           "-shared", "-o", out, src]
+    cmd = ["gcc", "-O3", "-march=native", "-std=c99", "-fopenmp", "-pthread", "-fPIC", "-ffp-contract=off",
+           "-shared", "-o", out, *src, "-lm"]
     try:
         subprocess.run(cmd, check=True, capture_output=True, timeout=120)
         lib = C.CDLL(out)
@@ -314,11 +314,37 @@ def cpu_baseline(args, params):
         out["c1_stats_mreads_s"] = round(d1 / e1 / 1e6, 3)
         c1 = (f"; c1_stats_mreads_s: C1 `stats` without filter, same reads, {d1 // n} passes "
               f"in {e1:.1f} s")
+    if args.config == "c2":
+        out["refarch"] = refarch_baseline(lib, params, bs[0], n, budget=max(2.0, args.cpu_seconds / 3))
     out["sample"] = (f"{n} synthetic {L} bp {'pairs' if mates == 2 else 'reads'} (seed "
                      f"{args.seed}, same generator and options), {done // n} passes in "
                      f"{el:.1f} s; {what}, {threads} OpenMP threads (this GPU's CPU share; "
                      f"{ncores} visible); value_1thread: one pass on 1 thread ({el1:.1f} s){c1}")
     return out
+
+
+def refarch_baseline(lib, params, batch, n, budget):
+    """The reference's own stats architecture on the CPU (oracle/refarch.c):
+    2 worker threads (src/stats_options.c:21) build per-read records per
+    10,000-read batch (:22), ONE consumer merges them base by base through
+    hash maps (src/stats_fastq.c:257-417).  Context beside the OpenMP port,
+    never a target; timed on the first reads of the port's sample."""
+    lib.refarch_stats.restype = C.c_int
+    lib.refarch_stats.argtypes = [C.POINTER(H.Params), C.POINTER(H.Batch), C.c_int, C.c_int, C.c_void_p]
+    m = min(n, 400_000)
+    sub = H.Batch(m, batch.seq, batch.quality, batch.data_indices)
+    ctr = np.zeros(H.counters_len(params.lmax), np.uint64)
+    done, t0 = 0, time.perf_counter()
+    while True:
+        assert lib.refarch_stats(C.byref(params), C.byref(sub), 10_000, 2, ctr.ctypes.data) == 0
+        done += m
+        el = time.perf_counter() - t0
+        if el >= budget:
+            break
+    return {"value": round(done / el / 1e6, 3), "unit": "Mreads/s", "cores": 3, "kind": "refarch",
+            "sample": f"first {m} reads of the port's sample, {done // m} passes in {el:.1f} s: "
+                      "oracle/refarch.c, 2 worker threads (10,000-read batches) + 1 hash-map "
+                      "consumer thread, the shape of src/stats_fastq.c:202-417"}
 
 
 def read_status(n, seed, first=0):
@@ -597,6 +623,36 @@ def shard(args, rank):
     return [rank * args.reads, (rank + 1) * args.reads]
 
 
+def device_id(dev_index):
+    """PCI address and UUID of a HIP device (torch's device properties)."""
+    import torch
+    pr = torch.cuda.get_device_properties(dev_index)
+    pci = f"{getattr(pr, 'pci_domain_id', 0):04x}:{getattr(pr, 'pci_bus_id', 0):02x}:{getattr(pr, 'pci_device_id', 0):02x}"
+    return pci, str(getattr(pr, "uuid", ""))
+
+
+def rank_table(dist, world, mine):
+    """N > 1: every rank's record (rank, device, PCI address, timed seconds,
+    hot-kernel launch time) gathered on rank 0 over gloo, in rank order, so a
+    slow or shared rank is visible in the one line."""
+    got = [None] * world
+    dist.all_gather_object(got, mine)
+    return sorted(got, key=lambda g: g["rank"])
+
+
+def check_distinct_devices(ranks, share_device):
+    """Ranks on one node must hold distinct GPUs (one PCI function each) unless
+    --share-device asks for the functional shared run; returns an error or None."""
+    seen = {}
+    for g in ranks:
+        key = (g["pci"], g["uuid"])
+        if key in seen and not share_device:
+            return (f"bench: ranks {seen[key]} and {g['rank']} share device {g['pci']} "
+                    f"(uuid {g['uuid']}); pass --share-device for a functional run")
+        seen.setdefault(key, g["rank"])
+    return None
+
+
 def result_line(args, cfg, world, el, steps_reads, roofline, rccl_ranks, dtype, extra_config=None):
     cfgd = {"workload": cfg["workload"], "reads_per_gpu": args.reads, "read_length": args.read_length,
             "batch_reads": args.batch_reads,
@@ -623,6 +679,9 @@ def result_line(args, cfg, world, el, steps_reads, roofline, rccl_ranks, dtype, 
     }
 
 
+RANK_KEYS = ("rank", "device", "pci", "uuid", "el_s", "avg_launch_us")
+
+
 def dry_run_rank(args, world, rank):
     """--launch-dry-run: the rank plumbing on CPU.  Each rank derives its read
     range, fills the host offsets of its first reads with the same generator
@@ -639,7 +698,9 @@ def dry_run_rank(args, world, rank):
     s = H.Synth(args.seed, args.read_length, 5, 5, 1, 33, 0)
     idx = np.zeros(n + 1, np.int32)
     H.check(H.lib.hpgq_synth_indices_host(C.byref(s), lo, n, idx.ctypes.data), "idx")
-    mine = {"rank": rank, "range": [lo, hi], "first_bytes": int(idx[-1]), "pid": os.getpid()}
+    mine = {"rank": rank, "range": [lo, hi], "first_bytes": int(idx[-1]), "pid": os.getpid(),
+            # the per-rank record of a real N > 1 line (no device here)
+            "device": None, "pci": f"dry-run-{rank}", "uuid": "", "el_s": None, "avg_launch_us": None}
     t0 = time.perf_counter()
     got = [None] * world
     if world > 1:
@@ -655,9 +716,15 @@ def dry_run_rank(args, world, rank):
         if not ok:
             print(f"bench: bad shards {got}", file=sys.stderr)
             sys.exit(3)
-        out = result_line(args, cfg, world, None, 0, None, None, "u8",
-                          {"dry_run": True, "shards": [g["range"] for g in sorted(got, key=lambda g: g["rank"])],
-                           "rendezvous_s": round(el, 4)})
+        extra = {"dry_run": True, "shards": [g["range"] for g in sorted(got, key=lambda g: g["rank"])],
+                 "rendezvous_s": round(el, 4)}
+        if world > 1:
+            extra["ranks"] = [{k: g[k] for k in RANK_KEYS} for g in sorted(got, key=lambda g: g["rank"])]
+            err = check_distinct_devices(extra["ranks"], args.share_device)
+            if err:
+                print(err, file=sys.stderr)
+                sys.exit(3)
+        out = result_line(args, cfg, world, None, 0, None, None, "u8", extra)
         out["dry_run"] = True
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -802,14 +869,23 @@ def main():
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    if world > 1:   # max over ranks (gloo, host tensor)
-        t = torch.tensor([el], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
     if per_step:
         timed_ms = sum(a.elapsed_time(b) for a, b in ev)
     else:
         timed_ms = ev[0][0].elapsed_time(ev[-1][1])
+    ranks = None
+    if world > 1:
+        # every rank's own clock and hot-kernel time, then the max over ranks
+        pci, uuid = device_id(local_dev)
+        ranks = rank_table(dist, world, {"rank": rank, "device": local_dev, "pci": pci, "uuid": uuid,
+                                         "el_s": round(el, 6),
+                                         "avg_launch_us": round(timed_ms / (args.steps * nb) * 1e3, 1)})
+        el = max(g["el_s"] for g in ranks)
+        err = check_distinct_devices(ranks, args.share_device)
+        if err:
+            if rank == 0:
+                print(err, file=sys.stderr)
+            sys.exit(3)
 
     # sanity: every read accounted for (after the all-reduce: every rank's reads)
     if kmers:
@@ -848,6 +924,8 @@ def main():
                 "avg_launch_us": round(avg_launch_s * 1e6, 1),
                 "alg_bytes_per_launch": int(bytes_per_launch)}
     extra = {"route": args.route} if args.route else {}
+    if ranks is not None:
+        extra["ranks"] = ranks
     if args.share_device:
         extra["shared_device"] = f"{world} ranks on {ndev} device(s): functional run, not a scaling number"
     out = result_line(args, cfg, world, el, total, roofline, rccl_ranks, "f64" if cgr else "u8", extra)

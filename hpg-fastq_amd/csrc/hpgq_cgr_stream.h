@@ -69,23 +69,9 @@
 // for only when its bound would decide.
 #pragma once
 
-// Timing-only ablations of the per-byte loop (tools/gpu_c5_ablation_r04.sh;
-// the tables they leave are wrong, never built into the product):
-//   1: no table add (a VALU xor into a register instead of the ds_add_u64)
-//   2: the quality window chain replaced by a constant
-//   3: no emission mask (every byte adds to its word's cell)
-//   4: a 32-bit ds_add_u32 of the count only
-//   5: (exact) bytes that end no word skip the add by EXEC masking instead of
-//      adding to the lane's spare cell
-#ifndef HPGQ_C5_ABLATION
-#define HPGQ_C5_ABLATION 0
-#endif
-
-// tiles of bytes in flight per wave: 2 (fetch the next tile while this one
-// is counted) or 3 (fetch the one after it)
-#ifndef HPGQ_C5_DEPTH
-#define HPGQ_C5_DEPTH 3
-#endif
+// (The round-4 timing-only ablations of the per-byte loop are a patch,
+// tools/probes/c5_ablation.patch, applied by tools/probes/build_src_variant.sh:
+// the tables they leave are wrong, so they are not in the product source.)
 
 namespace hpgq {
 namespace cgr {
@@ -379,15 +365,12 @@ __device__ __forceinline__ int32_t idx_window(const SArgs &A, __amdgpu_buffer_rs
   return j <= n ? v : 0x7FFFFFFF;
 }
 
-// the same loads, raw (HPGQ_C5_RAW_WINDOW): the value and the toggle word as
-// loaded, made into the window (idx_at, tog_at) only where scatter_starts uses
-// them.  The window is loop-carried; any operation on a loaded value at the
-// loop's merge point (the select above) makes the wave wait there for that load
-// and, vmcnt being in order, for every load issued before it -- the tile bytes
-// prefetched for the tiles after this one.
-#ifndef HPGQ_C5_RAW_WINDOW
-#define HPGQ_C5_RAW_WINDOW 1
-#endif
+// the same loads, raw: the value and the toggle word as loaded, made into the
+// window (idx_at, tog_at) only where scatter_starts uses them.  The window is
+// loop-carried; any operation on a loaded value at the loop's merge point (the
+// select above) makes the wave wait there for that load and, vmcnt being in
+// order, for every load issued before it -- the tile bytes prefetched for the
+// tiles after this one (round 4: a vmcnt(0) per tile removed).
 template <bool VALID>
 __device__ __forceinline__ int32_t idx_window_raw(const SArgs &A, __amdgpu_buffer_rsrc_t rt, int32_t r, int lane,
                                                   uint32_t &tw) {
@@ -406,7 +389,7 @@ __device__ __forceinline__ uint32_t tog_at(int32_t r, int lane, uint32_t tw) {
 // read starts in [base, limit) (limit - base <= 64 * kLaneBytes): bits into
 // the wave's LDS bitmap sc[64] (TOG: the validity toggles into tc[64]),
 // advancing the cursor r past them.  iw / itg are the window at r (loaded
-// ahead by the caller; HPGQ_C5_RAW_WINDOW: raw, see idx_window_raw); they come
+// ahead by the caller, raw: see idx_window_raw); they come
 // back as the window at the new r, its load in flight.  hop: the tile is its span's last, so the cursor moves on to rn
 // (the next span's first read) instead.
 template <bool VALID, bool TOG>
@@ -424,8 +407,8 @@ __device__ __forceinline__ void scatter_starts(const SArgs &A, __amdgpu_buffer_r
     r += c;
     return c;
   };
-  const int32_t x0 = HPGQ_C5_RAW_WINDOW ? idx_at(A, r, lane, iw) : iw;
-  const uint32_t tg0 = HPGQ_C5_RAW_WINDOW && VALID ? tog_at(r, lane, itg) : itg;
+  const int32_t x0 = idx_at(A, r, lane, iw);
+  const uint32_t tg0 = VALID ? tog_at(r, lane, itg) : itg;
   if (__builtin_expect(put(x0, tg0) == 64, 0)) {   // rare: more than 64 starts in the tile
     int c;
     do {
@@ -435,7 +418,7 @@ __device__ __forceinline__ void scatter_starts(const SArgs &A, __amdgpu_buffer_r
     } while (c == 64);
   }
   if (hop) r = rn;
-  iw = HPGQ_C5_RAW_WINDOW ? idx_window_raw<VALID>(A, rt, r, lane, itg) : idx_window<VALID>(A, rt, r, lane, itg);
+  iw = idx_window_raw<VALID>(A, rt, r, lane, itg);
 }
 
 // a lane's bytes at o (o >= 0) from a buffer descriptor; bytes past the end read 0
@@ -498,7 +481,9 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
                                                         // that end no word do not collide)
   constexpr uint32_t kRun = 48 - K;
   // (VALID: the third tile's registers spill; it stays at 2)
-  constexpr int kDepth = !VALID && HPGQ_C5_DEPTH == 3 ? 3 : 2;
+  // tiles of bytes in flight per wave: 3 (the next two tiles fetched while
+  // this one is counted); the VALID kernel spills at 3 and keeps 2
+  constexpr int kDepth = !VALID ? 3 : 2;
   // per wave: start bitmaps of two tiles (this, next) + context; VALID: the
   // validity toggles of the two tiles
   constexpr int kBm = VALID ? 5 : 3;
@@ -520,7 +505,6 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
   const int32_t ns = (int32_t)nspans(a0, b1);
   const int32_t gw = (int32_t)blockIdx.x * kWaves + wid, nwav = (int32_t)gridDim.x * kWaves;
   bool risky = false;
-  uint32_t abl_sink = 0;   // (HPGQ_C5_ABLATION 1)
 
   // one descriptor pair per call: offsets past b1 + slack read zeros without
   // memory traffic (the context loads of tiles that enter no span, the
@@ -715,9 +699,7 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
                                      : c.p1 >> (sh - 64);
         const uint32_t w = win & M;   // M: the cell byte-address mask
         const int jo = j - K;   // the byte leaving the quality window
-        if (HPGQ_C5_ABLATION == 2) {
-          acc = 0x55u;
-        } else {
+        {
           const uint32_t qold = jo >= 0 ? __builtin_amdgcn_ubfe(qw[jo >> 2], 8 * (jo & 3), 8)
                                         : __builtin_amdgcn_ubfe(jo + kLaneBytes < kLaneBytes - 4 ? nq6 : nq7, 8 * (jo & 3), 8);
           acc = acc + __builtin_amdgcn_ubfe(qw[j >> 2], 8 * (j & 3), 8) - qold;
@@ -725,18 +707,9 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
         // addr = E bit j ? w : spare (v_bfe_i32 + v_bitop3; left to itself the
         // compiler spends three instructions on it)
         const uint32_t e = (uint32_t)__builtin_amdgcn_sbfe((int)E, j, 1);
-        const uint32_t addr = HPGQ_C5_ABLATION == 3 ? w : __builtin_amdgcn_bitop3_b32(e, w, spare, 0xCA);   // e ? w : spare
+        const uint32_t addr = __builtin_amdgcn_bitop3_b32(e, w, spare, 0xCA);   // e ? w : spare
         const unsigned long long inc = ((unsigned long long)acc << 32) | 1ull;
-        if (HPGQ_C5_ABLATION == 1)
-          abl_sink ^= addr + (uint32_t)(inc >> 32);
-        else if (HPGQ_C5_ABLATION == 5) {
-          if ((E >> j) & 1u)
-            atomicAdd(reinterpret_cast<unsigned long long *>(reinterpret_cast<char *>(tab) + w), inc);
-        }
-        else if (HPGQ_C5_ABLATION == 4)
-          atomicAdd(reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(tab) + addr), 1u);
-        else
-          atomicAdd(reinterpret_cast<unsigned long long *>(reinterpret_cast<char *>(tab) + addr), inc);
+        atomicAdd(reinterpret_cast<unsigned long long *>(reinterpret_cast<char *>(tab) + addr), inc);
       }
       // carry the last lane to the next tile's lane 0
       // (rotated by one lane: lane 0 holds lane 63's, the "old" operand of
@@ -753,7 +726,7 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
     int32_t r = sfirst[s];
     int32_t rn = sfirst[min(s + nwav, ns - 1)];
     uint32_t itg = 0;
-    int32_t iw = HPGQ_C5_RAW_WINDOW ? idx_window_raw<VALID>(A, rt, r, lane, itg) : idx_window<VALID>(A, rt, r, lane, itg);
+    int32_t iw = idx_window_raw<VALID>(A, rt, r, lane, itg);
     uint32_t skA = 0, skB = 0;   // VALID: skip state at the tile starts
     {
       uint32_t cs[4] = {0x4E4E4E4Eu, 0x4E4E4E4Eu, 0x4E4E4E4Eu, 0x4E4E4E4Eu}, cq[2] = {0u, 0u};
@@ -869,7 +842,6 @@ __global__ void __launch_bounds__(kWG) cgr_stream_kernel(SArgs A) {
     }
   }
   if (__ballot(risky) && lane == 0) atomicOr(A.gate, GATE_EXACT);
-  if (HPGQ_C5_ABLATION == 1 && abl_sink == 0x9E3779B9u) tab[lane] = 1ull;   // (keeps the sink live)
   __syncthreads();
   for (int i = threadIdx.x; i < cells; i += kWG) {
     const unsigned long long v = tab[i];

@@ -118,6 +118,15 @@ static void raw_range(int phred, int lo_q, int hi_q, uint32_t &lo4, uint32_t &hi
   hi4 = hib * 0x01010101u;
 }
 
+// the segmented kernels' branch-free form of one edit side's range (TrimSide)
+static void trim_side(uint32_t lo4, uint32_t hi4, int hi_none, int none_in, hpgq::TrimSide &S) {
+  if (none_in) lo4 = hi4 = 0;   // every byte >= both bounds: none in range
+  S.lq = lo4 ^ hpgq::kQFlip;
+  S.l7 = lo4 & 0x7F7F7F7Fu;
+  S.hq = hi_none && !none_in ? 0u : hi4 ^ hpgq::kQFlip;   // (no upper bound: ">= hi" never holds)
+  S.h7 = hi_none && !none_in ? hpgq::kQFlip : hi4 & 0x7F7F7F7Fu;
+}
+
 static int clamp_q(int q) { return q < -512 ? -512 : (q > 512 ? 512 : q); }
 
 // engine flags from the parameters
@@ -172,6 +181,8 @@ static void cold_params(const hpgq_params_t &p, hpgq::ColdParams &C) {
             C.el_lo_none, C.el_hi_none, C.el_none_in);
   raw_range(p.phred, p.edit_min_right_quality, p.edit_max_right_quality, C.er_lo4, C.er_hi4,
             C.er_lo_none, C.er_hi_none, C.er_none_in);
+  trim_side(C.el_lo4, C.el_hi4, C.el_hi_none, C.el_none_in, C.tl);
+  trim_side(C.er_lo4, C.er_hi4, C.er_hi_none, C.er_none_in, C.tr);
   int lo_none, hi_none, none_in;
   raw_range(p.phred, p.min_read_quality, p.max_read_quality, C.oor_lo4, C.oor_hi4, lo_none,
             hi_none, none_in);
@@ -927,25 +938,34 @@ int hpgq_debug_set_route(hpgq_ctx_t *c, int route) {
   if (r > HPGQ_ROUTE_FIRST_WIDE || (route & ~(0xF | HPGQ_ROUTE_NO_ADAPTIVE))) return HPGQ_E_INVALID;
   HPGQ_HIP_TRY(hipSetDevice(c->device));
   HPGQ_HIP_TRY(hipStreamSynchronize(c->stream));   // no call of the old chain in flight
-  if (c->h_report) (void)hipHostFree(c->h_report);
-  c->h_report = nullptr;
-  c->d_report = nullptr;
+  // plan the new route beside the old state (chains are plain values; the
+  // report word is the one resource) and swap it in only on success: a failed
+  // plan leaves the ctx exactly as it was
+  const Chain old0 = c->ch[0], old1 = c->ch[1];
+  const bool old_adaptive = c->adaptive;
+  uint32_t *const old_h = c->h_report, *const old_d = c->d_report;
+  const int old_route = c->route;
   c->ch[0] = Chain{};
   c->ch[1] = Chain{};
   c->adaptive = false;
+  c->h_report = c->d_report = nullptr;
+  c->route = route;
+  const int rc = plan(c, c->cus);
+  if (rc) {
+    if (c->h_report) (void)hipHostFree(c->h_report);   // (a plan that failed after its allocation)
+    c->ch[0] = old0;
+    c->ch[1] = old1;
+    c->adaptive = old_adaptive;
+    c->h_report = old_h;
+    c->d_report = old_d;
+    c->route = old_route;
+    return rc;
+  }
+  if (old_h) (void)hipHostFree(old_h);
   c->mode = 0;
   c->wide_calls = 0;
   c->min_seq = c->seq + 1;
-  const int old = c->route;
-  c->route = route;
-  const int rc = plan(c, c->cus);
-  if (rc) {   // back to the previous route
-    c->route = old;
-    c->ch[0] = Chain{};
-    c->ch[1] = Chain{};
-    (void)plan(c, c->cus);
-  }
-  return rc;
+  return HPGQ_OK;
 }
 
 }  // extern "C"

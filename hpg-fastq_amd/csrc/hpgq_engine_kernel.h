@@ -51,6 +51,17 @@ constexpr int kChunk = 252;       // positions per chunk (63 lanes x 4)
 constexpr int F_FILTER = 1, F_EDIT = 2, F_STATS = 4, F_NEED_N = 8, F_NEED_OOR = 16, F_NEED_LR = 32,
               F_OOR_LO_NONE = 64, F_OOR_HI_NONE = 128, F_OOR_ALL = 256;
 
+// One edit side's in-range test on RAW quality dwords w (biased b = w ^ 0x80,
+// range [lo, hi1) biased), branch-free: with x = w ^ 0x80 the SWAR "x >= c"
+// of bit 7 per byte is (~w & cq) | (~(w ^ cq) & ((w | 0x80) - c7)), cq = c ^
+// 0x80, c7 = c & 0x7F (trim_side_ok).  lq / l7 and hq / h7 are those of lo4
+// and hi4.  No upper bound: hq = 0, h7 = 0x80 (the formula is then 0 for
+// every byte); no lower bound: lo4 = 0 (always >=); an empty range: lo4 = hi4
+// = 0 (every byte >= both: none in range).
+struct TrimSide {
+  uint32_t lq, l7, hq, h7;
+};
+
 // parameters only the rarer paths read
 struct ColdParams {
   int left_len, min_left, max_left;
@@ -60,6 +71,7 @@ struct ColdParams {
   int el_lo_none, el_hi_none, el_none_in, er_lo_none, er_hi_none, er_none_in;
   uint32_t oor_lo4, oor_hi4;
   int max_n, max_oor;
+  TrimSide tl, tr;   // the edit windows' in-range tests (segmented kernels' trim_finish)
 };
 
 struct EngineArgs {

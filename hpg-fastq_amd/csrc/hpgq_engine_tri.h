@@ -50,25 +50,13 @@ constexpr int kTriSlack = 8;    // readable bytes past the data end the loads ma
 
 // The unit epilogue reads each read's length and trim word back from the read
 // table (LDS) instead of holding them in VGPRs across the unit's steps (4 per
-// mate: current and next unit), which the paired-end edit kernel spilled.
-#ifndef HPGQ_TAB_LEN
-#define HPGQ_TAB_LEN 1
-#endif
-// Paired-end edit, usual windows: both mates' trim loads in flight at once
-// (1), or one mate's loads issued and finished before the other's (0: no
-// TrimLoads of two mates live together).
-#ifndef HPGQ_PE_TRIM_OVERLAP
-#define HPGQ_PE_TRIM_OVERLAP 1
-#endif
-// The exact mean-quality sum (u64 per lane and mate) accumulates in per-lane
-// LDS slots (one no-return ds_add_u64 per unit) instead of a VGPR pair held
-// across the loop: the paired-end edit kernel spilled exactly those pairs,
-// a scratch load + store per unit and mate (~200 MB of scratch writes per
-// 10 M pairs).
-#ifndef HPGQ_FX_LDS
-#define HPGQ_FX_LDS 1
-#endif
-constexpr int kFxWords = HPGQ_FX_LDS ? 128 : 0;   // per wave and mate: 64 u64
+// mate: current and next unit), which the paired-end edit kernel spilled
+// (TABLEN below; the follow-up stages keep them in registers).  The exact
+// mean-quality sum (u64 per lane and mate) accumulates in per-lane LDS slots
+// (one no-return ds_add_u64 per unit) instead of a VGPR pair held across the
+// loop: the paired-end edit kernel spilled exactly those pairs, a scratch
+// load + store per unit and mate (~200 MB of scratch writes per 10 M pairs).
+constexpr int kFxWords = 128;   // per wave and mate: 64 u64
 
 constexpr int GEO_TRI = 0, GEO_HEX = 1, GEO_WIDE = 2;
 constexpr int X_NOOR = 1, X_LR = 2;   // extra filter scans (engine_tri_x_kernel)
@@ -216,75 +204,92 @@ using UndoTag = TriTag<2>;   // take back what the same step just added (nibble 
 // unit prologue, one lane per read.
 
 // the trim windows' quality bytes for the usual windows (left <= 16, right <=
-// 32): three 16-byte loads issued together, the right ones at pb = n - 32 (or
-// 0 for a short read, so no load starts before the read's own offset)
+// 32): three 16-byte loads issued together: the first 16 bytes of the read and
+// the 32 bytes ENDING at its end (from off + n - 32, even for a read shorter
+// than 32: the bytes before the read are the previous read's and lie before
+// any right window, so trim_finish needs no mask).  Only where that start
+// falls below the buffer (the first reads of a batch) do the loads start at 0
+// and hi = off + n < 32 marks the window's end (trim_finish masks past it).
+// Lanes without a read pass a negative offset (0xC0000000): out of range.
 struct TrimLoads {
   v4u wl, wr0, wr1;
+  int hi;   // the right window ends at byte hi of the 32 loaded (32 but at the buffer start)
 };
 
 __device__ __forceinline__ bool trim_usual(const ColdParams &C) { return C.e_left_len <= 16 && C.e_right_len <= 32; }
 
 __device__ __forceinline__ TrimLoads trim_issue(const ColdParams &C, __amdgpu_buffer_rsrc_t rq, int off, int n) {
-  const int pb = n >= 32 ? n - 32 : 0;
   TrimLoads T;
-#if defined(HPGQ_EDIT_ABL_NOTRIM) && HPGQ_EDIT_ABL_NOTRIM == 3   // (timing-only: the windows made up, no loads)
-  {
-    const uint32_t x = (uint32_t)off * 0x9E3779B1u, y = (uint32_t)n * 0x85EBCA6Bu;
-    T.wl = v4u{x, y, x ^ y, x + y};
-    T.wr0 = v4u{y, x, x - y, x | y};
-    T.wr1 = v4u{x & y, ~x, ~y, x * 3u};
-    return T;
-  }
-#endif
   T.wl = C.e_left_len > 0 ? __builtin_amdgcn_raw_buffer_load_b128(rq, (uint32_t)off, 0, 0) : v4u{0u, 0u, 0u, 0u};
   T.wr0 = T.wr1 = v4u{0u, 0u, 0u, 0u};
+  int pa = off + n - 32;
+  if (pa < 0 && off >= 0) pa = 0;
+  T.hi = off + n - pa;
   if (C.e_right_len > 0) {
-    T.wr0 = __builtin_amdgcn_raw_buffer_load_b128(rq, (uint32_t)(off + pb), 0, 0);
-    T.wr1 = __builtin_amdgcn_raw_buffer_load_b128(rq, (uint32_t)(off + pb + 16), 0, 0);
+    T.wr0 = __builtin_amdgcn_raw_buffer_load_b128(rq, (uint32_t)pa, 0, 0);
+    T.wr1 = __builtin_amdgcn_raw_buffer_load_b128(rq, (uint32_t)(pa + 16), 0, 0);
   }
   return T;
 }
 
-// 0x80 per in-range byte of raw quality words x, y (biased here, as the thresholds)
-__device__ __forceinline__ uint64_t trim_ok(const ColdParams &C, uint32_t x, uint32_t y, bool right) {
-  uint32_t lo, hi;
-  if (!right) {
-    lo = in_range(x ^ kQFlip, C.el_lo4, C.el_hi4, C.el_lo_none, C.el_hi_none, C.el_none_in);
-    hi = in_range(y ^ kQFlip, C.el_lo4, C.el_hi4, C.el_lo_none, C.el_hi_none, C.el_none_in);
-  } else {
-    lo = in_range(x ^ kQFlip, C.er_lo4, C.er_hi4, C.er_lo_none, C.er_hi_none, C.er_none_in);
-    hi = in_range(y ^ kQFlip, C.er_lo4, C.er_hi4, C.er_lo_none, C.er_hi_none, C.er_none_in);
+// v_ffbl / v_ffbh with the hardware's all-ones result for 0 (the builtins'
+// defined-at-zero forms add a compare and a select per dword)
+__device__ __forceinline__ uint32_t ffbl_raw(uint32_t x) {
+  uint32_t r;
+  asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+__device__ __forceinline__ uint32_t ffbh_raw(uint32_t x) {
+  uint32_t r;
+  asm("v_ffbh_u32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+
+// 0x80 per in-range byte of the raw quality dword w (TrimSide): >= the lower
+// bound and not >= the upper one, six VALU (w | 0x80 shared)
+__device__ __forceinline__ uint32_t trim_side_ok(uint32_t w, const TrimSide &S) {
+  const uint32_t wh = w | kQFlip;
+  const uint32_t ge_lo = (~w & S.lq) | (~(w ^ S.lq) & (wh - S.l7));
+  const uint32_t ge_hi = (~w & S.hq) | (~(w ^ S.hq) & (wh - S.h7));
+  return ge_lo & ~ge_hi & kQFlip;
+}
+
+// the trims of a read of length n from its usual-window loads: ts | te << 16.
+// Branch-free (round 5): ts = min(first in-range index of the left window,
+// min(left_len, n)); te = min(min(right_len, n - ts), hi - 1 - last in-range
+// index of the 32 bytes ending at the read's end).  A dword with no in-range
+// byte gives ffbl / ffbh = ~0, i.e. an index far past any window.
+__device__ __forceinline__ uint32_t trim_finish(const ColdParams &C, const TrimLoads &T, int n) {
+  const uint32_t wl[4] = {T.wl.x, T.wl.y, T.wl.z, T.wl.w};
+  const uint32_t wr[8] = {T.wr0.x, T.wr0.y, T.wr0.z, T.wr0.w, T.wr1.x, T.wr1.y, T.wr1.z, T.wr1.w};
+  uint32_t first = ~0u;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) first = min(first, (ffbl_raw(trim_side_ok(wl[w], C.tl)) >> 3) + 4u * w);
+  uint32_t okr[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) okr[k] = trim_side_ok(wr[k], C.tr);
+  if (__builtin_expect(T.hi < 32, 0)) {   // a read at the buffer start: bytes >= hi are the next read's
+#pragma unroll
+    for (int k = 0; k < 8; ++k) okr[k] &= byte_mask(T.hi - 4 * k);
   }
-  return (uint64_t)lo | ((uint64_t)hi << 32);
+  int last = -1;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) last = max(last, 4 * k + 3 - (int)(ffbh_raw(okr[k]) >> 3));
+  const int ts = (int)min(first, (uint32_t)min(C.e_left_len, n));
+  const int te = min(min(C.e_right_len, n - ts), T.hi - 1 - last);
+  return (uint32_t)ts | ((uint32_t)te << 16);
+}
+
+
+// 0x80 per in-range byte of raw quality words x, y (bytes 0-3, 4-7)
+__device__ __forceinline__ uint64_t trim_ok(const ColdParams &C, uint32_t x, uint32_t y, bool right) {
+  const TrimSide &S = right ? C.tr : C.tl;
+  return (uint64_t)trim_side_ok(x, S) | ((uint64_t)trim_side_ok(y, S) << 32);
 }
 
 __device__ __forceinline__ uint64_t trim_low_bytes(int k) { return k >= 8 ? ~0ull : ((1ull << (8 * max(k, 0))) - 1); }
 
-// the trims of a read of length n from its usual-window loads: ts | te << 16
-__device__ __forceinline__ uint32_t trim_finish(const ColdParams &C, const TrimLoads &T, int n) {
-  int ts = 0, te = 0;
-  const int pb = n >= 32 ? n - 32 : 0;
-  if (C.e_left_len > 0) {
-    const int lim = min(C.e_left_len, n);
-    const uint64_t k0 = trim_ok(C, T.wl.x, T.wl.y, false) & trim_low_bytes(lim);
-    const uint64_t k1 = trim_ok(C, T.wl.z, T.wl.w, false) & trim_low_bytes(lim - 8);
-    ts = k0 ? (__builtin_ctzll(k0) >> 3) : k1 ? 8 + (__builtin_ctzll(k1) >> 3) : lim;
-  }
-  if (C.e_right_len > 0) {
-    const int lim = min(C.e_right_len, n - ts);
-    const int lo = n - lim - pb, hi = n - pb;   // positions [lo, hi) of the 32 loaded
-    te = lim;
-    const uint64_t ok[4] = {trim_ok(C, T.wr0.x, T.wr0.y, true), trim_ok(C, T.wr0.z, T.wr0.w, true),
-                            trim_ok(C, T.wr1.x, T.wr1.y, true), trim_ok(C, T.wr1.z, T.wr1.w, true)};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {   // the last in-range byte wins (highest k last)
-      const uint64_t m = ok[k] & trim_low_bytes(hi - 8 * k) & ~trim_low_bytes(lo - 8 * k);
-      if (m) te = n - 1 - (pb + 8 * k + ((63 - __builtin_clzll(m)) >> 3));
-    }
-  }
-  return (uint32_t)ts | ((uint32_t)te << 16);
-}
-
+// any window: the usual ones by trim_finish, else 8 bytes at a time
 __device__ __forceinline__ uint32_t trim_word(const ColdParams &C, __amdgpu_buffer_rsrc_t rq,
                                               int off, int n) {
   auto ok8 = [&](int pos, bool right) __attribute__((always_inline)) -> uint64_t {
@@ -359,7 +364,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   // fails few reads and ran 4 % slower with it: 692 vs 665 us per 10 M reads)
   constexpr bool PF = NM == 1 && !EDIT && !FOLLOW && XM != X_LR;
   constexpr bool LATE = EDIT;   // the unit prologue's place (see the unit loop)
-  constexpr bool TABLEN = HPGQ_TAB_LEN && !FOLLOW;   // epilogue lengths / trims from the read table
+  constexpr bool TABLEN = !FOLLOW;   // epilogue lengths / trims from the read table
   // PEU (paired-end): a group is ONE step of both mates (grp[slot][m]); both
   // are added, the pair is decided from both scans at once (ds_bpermute), and
   // a failed pair is taken back out of the nibble counters from the registers
@@ -446,14 +451,12 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   };
   uint32_t *scratch = wtab + NM * kMateWaveWords;
   unsigned long long *dword = reinterpret_cast<unsigned long long *>(scratch + 64);   // 8 B aligned
-  // per-lane exact mean-quality sums (HPGQ_FX_LDS), 8 B aligned
+  // per-lane exact mean-quality sums, 8 B aligned
   auto fxs = [&](int m) __attribute__((always_inline)) {
     return reinterpret_cast<unsigned long long *>(scratch + 64 + 4 + m * kFxWords);
   };
-  if (HPGQ_FX_LDS) {
 #pragma unroll
-    for (int m = 0; m < NM; ++m) fxs(m)[lane] = 0ull;
-  }
+  for (int m = 0; m < NM; ++m) fxs(m)[lane] = 0ull;
   // byte masks by valid-byte count c = clamp(n - p0, 0, 4 NW): mtab[c][w]
   // (one LDS read per step instead of a clamp and a 64-bit shift per word)
   uint32_t *mtab = base + tab_words + kWaves * kWaveWords;   // 16 B aligned
@@ -482,13 +485,10 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
 #pragma unroll
   for (int m = 0; m < NM; ++m) acc[m].zero();
   int since_flush = 0;   // steps per mate added since the last LDS flush (a byte grows <= 1 per step)
-  uint64_t fx16[NM];
   uint32_t cnt[NM][5];   // input, passed, failed, edited, stats
 #pragma unroll
-  for (int m = 0; m < NM; ++m) {
-    fx16[m] = 0;
+  for (int m = 0; m < NM; ++m)
     for (int k = 0; k < 5; ++k) cnt[m][k] = 0;
-  }
   uint32_t ndefer = 0;   // reads this wave handed to the next stage
 
   const int ublock = FOLLOW ? A.unit_reads : kBlock;   // reads per unit
@@ -539,11 +539,11 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     // per mate; single-end keeps trim_word, whose registers fit better)
     TrimLoads tl[NM];
     const ColdParams &cold = cold_all;
-    const bool usual = HPGQ_PE_TRIM_OVERLAP && EDIT && NM == 2 && trim_usual(cold);
+    const bool usual = EDIT && NM == 2 && trim_usual(cold);
     if (usual) {
 #pragma unroll
       for (int m = 0; m < NM; ++m)
-        tl[m] = trim_issue(cold, rq[m], live ? bq[m] + ia[m] : (int)0x80000000, ie[m] - ia[m]);
+        tl[m] = trim_issue(cold, rq[m], live ? bq[m] + ia[m] : (int)0xC0000000, ie[m] - ia[m]);
     }
 #pragma unroll
     for (int m = 0; m < NM; ++m) {
@@ -551,12 +551,6 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       tw[m] = 0;
       if (EDIT) {   // trim here, then describe the trimmed window
         tw[m] = !live ? 0u : usual ? trim_finish(cold, tl[m], e - a) : trim_word(cold, rq[m], bq[m] + a, e - a);
-#ifdef HPGQ_EDIT_ABL_NOTRIM   // timing-only ablations (wrong trims): 1 no trim gathers, no trims;
-                              // 2 the trims computed (gathers and all), then not applied;
-                              // 3 computed from made-up windows (no gathers), not applied
-        if (HPGQ_EDIT_ABL_NOTRIM >= 2) asm volatile("" ::"v"(tw[m]));
-        tw[m] = 0u;
-#endif
         if (A.trim && live) A.trim[(size_t)m * (size_t)A.num_reads + rid] = tw[m];
         a += (int)(tw[m] & 0xFFFFu);
         e -= (int)(tw[m] >> 16);
@@ -567,7 +561,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       const uint32_t xq = live ? (uint32_t)(bq[m] + a) : 0x80000000u;
       // (FOLLOW: the read id rides in the record's spare dword, for the
       // epilogue; else the trim word, when the epilogue reads it back)
-      const uint32_t spare = FOLLOW || !HPGQ_TAB_LEN ? rid : tw[m];
+      const uint32_t spare = FOLLOW ? rid : tw[m];
       const v4u rec = v4u{xs & ~3u, xq & ~3u, n | ((xs & 3u) << 16) | ((xq & 3u) << 20), spare};
       *reinterpret_cast<v4u *>(tab(m, tb) + 4 * lane) = rec;
       len[m] = n;
@@ -1004,8 +998,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
             meanq_terms(s, wn, bin, fx);
             atomicAdd(&h[lp + 1 + bin], 1u);
             atomicAdd(&h[lp + 1 + HPGQ_MEANQ_BINS + (100 * gc) / wn], 1u);
-            if (HPGQ_FX_LDS) atomicAdd(&fxs(m)[lane], (unsigned long long)fx);   // (no return: ds_add_u64)
-            else fx16[m] += fx;
+            atomicAdd(&fxs(m)[lane], (unsigned long long)fx);   // (no return: ds_add_u64)
           }
         }
       }
@@ -1063,7 +1056,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   for (int m = 0; m < NM; ++m) {
     acc[m].widen();
     acc[m].flush(pos_acc(m), lp, p0);
-    const uint64_t tot = wave_sum64(HPGQ_FX_LDS ? (uint64_t)fxs(m)[lane] : fx16[m]);   // (LDS: in order per wave)
+    const uint64_t tot = wave_sum64((uint64_t)fxs(m)[lane]);   // (LDS: in order per wave)
     if (lane == 0) {
       unsigned long long *s = sc(m);
       if (cnt[m][0]) atomicAdd(&s[HPGQ_S_NUM_INPUT], (unsigned long long)cnt[m][0]);

@@ -54,6 +54,7 @@ typedef struct {
   char *cg_out;             /* raw u32 chaos-game tables dump (tests) */
   int quiet;
   int stream_writer;        /* filter / edit: one writer thread instead of mapped outputs */
+  int writer_hook;          /* tests only (--writer-test-hook): hpgq_mapout.h MAPOUT_HOOK_* */
 } cli_options_t;
 
 /* parse + validate (exits with the reference's messages on errors) */

@@ -117,7 +117,7 @@ static int exists(const char *path) {
 enum {
   O_THREADS = 1000, O_BATCH, O_QENC, O_KMERS, O_LRANGE, O_QRANGE, O_LLEN, O_LQRANGE, O_RLEN,
   O_RQRANGE, O_MAXN, O_MAXOOQ, O_GPU, O_LMAX, O_CHUNK, O_PRINT, O_COUNTERS, O_QUIET,
-  O_KMERSOUT, O_CG, O_KCG, O_GS, O_GPUS, O_CGBATCH, O_CGOUT, O_GPUW, O_STREAMW
+  O_KMERSOUT, O_CG, O_KCG, O_GS, O_GPUS, O_CGBATCH, O_CGOUT, O_GPUW, O_STREAMW, O_WHOOK
 };
 
 cli_options_t *cli_parse(int command, const char *exec_name, int argc, char **argv) {
@@ -170,6 +170,7 @@ cli_options_t *cli_parse(int command, const char *exec_name, int argc, char **ar
       {"kmers-out", required_argument, 0, O_KMERSOUT},
       {"quiet", no_argument, 0, O_QUIET},
       {"stream-writer", no_argument, 0, O_STREAMW},
+      {"writer-test-hook", required_argument, 0, O_WHOOK},
       {0, 0, 0, 0}};
   if (argc < 2) usage(o);
   optind = 1;
@@ -212,6 +213,7 @@ cli_options_t *cli_parse(int command, const char *exec_name, int argc, char **ar
       case O_CGOUT: o->cg_out = strdup(optarg); break;
       case O_QUIET: o->quiet = 1; break;
       case O_STREAMW: o->stream_writer = 1; break;
+      case O_WHOOK: o->writer_hook = atoi(optarg); break;   /* (tests: hpgq_mapout.h MAPOUT_HOOK_*) */
       default: usage(o);
     }
   }

@@ -55,6 +55,7 @@
 #include <unistd.h>
 
 #include "hpgq_cli.h"
+#include "hpgq_mapout.h"
 
 #define MAX_WORKERS 16
 #define MAX_SLOTS (2 * MAX_WORKERS + 2)
@@ -100,7 +101,8 @@ typedef struct {
   uint64_t written_pass, written_fail;
   /* mapped outputs: [0] passed / edit.fq, [1] failed.fq (NULL: not written) */
   int mmap_out;
-  char *map[2];
+  mapout_t mo;           /* the mappings: reservation, prefault threads, SIGBUS guard */
+  char *map[2];          /* (= mo.map) */
   size_t map_cap;
   uint64_t out_off[2];   /* bytes placed so far per output */
   int64_t placed;        /* chunks placed (in input order) */
@@ -595,6 +597,11 @@ static void run_parts(void *(*fn)(void *), copy_part_t *part, int n) {
   }
 }
 
+static void copy_part_run(void *arg) {
+  copy_part_t *cp = arg;
+  copy_records(cp->P, cp->s, cp->i0, cp->i1, cp->dst);
+}
+
 /* copier thread: takes parts off the queue; the last part of a chunk frees its
  * slot for the reader */
 static void *copier_main(void *arg) {
@@ -609,8 +616,10 @@ static void *copier_main(void *arg) {
     copy_part_t *cp = P->cq[P->cq_head % P->cq_cap];
     P->cq_head++;
     pthread_mutex_unlock(&P->cq_mu);
-    copy_records(cp->P, cp->s, cp->i0, cp->i1, cp->dst);
+    /* a store the file system cannot back ends the copy with HPGQ_E_IO, not SIGBUS */
+    const int e = mapout_guard(copy_part_run, cp);
     pthread_mutex_lock(&P->mu);
+    if (e && !P->error) P->error = e;
     if (--cp->s->parts_left == 0) {
       cp->s->state = 0;
       P->copies_pending--;
@@ -656,7 +665,7 @@ static void stop_copiers(pipe_t *P) {
  * parallel), place it after chunk k-1 (which only needs k-1's sizes, not its
  * copies), queue its parts for the copier threads (the slot stays busy, state
  * 3, until they are copied) */
-static int place_and_copy(pipe_t *P, slot_t *s) {
+static int place_and_copy(pipe_t *P, slot_t *s, int *handed) {
   copy_part_t *part = s->parts;
   int n = P->o->num_threads;
   const int64_t per_min = 16384;   /* records per copier at least */
@@ -684,10 +693,11 @@ static int place_and_copy(pipe_t *P, slot_t *s) {
     rc = -1;
   } else if (P->out_off[0] + sz[0] > P->map_cap || P->out_off[1] + sz[1] > P->map_cap) {
     rc = HPGQ_E_IO;   /* (cannot happen: each output is at most the input) */
-  } else {
+  } else if ((rc = mapout_error(&P->mo)) == 0) {   /* (a window the prefault threads could not back) */
     for (int c = 0; c < 2; ++c) {
       base[c] = P->out_off[c];
       P->out_off[c] += sz[c];
+      mapout_advance(&P->mo, c, P->out_off[c]);
     }
     P->placed++;
   }
@@ -705,16 +715,20 @@ static int place_and_copy(pipe_t *P, slot_t *s) {
     if (rec_class(P, s, i)) ++nfail;
     else ++npass;
   }
+  const int queue = s->nreads > 0;
   pthread_mutex_lock(&P->mu);
   P->written_pass += npass;
   P->written_fail += nfail;
-  if (s->nreads > 0) {   /* busy until copied (set before the parts can finish) */
+  if (queue) {   /* busy until copied (set before the parts can finish) */
     s->state = 3;
     s->parts_left = n;
     P->copies_pending++;
   }
   pthread_mutex_unlock(&P->mu);
-  if (s->nreads > 0) {
+  /* from here the copiers own the slot: the last part frees it and the reader
+   * may refill it at once, so neither this function nor the worker touches s */
+  *handed = queue;
+  if (queue) {
     pthread_mutex_lock(&P->cq_mu);
     for (int t = 0; t < n; ++t) P->cq[P->cq_tail++ % P->cq_cap] = &part[t];
     pthread_cond_broadcast(&P->cq_cv);
@@ -723,38 +737,28 @@ static int place_and_copy(pipe_t *P, slot_t *s) {
   return 0;
 }
 
-/* map the outputs for the parallel writer: each is at most the input (+ the
- * final newline the reader may add); 0 when mapped, else the stream writer runs */
+/* map the outputs for the parallel writer (hpgq_mapout.h): each is at most
+ * the input (+ the final newline the reader may add); 0 when mapped, 1: the
+ * stream writer runs (files left empty), < 0 an error */
 static int map_outputs(pipe_t *P) {
-  FILE *f[2] = {P->out_pass, P->out_fail};
+  const int fd[2] = {P->out_pass ? fileno(P->out_pass) : -1, P->out_fail ? fileno(P->out_fail) : -1};
   P->map_cap = (size_t)P->size + 4096;
-  /* a store into a mapped page the file system cannot back is a SIGBUS, not
-   * an error return: map only when the outputs (together at most the input)
-   * surely fit, else the stream writer reports ENOSPC as an I/O error */
-  struct statvfs vs;
-  if (!f[0] || fstatvfs(fileno(f[0]), &vs) ||
-      (unsigned long long)vs.f_bavail * vs.f_frsize < (unsigned long long)P->map_cap + (64ull << 20))
-    return -1;
-  for (int c = 0; c < 2; ++c) {
-    if (!f[c]) continue;
-    const int fd = fileno(f[c]);
-    struct stat st;
-    if (fstat(fd, &st) || !S_ISREG(st.st_mode) || ftruncate(fd, (off_t)P->map_cap)) return -1;
-    void *m = mmap(NULL, P->map_cap, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
-    if (m == MAP_FAILED) return -1;
-    P->map[c] = m;
-  }
+  /* prefault two chunks ahead of the placed records, on two threads (a third
+   * and fourth made one tmpfs file's page allocation slower, r04 probe) */
+  const size_t ahead = (size_t)2 * ((size_t)P->o->chunk_mb << 20);
+  const int rc = mapout_open(&P->mo, fd, P->map_cap, ahead, 2, P->o->writer_hook);
+  if (rc) return rc;
+  P->map[0] = P->mo.map[0];
+  P->map[1] = P->mo.map[1];
   P->mmap_out = 1;
   return 0;
 }
 
 static void unmap_outputs(pipe_t *P, int *rc) {
-  FILE *f[2] = {P->out_pass, P->out_fail};
-  for (int c = 0; c < 2; ++c) {
-    if (P->map[c]) munmap(P->map[c], P->map_cap);
-    P->map[c] = NULL;
-    if (f[c] && P->mmap_out && ftruncate(fileno(f[c]), (off_t)P->out_off[c]) && *rc == 0) *rc = HPGQ_E_IO;
-  }
+  const uint64_t size[2] = {P->out_off[0], P->out_off[1]};
+  const int e = mapout_close(&P->mo, size);
+  if (e && *rc == 0) *rc = e;
+  P->map[0] = P->map[1] = NULL;
 }
 
 /* one GPU worker: its own ctx, parser, k-mer and CGR accumulators on one device */
@@ -860,15 +864,17 @@ static void *worker_main(void *arg) {
     pthread_mutex_unlock(&P->mu);
     if (stop) break;
     trace_at(P, k, 2, W->w);
+    const size_t use = s->use;   /* (s is the copiers' once place_and_copy handed it over) */
+    int handed = 0;
     int rc = worker_chunk(W, s);
     if (rc == 0 && writes && P->mmap_out) {
-      rc = place_and_copy(P, s);   /* (an empty chunk is placed too: input order) */
+      rc = place_and_copy(P, s, &handed);   /* (an empty chunk is placed too: input order) */
     }
     trace_at(P, k, 4, -1);
-    W->fastq_bytes += (double)s->use;
+    W->fastq_bytes += (double)use;
     pthread_mutex_lock(&P->mu);
     if (rc && !P->error) P->error = rc;
-    if (s->state != 3) s->state = writes && rc == 0 && !P->mmap_out ? 2 : 0;   /* (3: the copiers free it) */
+    if (!handed) s->state = writes && rc == 0 && !P->mmap_out ? 2 : 0;   /* (handed: the copiers free it) */
     pthread_cond_broadcast(&P->cv);
     pthread_mutex_unlock(&P->mu);
     if (rc) {
@@ -950,22 +956,16 @@ int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, 
     if (!P.out_pass || ((!edit || o->filter_on) && !P.out_fail)) rc = HPGQ_E_INVALID;
     if (P.out_pass) setvbuf(P.out_pass, NULL, _IOFBF, 16 << 20);
     if (P.out_fail) setvbuf(P.out_fail, NULL, _IOFBF, 16 << 20);
-    if (rc == 0 && !o->stream_writer && map_outputs(&P)) {   /* not mappable: the writer thread */
-      FILE *f[2] = {P.out_pass, P.out_fail};
-      for (int c = 0; c < 2; ++c) {
-        if (P.map[c]) munmap(P.map[c], P.map_cap);
-        struct stat fs;
-        /* (a regular file map_outputs may have extended: back to empty) */
-        if (f[c] && fstat(fileno(f[c]), &fs) == 0 && S_ISREG(fs.st_mode) && ftruncate(fileno(f[c]), 0))
-          rc = HPGQ_E_IO;
-      }
-      P.map[0] = P.map[1] = NULL;
-      P.mmap_out = 0;
+    if (rc == 0 && !o->stream_writer) {   /* not mappable (1): the writer thread */
+      const int m = map_outputs(&P);
+      if (m < 0) rc = m;
     }
     res->writer = P.mmap_out ? 1 : 2;
-    if (P.trace)
-      fprintf(stderr, "hpg-fastq: writer: %s\n", P.mmap_out ? "mapped output files, parallel copy"
-                                                            : "one stream writer thread");
+    if (P.trace && P.mmap_out)
+      fprintf(stderr, "hpg-fastq: writer: mapped output files, parallel copy (windows reserved by %s)\n",
+              mapout_mode_name[__atomic_load_n(&P.mo.mode, __ATOMIC_RELAXED)]);
+    else if (P.trace)
+      fprintf(stderr, "hpg-fastq: writer: one stream writer thread\n");
   }
   if (rc) goto done;
 
@@ -985,8 +985,11 @@ int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, 
   pthread_join(reader, NULL);
   if (writer_thread) pthread_join(writer, NULL);
   if (P.mmap_out) stop_copiers(&P);   /* every placed chunk is in the maps */
+  /* the first error wins (P.error: a worker's, the reader's or a copier's;
+   * a worker that stopped on it afterwards returns a generic code) */
+  if (P.error)
+    rc = P.error < 0 && P.error != HPGQ_E_FORMAT && P.error != HPGQ_E_IO ? HPGQ_E_INVALID : P.error;
   for (int w = 0; w < G && rc == 0; ++w) rc = W[w].rc;
-  if (rc == 0 && P.error) rc = P.error < 0 && P.error != HPGQ_E_FORMAT ? HPGQ_E_INVALID : P.error;
 
   /* the read-sharded merge: device counters, k-mer and CGR tables summed over
    * the workers (u64; CGR u32, which wraps like the reference's tables) */

@@ -39,6 +39,23 @@ def test_launcher_spawns_ranks_and_shards_reads(n):
     assert line["n_gpus"] == n
     assert set(line) - {"dry_run"} == LINE_KEYS
     assert line["config"]["shards"] == [[k * 5000, (k + 1) * 5000] for k in range(n)]
+    # the per-rank diagnostics of an N > 1 line: one record
+    # per rank in rank order with its device, PCI address, clock and kernel time
+    ranks = line["config"]["ranks"]
+    assert [g["rank"] for g in ranks] == list(range(n))
+    assert all(set(g) == {"rank", "device", "pci", "uuid", "el_s", "avg_launch_us"} for g in ranks)
+    assert len({g["pci"] for g in ranks}) == n
+
+
+def test_distinct_device_check():
+    """Two ranks on one PCI function fail the run unless --share-device."""
+    sys.path.insert(0, ROOT)
+    import bench
+    same = [{"rank": 0, "pci": "0000:05:00", "uuid": "u"}, {"rank": 1, "pci": "0000:05:00", "uuid": "u"}]
+    assert "share device" in bench.check_distinct_devices(same, False)
+    assert bench.check_distinct_devices(same, True) is None
+    other = [{"rank": 0, "pci": "0000:05:00", "uuid": "u"}, {"rank": 1, "pci": "0000:15:00", "uuid": "v"}]
+    assert bench.check_distinct_devices(other, False) is None
 
 
 def test_one_gpu_line_shape_unchanged():
@@ -48,6 +65,7 @@ def test_one_gpu_line_shape_unchanged():
     assert line["n_gpus"] == 1
     assert set(line) - {"dry_run"} == LINE_KEYS
     assert "rccl_ranks" not in line["config"]   # only N > 1 lines carry it
+    assert "ranks" not in line["config"]
 
 
 def test_gpus_world_size_mismatch_fails():

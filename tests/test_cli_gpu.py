@@ -127,6 +127,43 @@ def test_cli_edit_outputs(tmp_path, writer):
     assert (tmp_path / "failed.fq").read_bytes() == b"".join(bad)
 
 
+def _filter_expected(reads):
+    p = H.filter_params(lmax=1024, read_quality_range="20,", read_length_range="50,")
+    mask, _, _ = O.run(p, reads)
+    recs = [h + sq + nl + plus + q + nl for (h, sq, plus, q, nl) in _records(reads)]
+    return (b"".join(r for r, m in zip(recs, mask) if m), b"".join(r for r, m in zip(recs, mask) if not m))
+
+
+def test_cli_writer_reservation_failure_uses_stream_writer(tmp_path):
+    """The mapped writer reserves each output's first window before using the
+    mapping (hpgq_mapout.c); when that fails (test hook in the options struct,
+    --writer-test-hook 1) the stream writer runs and the files are exact."""
+    reads = O.synth(15000, seed=31, L=150)
+    fq = _write(tmp_path, reads)
+    r = run_cli(["filter", "-f", fq, "-o", tmp_path, "--read-quality-range", "20,", "--read-length-range", "50,",
+                 "--chunk-mb", 1, "--quiet", "--writer-test-hook", 1], env={"HPGQ_TRACE": "1"})
+    assert WRITER_LINE["stream"] in r.stderr, r.stderr[-2000:]
+    passed, failed = _filter_expected(reads)
+    assert (tmp_path / "passed.fq").read_bytes() == passed
+    assert (tmp_path / "failed.fq").read_bytes() == failed
+
+
+@pytest.mark.parametrize("hook", [2, 4])
+def test_cli_writer_store_failure_is_io_error(tmp_path, hook):
+    """A prefault window the file system cannot back (hook 2), or a store into
+    a mapped page past the file's end -- what a file system filled by another
+    writer does to a mapping -- (hook 4: passed.fq shrinks to 0 behind its
+    mapping) ends the run with HPGQ_E_IO and exit status 1, not a SIGBUS."""
+    # (hook 2 needs an input past the 32 MB first window, which is reserved up front)
+    reads = O.synth(150000 if hook == 2 else 40000, seed=32, L=150)
+    fq = _write(tmp_path, reads)
+    r = run_cli(["filter", "-f", fq, "-o", tmp_path, "--read-quality-range", "20,", "--read-length-range", "50,",
+                 "--chunk-mb", 1, "--quiet", "--writer-test-hook", hook], check=False, env={"HPGQ_TRACE": "1"})
+    assert r.returncode == 1, (r.returncode, r.stderr[-2000:])   # (a SIGBUS death would be -7)
+    assert WRITER_LINE["mmap"] in r.stderr
+    assert "Error: file i/o error (-9)" in r.stderr, r.stderr[-2000:]
+
+
 def test_cli_writer_to_devices(tmp_path):
     """Outputs that cannot be mapped (here: symlinks to /dev/null) take the
     stream writer, and the run succeeds."""

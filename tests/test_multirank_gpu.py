@@ -107,3 +107,7 @@ def test_bench_launches_two_ranks(config):
     assert line["config"]["rccl_ranks"] == 2
     assert "shared_device" in line["config"]
     assert line["value"] > 0
+    ranks = line["config"]["ranks"]   # per-rank clock, kernel time and device
+    assert [g["rank"] for g in ranks] == [0, 1]
+    assert all(g["el_s"] > 0 and g["avg_launch_us"] > 0 and g["pci"] for g in ranks)
+    assert max(g["el_s"] for g in ranks) * 1e3 / 2 == pytest.approx(line["ms_per_step"], rel=1e-3, abs=1e-3)

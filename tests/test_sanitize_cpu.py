@@ -8,7 +8,9 @@
 The GPU pipeline threads are exercised by tests/test_cli_gpu.py."""
 import importlib.util
 import os
+import shutil
 import subprocess
+import tempfile
 
 import numpy as np
 import pytest
@@ -126,3 +128,22 @@ def test_report_quality_rows_run_to_key_zero(san, tmp_path):
     assert got == exp["read.quality.histogram.data"]
     keys = [int(line.split(b"\t")[0]) + 33 for line in got.splitlines()]
     assert keys[0] < 0 and keys[-1] == 0 and keys == list(range(keys[0], 1)), keys
+
+
+@pytest.mark.parametrize("mode", ["normal", "reserve", "populate", "sigbus"])
+def test_mapped_writer_failure_modes(san, mode):
+    """hpgq_mapout.c under ASan/UBSan, no GPU: the prefault
+    windows and guarded copies produce exact files; a failed first-window
+    reservation sends the pipeline to the stream writer with the files left
+    empty; a prefault window the file system cannot back is HPGQ_E_IO; a store
+    past the file's end (what a full file system does to a mapping) is caught
+    by the SIGBUS guard as HPGQ_E_IO and the process lives on.  The hooks are
+    the options struct's writer_hook (--writer-test-hook), not the environment."""
+    if not os.path.isdir("/dev/shm"):
+        pytest.skip("no /dev/shm (tmpfs)")
+    d = tempfile.mkdtemp(dir="/dev/shm", prefix="hpgq_mapout_")
+    try:
+        r = subprocess.run([str(san / "mapout_main"), mode, d], capture_output=True, text=True, timeout=300, env=ENV)
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+    assert r.returncode == 0 and f"mapout_main: ok {mode}" in r.stdout, r.stdout + r.stderr

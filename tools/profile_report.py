@@ -123,9 +123,20 @@ def main():
                     rec["lds_conflict_ratio"] = round(l2["SQ_LDS_BANK_CONFLICT"] / l2["SQ_LDS_IDX_ACTIVE"], 4)
                 if ta.get("GRBM_GUI_ACTIVE"):   # GRBM sums 8 XCDs, TA_TA_BUSY_sum 256 CUs
                     rec["ta_busy_frac"] = round(ta["TA_TA_BUSY_sum"] / 256 / (ta["GRBM_GUI_ACTIVE"] / 8), 4)
+        # the bench lines of this session carry THIS session's PMC bytes (bench.py
+        # copies whatever profiles/pmc_engine_<cfg>.json held when it ran, which
+        # is the previous session's: VERDICT r4 item 7)
+        src = (f"profiles/{a.round}_pmc_engine_{cfg}.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, "
+               "separate passes, same session)")
         cb = bench_line(os.path.join(PROF, f"bench_{cfg}.json"))
         if cb:
+            cb["roofline"]["traffic"] = rec["hbm_bytes_per_launch"]
+            cb["roofline"]["traffic_source"] = src
             json.dump(cb, open(os.path.join(OUT, f"{a.round}_bench_{cfg}.json"), "w"), indent=1)
+        if cfg == "c2" and b:
+            b["roofline"]["traffic"] = rec["hbm_bytes_per_launch"]
+            b["roofline"]["traffic_source"] = src
+            json.dump(b, open(os.path.join(OUT, f"{a.round}_bench.json"), "w"), indent=1)
         bt = glob.glob(os.path.join(PROF, f"btrace_{cfg}", "**", "run_kernel_stats.csv"), recursive=True)
         if bt:
             shutil.copy(bt[0], os.path.join(OUT, f"{a.round}_bench_{cfg}_kernel_stats.csv"))
