@@ -216,7 +216,7 @@ static void catch_all(Stage &s, int nm, int lmax, bool gen, bool follow) {
                 follow ? " (follow-up)" : "");
 }
 
-static size_t seg_lds(const hpgq_params_t &p, int nm, int xm, int pos) {
+static size_t seg_lds(const hpgq_params_t &p, int nm, int xm, int pos, bool follow = false, int block = 0) {
   const size_t lp = (size_t)std::min(p.lmax, pos);   // the kernel's on-chip positions (tri_body: lp)
   const size_t hlen = lp + 1 + HPGQ_MEANQ_BINS + HPGQ_GC_BINS;
   const size_t mate_words = (size_t)6 * lp + ((hlen + 1) & ~(size_t)1) + 2 * HPGQ_NUM_SCALARS;
@@ -225,8 +225,12 @@ static size_t seg_lds(const hpgq_params_t &p, int nm, int xm, int pos) {
   // extra scan) + the per-lane mean-quality sums, per wave a compaction scratch
   // and a deferral word
   const size_t lists = 1 + ((xm & hpgq::X_NOOR) ? 1 : 0) + ((xm & hpgq::X_LR) ? 1 : 0);
+  // (+ paired-end edit, first stage, no extra scans: the DMA rows of the next
+  // unit's trim windows, 3 x block x 16 B per mate, tri_body TDMA)
+  const bool tdma = p.edit_on && !follow && nm == 2 && xm == 0;
+  const size_t dma_words = tdma ? (size_t)nm * 3 * (size_t)block * 4 : 0;
   return (size_t)nm * mate_words * 4 + 16 + 17 * 16 +
-         (size_t)hpgq::kWaves * ((size_t)nm * (2 * 256 + 64 * lists + hpgq::kFxWords) + 64 + 4) * 4;
+         (size_t)hpgq::kWaves * ((size_t)nm * (2 * 256 + 64 * lists + hpgq::kFxWords) + 64 + 4 + dma_words) * 4;
 }
 
 static size_t catch_all_lds(const hpgq_params_t &p, int nm) {
@@ -301,13 +305,13 @@ static int plan_chain(hpgq_ctx *c, Chain &ch, int cus, int geo_force) {
   // a merged read longer than lmax leaves the segmented kernels (the
   // catch-all counts it as a long read)
   ch.s1.defer_len = stats ? std::min(pos1, p.lmax) : pos1;
-  int rc = finish_stage(c, ch.s1, seg_lds(p, c->nm, xm, pos1), cus);
+  int rc = finish_stage(c, ch.s1, seg_lds(p, c->nm, xm, pos1, false, seg_block(geo)), cus);
   if (rc) return rc;
   ch.has2 = geo != hpgq::GEO_WIDE && ch.s1.defer_len < posw && !(stats && p.lmax <= pos1);
   if (ch.has2) {
     if (!seg_stage(ch.s2, hpgq::GEO_WIDE, c->nm, edit, xm, true)) return HPGQ_E_INVALID;
     ch.s2.defer_len = stats ? std::min(posw, p.lmax) : posw;
-    rc = finish_stage(c, ch.s2, seg_lds(p, c->nm, xm, posw), cus);
+    rc = finish_stage(c, ch.s2, seg_lds(p, c->nm, xm, posw, true), cus);
     if (rc) return rc;
   }
   ch.has3 = true;

@@ -247,11 +247,14 @@ __device__ __forceinline__ uint32_t ffbh_raw(uint32_t x) {
 
 // 0x80 per in-range byte of the raw quality dword w (TrimSide): >= the lower
 // bound and not >= the upper one, six VALU (w | 0x80 shared)
+// (each compare is ONE v_bitop3 of (w, c ^ 0x80, (w | 0x80) - (c & 0x7F)):
+// truth table 0x8E = (~w & c') | (~(w ^ c') & d); hipcc left to itself spends
+// three instructions on it; the combine ge_lo & ~ge_hi & 0x80 is bitop3 0x20)
 __device__ __forceinline__ uint32_t trim_side_ok(uint32_t w, const TrimSide &S) {
   const uint32_t wh = w | kQFlip;
-  const uint32_t ge_lo = (~w & S.lq) | (~(w ^ S.lq) & (wh - S.l7));
-  const uint32_t ge_hi = (~w & S.hq) | (~(w ^ S.hq) & (wh - S.h7));
-  return ge_lo & ~ge_hi & kQFlip;
+  const uint32_t ge_lo = __builtin_amdgcn_bitop3_b32(w, S.lq, wh - S.l7, 0x8E);
+  const uint32_t ge_hi = __builtin_amdgcn_bitop3_b32(w, S.hq, wh - S.h7, 0x8E);
+  return __builtin_amdgcn_bitop3_b32(ge_lo, ge_hi, kQFlip, 0x20);
 }
 
 // the trims of a read of length n from its usual-window loads: ts | te << 16.
@@ -280,6 +283,20 @@ __device__ __forceinline__ uint32_t trim_finish(const ColdParams &C, const TrimL
   return (uint32_t)ts | ((uint32_t)te << 16);
 }
 
+
+// 16 bytes per lane from a buffer straight into LDS (buffer_load_dwordx4 ...
+// lds: lane l writes at lds + 16 l; no VGPR destination).  Inline asm, so the
+// compiler neither sees the LDS write (it would make every later LDS read of
+// the kernel wait for it: one exposed HBM round trip per unit again) nor
+// counts it: the reader waits for it explicitly (s_waitcnt vmcnt, in order).
+// M0 (the LDS base) is saved and restored around it.
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t lds) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(rs), "s"(lds)
+               : "memory");
+}
 
 // 0x80 per in-range byte of raw quality words x, y (bytes 0-3, 4-7)
 __device__ __forceinline__ uint64_t trim_ok(const ColdParams &C, uint32_t x, uint32_t y, bool right) {
@@ -376,6 +393,14 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   constexpr int NW = GG::kNW, kSegs = GG::kSegs, kSegW = GG::kSegW, kBlock = GG::kBlock, kU = GG::kU;
   static_assert(4 * kU <= kNibbleEvery && kBlock / kSegs - 4 * kU <= kNibbleEvery, "nibble widening");
   static_assert(kSegs * kSegW <= 64 && kBlock < 64 && kBlock % kSegs == 0, "geometry");
+  // TDMA (paired-end edit, first stage, no extra scans -- whose LDS would not
+  // fit at 3 workgroups per CU): a unit's trim windows come from LDS, DMA'd
+  // there during the unit before's last group pair, instead of gathers whose
+  // round trip the unit prologue waited for.  Round 5, one
+  // box: c4_pe 1578 -> 1500 us; single-end measured no faster (its lines,
+  // fetched earlier, are evicted before the stream comes back for them: HBM
+  // traffic 1.34 -> 1.40x, C4 824 -> 840 us), so single-end keeps the gathers.
+  constexpr bool TDMA = EDIT && !FOLLOW && NM == 2 && XM == 0;
   if (FOLLOW && follow_up_idle(A)) return;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x;
@@ -440,7 +465,10 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     return reinterpret_cast<unsigned long long *>(base + m * mate_words + 6 * lp + hist_words);
   };
   constexpr int kMateWaveWords = 2 * 256 + 64 * (1 + (NX ? 1 : 0) + (LR ? 1 : 0));
-  constexpr int kWaveWords = NM * kMateWaveWords + 64 + 4 + NM * kFxWords;   // (multiple of 4: 16 B tables)
+  // TDMA: the next unit's trim windows, DMA'd one unit ahead (see dma_windows):
+  // per mate three rows (left, right 0, right 1) of kBlock x 16 B
+  constexpr int kDmaWords = TDMA ? NM * 3 * kBlock * 4 : 0;
+  constexpr int kWaveWords = NM * kMateWaveWords + 64 + 4 + NM * kFxWords + kDmaWords;   // (multiple of 4: 16 B tables)
   const int tab_words = (NM * mate_words + 3) & ~3;   // 16 B aligned (host: + 16 B)
   uint32_t *wtab = base + tab_words + wave * kWaveWords;
   auto tab = [&](int m, int tb) __attribute__((always_inline)) { return wtab + m * kMateWaveWords + tb * 256; };
@@ -451,6 +479,10 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   };
   uint32_t *scratch = wtab + NM * kMateWaveWords;
   unsigned long long *dword = reinterpret_cast<unsigned long long *>(scratch + 64);   // 8 B aligned
+  // the DMA rows of mate m, window w (16 B aligned)
+  auto dma_row = [&](int m, int w) __attribute__((always_inline)) {
+    return scratch + 64 + 4 + NM * kFxWords + (m * 3 + w) * kBlock * 4;
+  };
   // per-lane exact mean-quality sums, 8 B aligned
   auto fxs = [&](int m) __attribute__((always_inline)) {
     return reinterpret_cast<unsigned long long *>(scratch + 64 + 4 + m * kFxWords);
@@ -512,7 +544,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   // and deferred reads get length 0 and out-of-range offsets.  Returns this
   // lane's lengths (the epilogue needs them) and the deferred-lane mask.
   auto load_block = [&](const Unit &U, int tb, uint32_t (&len)[NM], uint32_t (&tw)[NM], uint64_t &dm,
-                        const int32_t (&ia)[NM], const int32_t (&ie)[NM]) __attribute__((always_inline)) {
+                        const int32_t (&ia)[NM], const int32_t (&ie)[NM], bool dma) __attribute__((always_inline)) {
     const bool on = lane < U.nr;
     const uint32_t rid = (uint32_t)(U.u * ublock) + (FOLLOW ? scratch[lane] : (uint32_t)lane);
     bool dfr = false;
@@ -534,13 +566,27 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       if (lane == 0) A.defer_bits[U.u] = pbits;
       ndefer += (uint32_t)__builtin_popcountll(dm);
     }
-    // EDIT (paired-end), usual windows: both mates' trim loads in flight
+    // EDIT, usual windows: from the DMA rows (dma: the windows were DMA'd
+    // during the unit before, and waited for by the caller), else (the first
+    // unit; paired-end kernels without TDMA) both mates' trim loads in flight
     // before the first is finished (one exposed round trip per unit, not one
-    // per mate; single-end keeps trim_word, whose registers fit better)
+    // per mate; single-end without TDMA keeps trim_word)
     TrimLoads tl[NM];
     const ColdParams &cold = cold_all;
-    const bool usual = EDIT && NM == 2 && trim_usual(cold);
-    if (usual) {
+    const bool fromdma = TDMA && dma && trim_usual(cold);
+    const bool usual = EDIT && (fromdma || (NM == 2 && trim_usual(cold)));
+    if (fromdma) {
+#pragma unroll
+      for (int m = 0; m < NM; ++m) {
+        const int off = live ? bq[m] + ia[m] : (int)0xC0000000, n = ie[m] - ia[m];
+        tl[m].wl = *reinterpret_cast<const v4u *>(dma_row(m, 0) + 4 * lane);
+        tl[m].wr0 = *reinterpret_cast<const v4u *>(dma_row(m, 1) + 4 * lane);
+        tl[m].wr1 = *reinterpret_cast<const v4u *>(dma_row(m, 2) + 4 * lane);
+        int pa = off + n - 32;
+        if (pa < 0 && off >= 0) pa = 0;
+        tl[m].hi = off + n - pa;
+      }
+    } else if (usual) {
 #pragma unroll
       for (int m = 0; m < NM; ++m)
         tl[m] = trim_issue(cold, rq[m], live ? bq[m] + ia[m] : (int)0xC0000000, ie[m] - ia[m]);
@@ -761,9 +807,35 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   int32_t ia[NM], ie[NM];   // offsets of the unit after the next one to be described
   Unit cur = it.next(), nxt = Unit{-1, 0, 0};
   for (int m = 0; m < NM; ++m) len[m] = lenn[m] = tw[m] = twn[m] = 0;
+  // TDMA: unit U's trim windows (lane j: read j's first 16 quality bytes and
+  // the 32 ending at its end, as trim_issue) into the wave's DMA rows, issued
+  // at the top of the unit before it, so they land while that unit streams
+  // (the offsets ia / ie of U were fetched a unit ahead).  Deferred and absent
+  // reads load from past the descriptor's range: no traffic.
+  auto dma_windows = [&](const Unit &U) __attribute__((always_inline)) {
+    if (lane >= kBlock) return;
+    const bool on = lane < U.nr;
+    bool dfr = false;
+#pragma unroll
+    for (int m = 0; m < NM; ++m) dfr = dfr || (ie[m] - ia[m] > dlim);
+    const bool live = on && !dfr;
+#pragma unroll
+    for (int m = 0; m < NM; ++m) {
+      const int off = bq[m] + ia[m], n = ie[m] - ia[m];
+      int pa = off + n - 32;
+      if (pa < 0) pa = 0;
+      const uint32_t kOut = 0x80000000u;
+      if (cold_all.e_left_len > 0)
+        dma16(rq[m], live ? (uint32_t)off : kOut, (uint32_t)(uintptr_t)dma_row(m, 0));
+      if (cold_all.e_right_len > 0) {
+        dma16(rq[m], live ? (uint32_t)pa : kOut, (uint32_t)(uintptr_t)dma_row(m, 1));
+        dma16(rq[m], live ? (uint32_t)pa + 16u : kOut, (uint32_t)(uintptr_t)dma_row(m, 2));
+      }
+    }
+  };
   if (cur.u >= 0) {
     fetch_idx(cur, ia, ie);
-    load_block(cur, tb, len, tw, dm, ia, ie);
+    load_block(cur, tb, len, tw, dm, ia, ie, false);
     nxt = it.next();
     fetch_idx(nxt, ia, ie);
     if (PEU) load_group_pe(tb, steps_of(cur, dm), 0, 0);
@@ -780,13 +852,28 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     // the algorithmic bytes); else at the unit start, a unit ahead.
     Unit nn2 = Unit{-1, 0, 0};
     int nnt = 0;
-    auto describe_next = [&]() __attribute__((always_inline)) {
-      load_block(nxt, tb ^ 1, lenn, twn, dmn, ia, ie);
+    // TDMA: the DMA rows are filled at the start of this unit's last group
+    // pair (issue_dma: about one group of work before the next unit's
+    // prologue reads them; a unit earlier their lines left L2 before the
+    // stream came back for them, +0.5 GB of HBM traffic per C4 launch);
+    // `drained`: no load was issued after them (a wholly deferred unit), else
+    // at least that pair's second group's four (two steps x two buffers; PEU:
+    // a step of both mates) were, and vmcnt counts in order
+    const bool tdma = TDMA && trim_usual(cold_all);
+    // (not at the loop's top: a use of the offsets there, a merge point, waited
+    // for every load in flight)
+    auto issue_dma = [&]() __attribute__((always_inline)) {
+      if (tdma && nxt.u >= 0) dma_windows(nxt);
+    };
+    auto describe_next = [&](bool drained) __attribute__((always_inline)) {
+      if (tdma && drained) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else if (tdma) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      load_block(nxt, tb ^ 1, lenn, twn, dmn, ia, ie, true);
       nn2 = it.next();
       fetch_idx(nn2, ia, ie);
       nnt = steps_of(nxt, dmn);
     };
-    if (!LATE) describe_next();
+    if (!LATE) describe_next(false);
     if (stats && since_flush > kByteEvery - kBlock / kSegs) {   // keep every byte <= 255
 #pragma unroll
       for (int m = 0; m < NM; ++m) acc[m].flush(pos_acc(m), lp, p0);
@@ -860,11 +947,12 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
         if (m + 1 < NM) {
           load_group(m + 1 < NM ? m + 1 : 0, tb, nt, 0, slot);
         } else {
-          if (LATE) describe_next();
+          if (LATE) describe_next(false);
           load_group(0, tb ^ 1, nnt, 0, slot);
         }
       };
       for (int g = 0; g < ngroups; g += 2) {
+        if (m == NM - 1 && g + 2 >= ngroups) issue_dma();   // (the unit's last group pair)
         load_group(m, tb, nt, g + 1, 1);
         process_group(g, 0);
         if (g + 2 < ngroups) load_group(m, tb, nt, g + 2, 0);
@@ -906,12 +994,13 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     if (PEU && ngroups > 0) {
       const int ng = (nt + 1) & ~1;   // one step per group, an even count
       for (int g = 0; g < ng; g += 2) {
+        if (g + 2 >= ng) issue_dma();   // (the unit's last group pair)
         load_group_pe(tb, nt, g + 1, 1);
         process_pair(g, 0);
         if (g + 2 < ng) {
           load_group_pe(tb, nt, g + 2, 0);
         } else {
-          if (LATE) describe_next();
+          if (LATE) describe_next(false);
           load_group_pe(tb ^ 1, nnt, 0, 0);
         }
         process_pair(g + 1, 1);
@@ -924,10 +1013,12 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       run_mate(MateTag<0>{});
       if (NM == 2) run_mate(MateTag<NM - 1>{});
     } else if (PEU) {
-      if (LATE) describe_next();
+      issue_dma();
+      if (LATE) describe_next(true);
       load_group_pe(tb ^ 1, nnt, 0, 0);   // a wholly deferred unit: straight to the next
     } else {
-      if (LATE) describe_next();
+      issue_dma();
+      if (LATE) describe_next(true);
       load_group(0, tb ^ 1, nnt, 0, 0);   // a wholly deferred unit: straight to the next
     }
     since_flush += nt;

@@ -690,7 +690,7 @@ static int place_and_copy(pipe_t *P, slot_t *s, int *handed) {
   pthread_mutex_lock(&P->mu);
   while (P->placed != s->chunk && !P->error) pthread_cond_wait(&P->cv, &P->mu);
   if (P->error) {
-    rc = -1;
+    rc = P->error;   /* (stop; a copier's HPGQ_E_IO reaches the caller as is) */
   } else if (P->out_off[0] + sz[0] > P->map_cap || P->out_off[1] + sz[1] > P->map_cap) {
     rc = HPGQ_E_IO;   /* (cannot happen: each output is at most the input) */
   } else if ((rc = mapout_error(&P->mo)) == 0) {   /* (a window the prefault threads could not back) */
@@ -985,11 +985,11 @@ int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, 
   pthread_join(reader, NULL);
   if (writer_thread) pthread_join(writer, NULL);
   if (P.mmap_out) stop_copiers(&P);   /* every placed chunk is in the maps */
-  /* the first error wins (P.error: a worker's, the reader's or a copier's;
-   * a worker that stopped on it afterwards returns a generic code) */
-  if (P.error)
-    rc = P.error < 0 && P.error != HPGQ_E_FORMAT && P.error != HPGQ_E_IO ? HPGQ_E_INVALID : P.error;
   for (int w = 0; w < G && rc == 0; ++w) rc = W[w].rc;
+  /* (the reader's and writer's generic -1 is HPGQ_E_INVALID; a copier's or the
+   * prefault threads' HPGQ_E_IO stays what it is) */
+  if (rc == 0 && P.error)
+    rc = P.error < 0 && P.error != HPGQ_E_FORMAT && P.error != HPGQ_E_IO ? HPGQ_E_INVALID : P.error;
 
   /* the read-sharded merge: device counters, k-mer and CGR tables summed over
    * the workers (u64; CGR u32, which wraps like the reference's tables) */

@@ -59,6 +59,17 @@ def main():
         rec["hbm_bytes"] = rec["fetch_bytes_x2"] + rec["write_bytes"]
         if "alg" in rec:
             rec["traffic_over_alg"] = round(rec["hbm_bytes"] / rec["alg"], 4)
+    for d in sorted(glob.glob(os.path.join(top, "sq1_*"))):
+        if not os.path.isdir(d):
+            continue
+        key = os.path.basename(d)[4:]
+        cfg = key.split("_", 1)[1] if key.split("_", 1)[0] not in KERNELS and "_" in key and \
+            key.split("_", 1)[1] in ("c2", "c3", "c4", "c4_pe", "c4_noor", "c5", "c5_valid", "c2_kmers") else key
+        name = key[:-len(cfg) - 1] if cfg != key else "base"
+        a = pmc(d, KERNELS[cfg]) or {}
+        b = pmc(d.replace("sq1_", "sq2_"), KERNELS[cfg]) or {}
+        rec = out.setdefault(f"{name} {cfg}", {})
+        rec["sq"] = {**a, **b}
     for k, v in out.items():
         print(k, {x: y for x, y in v.items() if x not in ("us",)})
     if "--json" in sys.argv:

@@ -46,11 +46,17 @@ for v in $VARIANTS; do
     done
   done
 done
-unset HPGQ_LIB_PATH
-for spec in $SQ; do
-  IFS=: read cfg mode n L extra <<< "$spec"
-  A="python tools/prof_engine.py --mode $mode --reads $n --L $L --iters 3 $extra"
-  timeout -k 10 120 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH -d $O/sq1_$cfg -o run --output-format csv -- $A > $O/sq1_$cfg.log 2>&1 || exit 6
-  timeout -k 10 120 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS -d $O/sq2_$cfg -o run --output-format csv -- $A > $O/sq2_$cfg.log 2>&1 || exit 6
+# SQ passes: the in-tree build, or every variant with SQVAR=1 (sq1_<name>_<cfg>)
+for v in $([ -n "$SQVAR" ] && echo $VARIANTS || echo "base=."); do
+  name=${v%%=*}; lib=${v#*=}
+  if [ "$lib" = . ]; then unset HPGQ_LIB_PATH; else export HPGQ_LIB_PATH=$PWD/$lib; fi
+  tag=$([ -n "$SQVAR" ] && echo "${name}_" || echo "")
+  for spec in $SQ; do
+    IFS=: read cfg mode n L extra <<< "$spec"
+    A="python tools/prof_engine.py --mode $mode --reads $n --L $L --iters 3 $extra"
+    timeout -k 10 120 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH -d $O/sq1_$tag$cfg -o run --output-format csv -- $A > $O/sq1_$tag$cfg.log 2>&1 || exit 6
+    timeout -k 10 120 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_LDS -d $O/sq2_$tag$cfg -o run --output-format csv -- $A > $O/sq2_$tag$cfg.log 2>&1 || exit 6
+  done
 done
+unset HPGQ_LIB_PATH
 echo done > $O/DONE
