@@ -517,10 +517,13 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
 #pragma unroll
   for (int m = 0; m < NM; ++m) acc[m].zero();
   int since_flush = 0;   // steps per mate added since the last LDS flush (a byte grows <= 1 per step)
-  uint32_t cnt[NM][5];   // input, passed, failed, edited, stats
+  // per-wave counts: input and passed reads (pairs) are the same for both
+  // mates and failed = input - passed (a pass is valid), stats = passed when
+  // stats are on; only the edited count is per mate (SGPRs are short in the
+  // paired-end kernels: five counters per mate spilled into VGPR lanes)
+  uint32_t cnt_in = 0, cnt_pass = 0, cnt_ed[NM];
 #pragma unroll
-  for (int m = 0; m < NM; ++m)
-    for (int k = 0; k < 5; ++k) cnt[m][k] = 0;
+  for (int m = 0; m < NM; ++m) cnt_ed[m] = 0;
   uint32_t ndefer = 0;   // reads this wave handed to the next stage
 
   const int ublock = FOLLOW ? A.unit_reads : kBlock;   // reads per unit
@@ -1070,15 +1073,13 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     const uint64_t failed = __ballot(valid && !pass);
     const uint32_t npass = (uint32_t)__builtin_popcountll(__ballot(pass));
     const uint32_t nvalid = (uint32_t)(nr - __builtin_popcountll(dm));
+    cnt_in += nvalid;
+    cnt_pass += npass;
 #pragma unroll
     for (int m = 0; m < NM; ++m) {
       const int n = (int)len[m];
-      if (EDIT) cnt[m][3] += (uint32_t)__builtin_popcountll(__ballot(valid && tw[m] != 0u));
-      cnt[m][0] += nvalid;
-      cnt[m][1] += npass;
-      cnt[m][2] += (uint32_t)__builtin_popcountll(failed);
+      if (EDIT) cnt_ed[m] += (uint32_t)__builtin_popcountll(__ballot(valid && tw[m] != 0u));
       if (stats) {
-        cnt[m][4] += npass;
         if (pass) {   // (reads longer than lmax were deferred: every pass merges)
           const uint32_t gc = r1[m] >> 18, wn = (uint32_t)n, s = r1[m] & 0x3FFFFu;
           uint32_t *h = hist(m);
@@ -1150,11 +1151,11 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     const uint64_t tot = wave_sum64((uint64_t)fxs(m)[lane]);   // (LDS: in order per wave)
     if (lane == 0) {
       unsigned long long *s = sc(m);
-      if (cnt[m][0]) atomicAdd(&s[HPGQ_S_NUM_INPUT], (unsigned long long)cnt[m][0]);
-      if (cnt[m][1]) atomicAdd(&s[HPGQ_S_NUM_PASSED], (unsigned long long)cnt[m][1]);
-      if (cnt[m][2]) atomicAdd(&s[HPGQ_S_NUM_FAILED], (unsigned long long)cnt[m][2]);
-      if (cnt[m][3]) atomicAdd(&s[HPGQ_S_NUM_EDITED], (unsigned long long)cnt[m][3]);
-      if (cnt[m][4]) atomicAdd(&s[HPGQ_S_NUM_STATS], (unsigned long long)cnt[m][4]);
+      if (cnt_in) atomicAdd(&s[HPGQ_S_NUM_INPUT], (unsigned long long)cnt_in);
+      if (cnt_pass) atomicAdd(&s[HPGQ_S_NUM_PASSED], (unsigned long long)cnt_pass);
+      if (cnt_in - cnt_pass) atomicAdd(&s[HPGQ_S_NUM_FAILED], (unsigned long long)(cnt_in - cnt_pass));
+      if (cnt_ed[m]) atomicAdd(&s[HPGQ_S_NUM_EDITED], (unsigned long long)cnt_ed[m]);
+      if (stats && cnt_pass) atomicAdd(&s[HPGQ_S_NUM_STATS], (unsigned long long)cnt_pass);
       if (tot) atomicAdd(&s[HPGQ_S_ACC_MEANQ_FX16], (unsigned long long)tot);
     }
   }

@@ -149,7 +149,7 @@ int mapout_open(mapout_t *m, const int fd[2], size_t cap, size_t ahead, int thre
   }
   pthread_mutex_init(&m->mu, NULL);
   pthread_cond_init(&m->cv, NULL);
-  if (threads < 1) threads = 1;
+  if (threads < 0) threads = 0;   /* (0: only the reserved first window; copies fault the rest in) */
   if (threads > MAPOUT_MAX_PF) threads = MAPOUT_MAX_PF;
   for (int t = 0; t < threads; ++t) {
     if (pthread_create(&m->th[t], NULL, pf_main, m)) break;

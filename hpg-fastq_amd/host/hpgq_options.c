@@ -104,7 +104,9 @@ static void usage(const cli_options_t *o) {
     printf("  --cg-out=<file>                 Write the raw u32 chaos-game tables + word count\n");
   if (o->command != CMD_STATS)
     printf("  --stream-writer                 Write the FastQ outputs through one writer thread\n"
-           "                                  (default: mapped output files filled in parallel)\n");
+           "                                  (default: mapped output files filled in parallel)\n"
+           "  --copy-threads=<int>            Mapped writer: copier threads (default --num-threads)\n"
+           "  --prefault-threads=<int>        Mapped writer: threads populating the outputs ahead (default 2)\n");
   printf("  --quiet                         No parameter / result display\n");
   exit(-1);
 }
@@ -117,7 +119,7 @@ static int exists(const char *path) {
 enum {
   O_THREADS = 1000, O_BATCH, O_QENC, O_KMERS, O_LRANGE, O_QRANGE, O_LLEN, O_LQRANGE, O_RLEN,
   O_RQRANGE, O_MAXN, O_MAXOOQ, O_GPU, O_LMAX, O_CHUNK, O_PRINT, O_COUNTERS, O_QUIET,
-  O_KMERSOUT, O_CG, O_KCG, O_GS, O_GPUS, O_CGBATCH, O_CGOUT, O_GPUW, O_STREAMW, O_WHOOK
+  O_KMERSOUT, O_CG, O_KCG, O_GS, O_GPUS, O_CGBATCH, O_CGOUT, O_GPUW, O_STREAMW, O_WHOOK, O_COPYT, O_PFT
 };
 
 cli_options_t *cli_parse(int command, const char *exec_name, int argc, char **argv) {
@@ -138,6 +140,7 @@ cli_options_t *cli_parse(int command, const char *exec_name, int argc, char **ar
   o->k_cg = 7;   /* DEFAULT_K_IN_CHAOS_GAME */
   o->cg_batch_size = 64000000;   /* DEFAULT_BATCH_SIZE_MB * 1000000, old/main_hpg_fastq_old.c:116 */
   o->gpu_workers = 2;
+  o->prefault_threads = -1;
   static const struct option longopts[] = {
       {"help", no_argument, 0, 'h'},
       {"fastq-file", required_argument, 0, 'f'},
@@ -171,6 +174,8 @@ cli_options_t *cli_parse(int command, const char *exec_name, int argc, char **ar
       {"quiet", no_argument, 0, O_QUIET},
       {"stream-writer", no_argument, 0, O_STREAMW},
       {"writer-test-hook", required_argument, 0, O_WHOOK},
+      {"copy-threads", required_argument, 0, O_COPYT},
+      {"prefault-threads", required_argument, 0, O_PFT},
       {0, 0, 0, 0}};
   if (argc < 2) usage(o);
   optind = 1;
@@ -214,6 +219,8 @@ cli_options_t *cli_parse(int command, const char *exec_name, int argc, char **ar
       case O_QUIET: o->quiet = 1; break;
       case O_STREAMW: o->stream_writer = 1; break;
       case O_WHOOK: o->writer_hook = atoi(optarg); break;   /* (tests: hpgq_mapout.h MAPOUT_HOOK_*) */
+      case O_COPYT: o->copy_threads = atoi(optarg); break;
+      case O_PFT: o->prefault_threads = atoi(optarg); break;
       default: usage(o);
     }
   }

@@ -631,7 +631,7 @@ static void *copier_main(void *arg) {
 }
 
 static int start_copiers(pipe_t *P) {
-  int n = P->o->num_threads;
+  int n = P->o->copy_threads > 0 ? P->o->copy_threads : P->o->num_threads;
   if (n > 64) n = 64;
   if (n < 1) n = 1;
   P->cq_cap = P->nslots * MAX_COPIERS;
@@ -746,7 +746,8 @@ static int map_outputs(pipe_t *P) {
   /* prefault two chunks ahead of the placed records, on two threads (a third
    * and fourth made one tmpfs file's page allocation slower, r04 probe) */
   const size_t ahead = (size_t)2 * ((size_t)P->o->chunk_mb << 20);
-  const int rc = mapout_open(&P->mo, fd, P->map_cap, ahead, 2, P->o->writer_hook);
+  const int pft = P->o->prefault_threads < 0 ? 2 : P->o->prefault_threads;
+  const int rc = mapout_open(&P->mo, fd, P->map_cap, ahead, pft, P->o->writer_hook);
   if (rc) return rc;
   P->map[0] = P->mo.map[0];
   P->map[1] = P->mo.map[1];
