@@ -142,8 +142,12 @@ struct TriAcc {
   // bytes -> LDS (pos_acc [6][lmax]: qsum, A, C, G, T, N/other); nibbles empty
   __device__ __forceinline__ void flush(uint32_t *pos_acc, int lmax, int p0) {
     // rare (every <= 255 steps): keep its 40 LDS addresses out of the hot
-    // loop's registers (hipcc would hoist them as loop invariants and spill)
-    asm volatile("" : "+v"(p0), "+s"(lmax), "+s"(pos_acc));
+    // loop's registers (hipcc would hoist them as loop invariants and spill).
+    // Only the indices pass through the asm: a pointer that did came out of it
+    // generic, so these adds became FLAT atomics, and a FLAT operation that may
+    // be in flight makes the wait-count pass wait for every load (vmcnt(0))
+    // at each use of a streamed group, all through the unit loop
+    asm volatile("" : "+v"(p0), "+s"(lmax));
 #pragma unroll
     for (int w = 0; w < NW; ++w) {
       const uint32_t qv[4] = {q02[w] & 0xFFFFu, q13[w] & 0xFFFFu, q02[w] >> 16, q13[w] >> 16};
@@ -175,7 +179,7 @@ __device__ __forceinline__ uint32_t tri_codes(uint32_t s, uint32_t m, uint32_t &
 // and one "other" count per position (sign: +1 add, -1 subtract)
 __device__ __forceinline__ uint32_t tri_fix(uint32_t s, uint32_t m, uint32_t codes, uint32_t *other,
                                             int lmax, int pos0, uint32_t sign) {
-  asm volatile("" : "+v"(pos0), "+s"(lmax), "+s"(other));   // rare path: no hoisted addresses
+  asm volatile("" : "+v"(pos0), "+s"(lmax));   // rare path: no hoisted addresses (indices only: see flush)
   const uint32_t ex = __builtin_amdgcn_perm(kX7Hi, kX7Lo, codes);
   const uint32_t ff = nonzero_bytes((s ^ ex) & m);
   if (ff) {
@@ -955,11 +959,22 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
         }
       };
       for (int g = 0; g < ngroups; g += 2) {
-        if (m == NM - 1 && g + 2 >= ngroups) issue_dma();   // (the unit's last group pair)
+        const bool last = g + 2 >= ngroups;
+        if (m == NM - 1 && last) issue_dma();   // (the unit's last group pair)
         load_group(m, tb, nt, g + 1, 1);
         process_group(g, 0);
-        if (g + 2 < ngroups) load_group(m, tb, nt, g + 2, 0);
-        else load_next_unit(0);
+        if (NM == 1) {
+          // ONE load site for slot 0, this unit's next group or the next unit's
+          // first: with two (if / else), the wait-count pass merged their
+          // pending loads at the join and made process_group(g + 1) wait for
+          // the loads just issued (vmcnt(0): a full HBM round trip per pair)
+          if (LATE && last) describe_next(false);
+          load_group(0, last ? tb ^ 1 : tb, last ? nnt : nt, last ? 0 : g + 2, 0);
+        } else if (!last) {
+          load_group(m, tb, nt, g + 2, 0);
+        } else {
+          load_next_unit(0);
+        }
         process_group(g + 1, 1);
         // nibbles hold at most 15 steps: widen after groups 0-3 and at the end
         if (stats && g == 2) acc[m].widen();
@@ -1000,12 +1015,9 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
         if (g + 2 >= ng) issue_dma();   // (the unit's last group pair)
         load_group_pe(tb, nt, g + 1, 1);
         process_pair(g, 0);
-        if (g + 2 < ng) {
-          load_group_pe(tb, nt, g + 2, 0);
-        } else {
-          if (LATE) describe_next(false);
-          load_group_pe(tb ^ 1, nnt, 0, 0);
-        }
+        const bool last = g + 2 >= ng;   // (one load site for slot 0, as in run_mate)
+        if (LATE && last) describe_next(false);
+        load_group_pe(last ? tb ^ 1 : tb, last ? nnt : nt, last ? 0 : g + 2, 0);
         process_pair(g + 1, 1);
         if (stats && ((g + 2) & 7) == 0)   // nibbles hold at most 15 steps
           for (int m = 0; m < NM; ++m) acc[m].widen();

@@ -149,6 +149,7 @@ int mapout_open(mapout_t *m, const int fd[2], size_t cap, size_t ahead, int thre
   }
   pthread_mutex_init(&m->mu, NULL);
   pthread_cond_init(&m->cv, NULL);
+  m->live = 1;
   if (threads < 0) threads = 0;   /* (0: only the reserved first window; copies fault the rest in) */
   if (threads > MAPOUT_MAX_PF) threads = MAPOUT_MAX_PF;
   for (int t = 0; t < threads; ++t) {
@@ -222,7 +223,7 @@ int mapout_guard(void (*fn)(void *), void *arg) {
 
 int mapout_close(mapout_t *m, const uint64_t size[2]) {
   int rc = 0;
-  if (m->nth) {
+  if (m->live) {
     pthread_mutex_lock(&m->mu);
     m->stop = 1;
     pthread_cond_broadcast(&m->cv);
@@ -232,6 +233,7 @@ int mapout_close(mapout_t *m, const uint64_t size[2]) {
     rc = m->err;
     pthread_mutex_destroy(&m->mu);
     pthread_cond_destroy(&m->cv);
+    m->live = 0;
   }
   const int mapped = m->map[0] || m->map[1];
   unmap_all(m);

@@ -51,6 +51,7 @@ typedef struct {
   pthread_cond_t cv;
   size_t want[2], next[2];
   int stop, err;
+  int live;               /* mu / cv initialised (a successful mapout_open) */
   int mode;               /* how windows are reserved: MAPOUT_POPULATE / _FALLOCATE / _UNRESERVED */
 } mapout_t;
 

@@ -6,6 +6,8 @@
 //   populate  madvise(MADV_POPULATE_WRITE) of each chunk, then the memset
 //   falloc    fallocate() of each chunk, then the memset (faults map
 //             pages already in the page cache)
+//   huge      madvise(MADV_HUGEPAGE) on the mapping, then first-touch faults
+//             (2 MB tmpfs pages where shmem_enabled allows "advise")
 // One JSON line per (mode, threads).
 //   gcc -O2 -pthread tmpfs_fill.c -o tmpfs_fill && ./tmpfs_fill /dev/shm 3000000000
 #define _GNU_SOURCE
@@ -23,8 +25,8 @@
 #define MADV_POPULATE_WRITE 23
 #endif
 
-enum { FAULT, POPULATE, FALLOC };
-static const char *names[] = {"fault", "populate", "falloc"};
+enum { FAULT, POPULATE, FALLOC, HUGE };
+static const char *names[] = {"fault", "populate", "falloc", "huge"};
 
 typedef struct {
   char *map;
@@ -57,7 +59,15 @@ int main(int argc, char **argv) {
   char path[4096];
   snprintf(path, sizeof path, "%s/hpgq_fill.tmp", dir);
   const int tlist[] = {1, 4, 8, 16};
-  for (int mode = 0; mode < 3; ++mode) {
+  char thp[256] = "?";
+  FILE *f = fopen("/sys/kernel/mm/transparent_hugepage/shmem_enabled", "r");
+  if (f) {
+    if (!fgets(thp, sizeof thp, f)) thp[0] = 0;
+    fclose(f);
+    thp[strcspn(thp, "\n")] = 0;
+  }
+  printf("{\"shmem_enabled\": \"%s\"}\n", thp);
+  for (int mode = 0; mode < 4; ++mode) {
     for (int ti = 0; ti < 4; ++ti) {
       const int T = tlist[ti];
       unlink(path);
@@ -65,6 +75,7 @@ int main(int argc, char **argv) {
       if (fd < 0 || ftruncate(fd, (off_t)bytes)) return 1;
       char *map = mmap(NULL, bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
       if (map == MAP_FAILED) return 1;
+      if (mode == HUGE && madvise(map, bytes, MADV_HUGEPAGE)) printf("{\"madv_hugepage\": \"failed\"}\n");
       pthread_t th[16];
       job_t jobs[16];
       const size_t per = (bytes / T + 4095) & ~(size_t)4095;

@@ -37,6 +37,7 @@ def main():
     gen = os.path.join(tmp, "fqgen")
     fq = f"/dev/shm/hpgq_wab_{os.getpid()}.fq"
     outd = f"/dev/shm/hpgq_wab_out_{os.getpid()}"
+    bench._load_hpgfastq()
     cpus = bench.numa_cpus(0)
     share = sorted(cpus)[:bench.omp_threads(len(cpus) or 16)] if cpus else None
     nthr = str(len(share) if share else 16)
