@@ -963,12 +963,12 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
         if (m == NM - 1 && last) issue_dma();   // (the unit's last group pair)
         load_group(m, tb, nt, g + 1, 1);
         process_group(g, 0);
-        if (NM == 1) {
-          // ONE load site for slot 0, this unit's next group or the next unit's
-          // first: with two (if / else), the wait-count pass merged their
-          // pending loads at the join and made process_group(g + 1) wait for
-          // the loads just issued (vmcnt(0): a full HBM round trip per pair)
-          if (LATE && last) describe_next(false);
+        if (NM == 1 && LATE) {
+          // edit: ONE load site for slot 0, this unit's next group or the next
+          // unit's first, behind the next unit's prologue (round 5: C4 811 ->
+          // 806 us; C2, whose else-branch is a plain load, ran 1.5 % slower
+          // this way and keeps the if / else)
+          if (last) describe_next(false);
           load_group(0, last ? tb ^ 1 : tb, last ? nnt : nt, last ? 0 : g + 2, 0);
         } else if (!last) {
           load_group(m, tb, nt, g + 2, 0);
