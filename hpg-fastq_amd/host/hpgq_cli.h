@@ -56,7 +56,7 @@ typedef struct {
   int stream_writer;        /* filter / edit: one writer thread instead of mapped outputs */
   int writer_hook;          /* tests only (--writer-test-hook): hpgq_mapout.h MAPOUT_HOOK_* */
   int copy_threads;         /* mapped writer: copier threads (0: --num-threads) */
-  int prefault_threads;     /* mapped writer: prefault threads (-1: default 2; 0: none past the first window) */
+  int prefault_threads;     /* mapped writer: prefault threads (-1: default, none past the first window) */
 } cli_options_t;
 
 /* parse + validate (exits with the reference's messages on errors) */

@@ -106,7 +106,7 @@ static void usage(const cli_options_t *o) {
     printf("  --stream-writer                 Write the FastQ outputs through one writer thread\n"
            "                                  (default: mapped output files filled in parallel)\n"
            "  --copy-threads=<int>            Mapped writer: copier threads (default --num-threads)\n"
-           "  --prefault-threads=<int>        Mapped writer: threads populating the outputs ahead (default 2)\n");
+           "  --prefault-threads=<int>        Mapped writer: threads populating the outputs ahead (default 0)\n");
   printf("  --quiet                         No parameter / result display\n");
   exit(-1);
 }

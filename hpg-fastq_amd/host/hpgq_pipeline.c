@@ -743,10 +743,14 @@ static int place_and_copy(pipe_t *P, slot_t *s, int *handed) {
 static int map_outputs(pipe_t *P) {
   const int fd[2] = {P->out_pass ? fileno(P->out_pass) : -1, P->out_fail ? fileno(P->out_fail) : -1};
   P->map_cap = (size_t)P->size + 4096;
-  /* prefault two chunks ahead of the placed records, on two threads (a third
-   * and fourth made one tmpfs file's page allocation slower, r04 probe) */
+  /* --prefault-threads N: populate two chunks ahead of the placed records on
+   * N threads.  Default none past the reserved first window: on MI355X boxes
+   * the prefault threads made stored `filter` slower (same box, alternating:
+   * median 16 vs 24-26 Mreads/s with 2 threads vs none, profiles/
+   * r05_writer_ab.json) -- they contend with the copiers for the one file's
+   * page allocation; the SIGBUS guard covers what is not reserved */
   const size_t ahead = (size_t)2 * ((size_t)P->o->chunk_mb << 20);
-  const int pft = P->o->prefault_threads < 0 ? 2 : P->o->prefault_threads;
+  const int pft = P->o->prefault_threads < 0 ? 0 : P->o->prefault_threads;
   const int rc = mapout_open(&P->mo, fd, P->map_cap, ahead, pft, P->o->writer_hook);
   if (rc) return rc;
   P->map[0] = P->mo.map[0];

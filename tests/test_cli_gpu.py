@@ -158,7 +158,9 @@ def test_cli_writer_store_failure_is_io_error(tmp_path, hook):
     reads = O.synth(150000 if hook == 2 else 40000, seed=32, L=150)
     fq = _write(tmp_path, reads)
     r = run_cli(["filter", "-f", fq, "-o", tmp_path, "--read-quality-range", "20,", "--read-length-range", "50,",
-                 "--chunk-mb", 1, "--quiet", "--writer-test-hook", hook], check=False, env={"HPGQ_TRACE": "1"})
+                 "--chunk-mb", 1, "--quiet", "--writer-test-hook", hook,
+                 # (the default prefaults nothing past the first window: hook 2 needs the threads)
+                 *(["--prefault-threads", 2] if hook == 2 else [])], check=False, env={"HPGQ_TRACE": "1"})
     assert r.returncode == 1, (r.returncode, r.stderr[-2000:])   # (a SIGBUS death would be -7)
     assert WRITER_LINE["mmap"] in r.stderr
     assert "Error: file i/o error (-9)" in r.stderr, r.stderr[-2000:]
