@@ -264,12 +264,17 @@ __device__ __forceinline__ uint32_t ffbh_raw(uint32_t x) {
 // (each compare is ONE v_bitop3 of (w, c ^ 0x80, (w | 0x80) - (c & 0x7F)):
 // truth table 0x8E = (~w & c') | (~(w ^ c') & d); hipcc left to itself spends
 // three instructions on it; the combine ge_lo & ~ge_hi & 0x80 is bitop3 0x20)
+// HINONE (no upper bound, TrimSide::hq = 0 and h7 = 0x80808080, for which
+// "≥ hi" never holds): the lower compare alone, four VALU
+template <bool HINONE = false>
 __device__ __forceinline__ uint32_t trim_side_ok(uint32_t w, const TrimSide &S) {
   const uint32_t wh = w | kQFlip;
   const uint32_t ge_lo = __builtin_amdgcn_bitop3_b32(w, S.lq, wh - S.l7, 0x8E);
+  if (HINONE) return ge_lo & kQFlip;
   const uint32_t ge_hi = __builtin_amdgcn_bitop3_b32(w, S.hq, wh - S.h7, 0x8E);
   return __builtin_amdgcn_bitop3_b32(ge_lo, ge_hi, kQFlip, 0x20);
 }
+__device__ __forceinline__ bool trim_hi_none(const TrimSide &S) { return S.hq == 0u && S.h7 == kQFlip; }
 
 // the trims of a read of length n from its usual-window loads: ts | te << 16.
 // Branch-free (round 5): ts = min(first in-range index of the left window,
@@ -279,12 +284,27 @@ __device__ __forceinline__ uint32_t trim_side_ok(uint32_t w, const TrimSide &S) 
 __device__ __forceinline__ uint32_t trim_finish(const ColdParams &C, const TrimLoads &T, int n) {
   const uint32_t wl[4] = {T.wl.x, T.wl.y, T.wl.z, T.wl.w};
   const uint32_t wr[8] = {T.wr0.x, T.wr0.y, T.wr0.z, T.wr0.w, T.wr1.x, T.wr1.y, T.wr1.z, T.wr1.w};
+  // (a side without an upper bound -- the usual `--left-quality-range 20,` --
+  // takes the four-VALU compare: a uniform branch per side; a left length of
+  // at most 12 leaves the window's last dword out: an in-range byte there
+  // would give ts >= 12 > left_len, which the min below makes left_len anyway)
   uint32_t first = ~0u;
+  const int nl = C.e_left_len <= 12 ? 3 : 4;
+  auto left = [&](auto hn) __attribute__((always_inline)) {
 #pragma unroll
-  for (int w = 0; w < 4; ++w) first = min(first, (ffbl_raw(trim_side_ok(wl[w], C.tl)) >> 3) + 4u * w);
+    for (int w = 0; w < 4; ++w)
+      if (w < nl) first = min(first, (ffbl_raw(trim_side_ok<decltype(hn)::value>(wl[w], C.tl)) >> 3) + 4u * w);
+  };
+  if (trim_hi_none(C.tl)) left(std::true_type{});
+  else left(std::false_type{});
   uint32_t okr[8];
+  if (trim_hi_none(C.tr)) {
 #pragma unroll
-  for (int k = 0; k < 8; ++k) okr[k] = trim_side_ok(wr[k], C.tr);
+    for (int k = 0; k < 8; ++k) okr[k] = trim_side_ok<true>(wr[k], C.tr);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) okr[k] = trim_side_ok<false>(wr[k], C.tr);
+  }
   if (__builtin_expect(T.hi < 32, 0)) {   // a read at the buffer start: bytes >= hi are the next read's
 #pragma unroll
     for (int k = 0; k < 8; ++k) okr[k] &= byte_mask(T.hi - 4 * k);
@@ -303,13 +323,16 @@ __device__ __forceinline__ uint32_t trim_finish(const ColdParams &C, const TrimL
 // compiler neither sees the LDS write (it would make every later LDS read of
 // the kernel wait for it: one exposed HBM round trip per unit again) nor
 // counts it: the reader waits for it explicitly (s_waitcnt vmcnt, in order).
-// M0 (the LDS base) is saved and restored around it.
+// M0 (the LDS base: lds + OFF bytes, added in the asm so only `lds` is held in
+// an SGPR across the loop, not one hoisted address per row) is saved and
+// restored around it.
+template <int OFF>
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t rs, uint32_t voff, uint32_t lds) {
   uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
+  asm volatile("s_mov_b32 %0, m0\n\ts_add_u32 m0, %3, %4\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\ts_mov_b32 m0, %0"
                : "=&s"(keep)
-               : "v"(voff), "s"(rs), "s"(lds)
-               : "memory");
+               : "v"(voff), "s"(rs), "s"(lds), "n"(OFF)
+               : "memory", "scc");
 }
 
 // 0x80 per in-range byte of raw quality words x, y (bytes 0-3, 4-7)
@@ -836,19 +859,22 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
 #pragma unroll
     for (int m = 0; m < NM; ++m) dfr = dfr || (ie[m] - ia[m] > dlim);
     const bool live = on && !dfr;
-#pragma unroll
-    for (int m = 0; m < NM; ++m) {
+    const uint32_t sb = (uint32_t)(uintptr_t)scratch;   // (the rows sit at constant offsets from it)
+    auto mate = [&](auto mtag) __attribute__((always_inline)) {
+      constexpr int m = decltype(mtag)::value;
+      constexpr int kRow0 = 4 * (64 + 4 + NM * kFxWords + m * 3 * kBlock * 4), kRowB = 4 * kBlock * 4;
       const int off = bq[m] + ia[m], n = ie[m] - ia[m];
       int pa = off + n - 32;
       if (pa < 0) pa = 0;
       const uint32_t kOut = 0x80000000u;
-      if (cold_all.e_left_len > 0)
-        dma16(rq[m], live ? (uint32_t)off : kOut, (uint32_t)(uintptr_t)dma_row(m, 0));
+      if (cold_all.e_left_len > 0) dma16<kRow0>(rq[m], live ? (uint32_t)off : kOut, sb);
       if (cold_all.e_right_len > 0) {
-        dma16(rq[m], live ? (uint32_t)pa : kOut, (uint32_t)(uintptr_t)dma_row(m, 1));
-        dma16(rq[m], live ? (uint32_t)pa + 16u : kOut, (uint32_t)(uintptr_t)dma_row(m, 2));
+        dma16<kRow0 + kRowB>(rq[m], live ? (uint32_t)pa : kOut, sb);
+        dma16<kRow0 + 2 * kRowB>(rq[m], live ? (uint32_t)pa + 16u : kOut, sb);
       }
-    }
+    };
+    mate(MateTag<0>{});
+    if (NM == 2) mate(MateTag<NM - 1>{});
   };
   if (cur.u >= 0) {
     fetch_idx(cur, ia, ie);
