@@ -186,6 +186,7 @@ static void cold_params(const hpgq_params_t &p, hpgq::ColdParams &C) {
   int lo_none, hi_none, none_in;
   raw_range(p.phred, p.min_read_quality, p.max_read_quality, C.oor_lo4, C.oor_hi4, lo_none,
             hi_none, none_in);
+  trim_side(C.oor_lo4, C.oor_hi4, hi_none, none_in, C.to);   // (no lower bound: lo4 = 0, ">= lo" always holds)
   C.max_n = p.max_N;
   C.max_oor = p.max_out_of_quality;
 }

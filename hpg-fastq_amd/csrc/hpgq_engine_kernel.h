@@ -72,6 +72,7 @@ struct ColdParams {
   uint32_t oor_lo4, oor_hi4;
   int max_n, max_oor;
   TrimSide tl, tr;   // the edit windows' in-range tests (segmented kernels' trim_finish)
+  TrimSide to;       // the filter's quality range (segmented kernels' out-of-range count)
 };
 
 struct EngineArgs {

@@ -457,11 +457,13 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   const bool stats = A.flags & F_STATS, filter = A.flags & F_FILTER;
   // NX: the filter's extra limits, read once (not from *A.cold inside the loop,
   // where each scalar reload would wait for the outstanding LDS operations too)
-  const uint32_t x_lo4 = NX ? (uint32_t)uni((int)A.cold->oor_lo4) : 0u;
-  const uint32_t x_hi4 = NX ? (uint32_t)uni((int)A.cold->oor_hi4) : 0u;
+  // (the quality range as the trims' TrimSide constants: no flags to branch on per word)
+  const TrimSide xr = NX ? TrimSide{(uint32_t)uni((int)A.cold->to.lq), (uint32_t)uni((int)A.cold->to.l7),
+                                    (uint32_t)uni((int)A.cold->to.hq), (uint32_t)uni((int)A.cold->to.h7)}
+                         : TrimSide{0u, 0u, 0u, 0u};
+  const bool x_hin = NX && trim_hi_none(xr);
   const int x_maxn = NX ? uni(A.cold->max_n) : 0, x_maxo = NX ? uni(A.cold->max_oor) : 0;
   const bool x_n = NX && (A.flags & F_NEED_N), x_o = NX && (A.flags & F_NEED_OOR);
-  const bool x_all = A.flags & F_OOR_ALL, x_lonone = A.flags & F_OOR_LO_NONE, x_hinone = A.flags & F_OOR_HI_NONE;
   // LR: the window filters, read once (see NX above); length 0 = off
   const int w_ll = LR ? max(uni(A.cold->left_len), 0) : 0, w_rl = LR ? max(uni(A.cold->right_len), 0) : 0;
   // (window means lie in [-383, 127] Phred: bounds clamped to +-512 keep k * bound in int32)
@@ -788,21 +790,38 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       qs = __builtin_amdgcn_sad_u8(qm[w], 0u, qs);
     }
     if (NX && !SUB) {   // N | out-of-range << 16 over the lane's valid bytes (as engine_kernel)
-      uint32_t nn = 0, oo = 0;
+      // Round 5: one uniform branch per count, not five per word (the flags
+      // of the range's shape cost c4_noor 4x C4's branches and 1.6x its VALU):
+      // N bytes by the SWAR zero test folded into one v_bitop3 (~t & ~v & m80);
+      // out of range = valid and not (>= lo and not >= hi) from the raw bytes
+      // with the TrimSide constants (a missing bound or an empty range is in
+      // the constants), one v_bitop3 per bound and one for the combine
+      uint32_t m80[NW];
 #pragma unroll
-      for (int w = 0; w < NW; ++w) {
-        const uint32_t m80 = mk[w] & 0x80808080u;
-        if (x_n) nn += (uint32_t)__builtin_popcount(zero_bytes(sw[w] ^ 0x4E4E4E4Eu) & m80);
-        if (x_o) {
-          uint32_t b;
-          if (x_all) {
-            b = 0x80808080u;
-          } else {
-            b = 0;
-            if (!x_lonone) b |= ~ge_bytes(qm[w], x_lo4) & 0x80808080u;   // (biased; m80 drops the masked bytes)
-            if (!x_hinone) b |= ge_bytes(qm[w], x_hi4);
+      for (int w = 0; w < NW; ++w) m80[w] = mk[w] & 0x80808080u;
+      uint32_t nn = 0, oo = 0;
+      if (x_n) {
+#pragma unroll
+        for (int w = 0; w < NW; ++w) {
+          const uint32_t v = sw[w] ^ 0x4E4E4E4Eu, t = (v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
+          nn += (uint32_t)__builtin_popcount(__builtin_amdgcn_bitop3_b32(t, v, m80[w], 0x02));
+        }
+      }
+      if (x_o) {
+        if (x_hin) {
+#pragma unroll
+          for (int w = 0; w < NW; ++w) {
+            const uint32_t ge_lo = __builtin_amdgcn_bitop3_b32(qw[w], xr.lq, (qw[w] | kQFlip) - xr.l7, 0x8E);
+            oo += (uint32_t)__builtin_popcount(__builtin_amdgcn_bitop3_b32(ge_lo, m80[w], 0u, 0x04));   // m80 & ~ge_lo
           }
-          oo += (uint32_t)__builtin_popcount(b & m80);
+        } else {
+#pragma unroll
+          for (int w = 0; w < NW; ++w) {
+            const uint32_t wh = qw[w] | kQFlip;
+            const uint32_t ge_lo = __builtin_amdgcn_bitop3_b32(qw[w], xr.lq, wh - xr.l7, 0x8E);
+            const uint32_t ge_hi = __builtin_amdgcn_bitop3_b32(qw[w], xr.hq, wh - xr.h7, 0x8E);
+            oo += (uint32_t)__builtin_popcount(__builtin_amdgcn_bitop3_b32(ge_lo, ge_hi, m80[w], 0x8A));   // m80 & (~ge_lo | ge_hi)
+          }
         }
       }
       x2 = nn | (oo << 16);
