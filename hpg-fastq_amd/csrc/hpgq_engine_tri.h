@@ -928,8 +928,11 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       if (tdma && nxt.u >= 0) dma_windows(nxt);
     };
     auto describe_next = [&](bool drained) __attribute__((always_inline)) {
-      if (tdma && drained) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      else if (tdma) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      // (the DMA is the youngest VMEM operation here: issued inside the pair's
+      // first process_pair, after its loads were waited for; `drained`: a
+      // wholly deferred unit, issued just before)
+      (void)drained;
+      if (tdma) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       load_block(nxt, tb ^ 1, lenn, twn, dmn, ia, ie, true);
       nn2 = it.next();
       fetch_idx(nn2, ia, ie);
@@ -1037,7 +1040,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       if (stats) acc[m].widen();
     };
     // PEU: step g of both mates added, the pair decided, a failed pair undone
-    auto process_pair = [&](int g, int slot) __attribute__((always_inline)) {
+    auto process_pair = [&](int g, int slot, bool dma_after) __attribute__((always_inline)) {
       constexpr int m1 = NM - 1;
       const int t = g;
       StepVals dsv;
@@ -1055,6 +1058,11 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       if (ls == kSegW - 1 && seg < kSegs && t < nt) wends(0)[kSegs * t + seg] = P0;
       const bool pass0 = !dec || read_ok(P0, x0, grp[slot][0].n);   // (only a bool lives on)
       const uint32_t x1 = account(MateTag<m1>{}, grp[slot][m1], stats, AddTag{}, d2, d3, dsv);
+      // TDMA: the next unit's windows, issued once this group's loads have been
+      // waited for: the DMA is invisible to hipCC's wait counts, so a
+      // compiler wait for any load after it (the loop top's, or this group's)
+      // would drain it on the spot (vmcnt counts in order)
+      if (dma_after) issue_dma();
       const uint32_t P1 = wave_scan(x1);
       if (ls == kSegW - 1 && seg < kSegs && t < nt) wends(m1)[kSegs * t + seg] = P1;
       if (!dec) return;
@@ -1067,13 +1075,12 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     if (PEU && ngroups > 0) {
       const int ng = (nt + 1) & ~1;   // one step per group, an even count
       for (int g = 0; g < ng; g += 2) {
-        if (g + 2 >= ng) issue_dma();   // (the unit's last group pair)
         load_group_pe(tb, nt, g + 1, 1);
-        process_pair(g, 0);
+        process_pair(g, 0, g + 2 >= ng);   // (the unit's last group pair: the DMA inside)
         const bool last = g + 2 >= ng;   // (one load site for slot 0, as in run_mate)
         if (LATE && last) describe_next(false);
         load_group_pe(last ? tb ^ 1 : tb, last ? nnt : nt, last ? 0 : g + 2, 0);
-        process_pair(g + 1, 1);
+        process_pair(g + 1, 1, false);
         if (stats && ((g + 2) & 7) == 0)   // nibbles hold at most 15 steps
           for (int m = 0; m < NM; ++m) acc[m].widen();
       }
