@@ -914,31 +914,26 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     // the algorithmic bytes); else at the unit start, a unit ahead.
     Unit nn2 = Unit{-1, 0, 0};
     int nnt = 0;
-    // TDMA: the DMA rows are filled at the start of this unit's last group
-    // pair (issue_dma: about one group of work before the next unit's
-    // prologue reads them; a unit earlier their lines left L2 before the
-    // stream came back for them, +0.5 GB of HBM traffic per C4 launch);
-    // `drained`: no load was issued after them (a wholly deferred unit), else
-    // at least that pair's second group's four (two steps x two buffers; PEU:
-    // a step of both mates) were, and vmcnt counts in order
+    // TDMA: the DMA rows are filled during this unit's last group pair
+    // (issue_dma, inside its first process_pair: part of a group of work
+    // before the next unit's prologue reads them; a unit earlier their lines
+    // left L2 before the stream came back for them, +0.5 GB of HBM traffic
+    // per C4 launch; at the pair's top hipcc's own vmcnt(0) drained it)
     const bool tdma = TDMA && trim_usual(cold_all);
-    // (not at the loop's top: a use of the offsets there, a merge point, waited
-    // for every load in flight)
     auto issue_dma = [&]() __attribute__((always_inline)) {
       if (tdma && nxt.u >= 0) dma_windows(nxt);
     };
-    auto describe_next = [&](bool drained) __attribute__((always_inline)) {
+    auto describe_next = [&]() __attribute__((always_inline)) {
       // (the DMA is the youngest VMEM operation here: issued inside the pair's
-      // first process_pair, after its loads were waited for; `drained`: a
-      // wholly deferred unit, issued just before)
-      (void)drained;
+      // first process_pair after its loads were waited for, or -- a wholly
+      // deferred unit -- just before)
       if (tdma) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       load_block(nxt, tb ^ 1, lenn, twn, dmn, ia, ie, true);
       nn2 = it.next();
       fetch_idx(nn2, ia, ie);
       nnt = steps_of(nxt, dmn);
     };
-    if (!LATE) describe_next(false);
+    if (!LATE) describe_next();
     if (stats && since_flush > kByteEvery - kBlock / kSegs) {   // keep every byte <= 255
 #pragma unroll
       for (int m = 0; m < NM; ++m) acc[m].template flush<PF>(pos_acc(m), lp, p0);
@@ -1012,7 +1007,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
         if (m + 1 < NM) {
           load_group(m + 1 < NM ? m + 1 : 0, tb, nt, 0, slot);
         } else {
-          if (LATE) describe_next(false);
+          if (LATE) describe_next();
           load_group(0, tb ^ 1, nnt, 0, slot);
         }
       };
@@ -1026,7 +1021,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
           // unit's first, behind the next unit's prologue (round 5: C4 811 ->
           // 806 us; C2, whose else-branch is a plain load, ran 1.5 % slower
           // this way and keeps the if / else)
-          if (last) describe_next(false);
+          if (last) describe_next();
           load_group(0, last ? tb ^ 1 : tb, last ? nnt : nt, last ? 0 : g + 2, 0);
         } else if (!last) {
           load_group(m, tb, nt, g + 2, 0);
@@ -1078,7 +1073,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
         load_group_pe(tb, nt, g + 1, 1);
         process_pair(g, 0, g + 2 >= ng);   // (the unit's last group pair: the DMA inside)
         const bool last = g + 2 >= ng;   // (one load site for slot 0, as in run_mate)
-        if (LATE && last) describe_next(false);
+        if (LATE && last) describe_next();
         load_group_pe(last ? tb ^ 1 : tb, last ? nnt : nt, last ? 0 : g + 2, 0);
         process_pair(g + 1, 1, false);
         if (stats && ((g + 2) & 7) == 0)   // nibbles hold at most 15 steps
@@ -1091,11 +1086,11 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       if (NM == 2) run_mate(MateTag<NM - 1>{});
     } else if (PEU) {
       issue_dma();
-      if (LATE) describe_next(true);
+      if (LATE) describe_next();
       load_group_pe(tb ^ 1, nnt, 0, 0);   // a wholly deferred unit: straight to the next
     } else {
       issue_dma();
-      if (LATE) describe_next(true);
+      if (LATE) describe_next();
       load_group(0, tb ^ 1, nnt, 0, 0);   // a wholly deferred unit: straight to the next
     }
     since_flush += nt;
