@@ -32,6 +32,7 @@ timed on this host's cores on a bounded sample, rank 0 at N=1 only).
 """
 import argparse
 import ctypes as C
+import datetime
 import json
 import os
 import sys
@@ -134,6 +135,8 @@ def parse():
                          "wide, auto_fixed)")
     ap.add_argument("--launch-dry-run", action="store_true",
                     help="launcher + read sharding on CPU: gloo ranks, no GPU, no kernels")
+    ap.add_argument("--dry-run-fail-rank", type=int, default=-1,
+                    help="tests only (with --launch-dry-run): this rank exits 2 before the rendezvous")
     ap.add_argument("--share-device", action="store_true",
                     help="functional test of N ranks on fewer GPUs (ranks share device LOCAL_RANK mod "
                          "count; RCCL over its socket transport): not a scaling measurement")
@@ -577,8 +580,13 @@ def launch_ranks(args):
         procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:], env=env,
                                       stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL, text=True))
     rc = 0
-    while any(p.poll() is None for p in procs):
-        bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+    while True:
+        # (poll EVERY rank each time: `any(p.poll() is None ...)` stops at the
+        # first running one and never sees a later rank that failed)
+        states = [p.poll() for p in procs]
+        if all(st is not None for st in states):
+            break
+        bad = [st for st in states if st not in (None, 0)]
         if bad:
             rc = bad[0]
             for p in procs:
@@ -604,6 +612,18 @@ def launch_ranks(args):
         print("bench: rank 0 printed no result line", file=sys.stderr)
         rc = 1
     return rc
+
+
+def rank_fail(code, msg=None):
+    """End a rank process now: os._exit, not sys.exit -- once libhpgq / HIP is
+    loaded, interpreter teardown can block on runtime threads, and a rank that
+    never exits leaves the others waiting at the rendezvous (the launcher only
+    ends them when one has exited non-zero)."""
+    if msg:
+        print(msg, file=sys.stderr)
+    sys.stderr.flush()
+    sys.stdout.flush()
+    os._exit(code)
 
 
 def rank_env(args):
@@ -690,9 +710,13 @@ def dry_run_rank(args, world, rank):
     import torch.distributed as dist
     _load_hpgfastq()
     cfg = CONFIGS[args.config]
+    if rank == args.dry_run_fail_rank:   # (the launcher must end the ranks left waiting)
+        rank_fail(2, f"bench: rank {rank} fails (--dry-run-fail-rank)")
     if world > 1:
         os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        # (a bounded rendezvous: a peer that never arrives ends this rank too;
+        # a fresh box's first `import torch` alone can take 1-2 minutes)
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=900))
     lo, hi = shard(args, rank)
     n = min(1000, args.reads)
     s = H.Synth(args.seed, args.read_length, 5, 5, 1, 33, 0)
@@ -741,8 +765,7 @@ def main():
     _load_hpgfastq()
     if args.config == "dropin":
         if world > 1:
-            print("bench: --config dropin is a one-GPU host-path harness", file=sys.stderr)
-            sys.exit(2)
+            rank_fail(2, "bench: --config dropin is a one-GPU host-path harness")
         return dropin_main(args)
     cfg = CONFIGS[args.config]
     import torch
@@ -750,13 +773,14 @@ def main():
 
     ndev = torch.cuda.device_count()
     if local >= ndev and not args.share_device:
-        print(f"bench: rank {rank} needs device {local} but {ndev} are visible", file=sys.stderr)
-        sys.exit(2)
+        rank_fail(2, f"bench: rank {rank} needs device {local} but {ndev} are visible")
     local_dev = local % max(ndev, 1)
     if world > 1:   # rank control on gloo; the data path's exchange is libhpgq's RCCL
         # one node: gloo on loopback (the container hostname may not resolve)
         os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        # (a bounded rendezvous: a peer that never arrives ends this rank too;
+        # a fresh box's first `import torch` alone can take 1-2 minutes)
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=900))
     torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)
 
@@ -811,8 +835,7 @@ def main():
         eng.comm_init(world, rank, obj[0])
         rccl_ranks = eng.comm_count()
         if rccl_ranks != world:
-            print(f"bench: RCCL communicator has {rccl_ranks} ranks, world is {world}", file=sys.stderr)
-            sys.exit(3)
+            rank_fail(3, f"bench: RCCL communicator has {rccl_ranks} ranks, world is {world}")
     ext = torch.cuda.ExternalStream(eng.stream, device=dev)
     hb = [[H.engine.device_batch(n, sq.data_ptr(), ql.data_ptr(), ix.data_ptr())
            for (sq, ql, ix) in mm] for (n, mm, _nb) in batches]
@@ -883,9 +906,7 @@ def main():
         el = max(g["el_s"] for g in ranks)
         err = check_distinct_devices(ranks, args.share_device)
         if err:
-            if rank == 0:
-                print(err, file=sys.stderr)
-            sys.exit(3)
+            rank_fail(3, err if rank == 0 else None)
 
     # sanity: every read accounted for (after the all-reduce: every rank's reads)
     if kmers:

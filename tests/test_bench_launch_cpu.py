@@ -84,6 +84,20 @@ def test_failing_rank_fails_the_launch():
     assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
 
 
+def test_one_failing_rank_ends_the_others():
+    """Only rank 1 fails, before the rendezvous rank 0 is waiting in: the
+    launcher sees it (it polls every rank, not up to the first running one),
+    ends rank 0 and exits non-zero within seconds -- on a GPU box rank 0 would
+    otherwise wait out the gloo timeout."""
+    import time
+    t0 = time.time()
+    r = _bench("--gpus", "2", "--launch-dry-run", "--reads", "5000", "--dry-run-fail-rank", "1")
+    assert r.returncode != 0
+    assert "rank 1 fails" in r.stderr
+    assert time.time() - t0 < 120
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+
+
 def test_gpu_run_refuses_missing_devices():
     """A rank on a host without enough devices exits non-zero before any
     kernel (here: no device at all, without --share-device)."""
