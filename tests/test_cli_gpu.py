@@ -148,6 +148,22 @@ def test_cli_writer_reservation_failure_uses_stream_writer(tmp_path):
     assert (tmp_path / "failed.fq").read_bytes() == failed
 
 
+@pytest.mark.parametrize("threads", [["--prefault-threads", 2], ["--prefault-threads", 4, "--copy-threads", 3],
+                                     ["--copy-threads", 1]])
+def test_cli_writer_thread_options_exact(tmp_path, threads):
+    """The mapped writer's thread options (prefault threads past the reserved
+    first window, fewer or more copiers than --num-threads) write exactly the
+    default's files (the input spans several 32 MB prefault windows)."""
+    reads = O.synth(150000, seed=34, L=150)
+    fq = _write(tmp_path, reads)
+    r = run_cli(["filter", "-f", fq, "-o", tmp_path, "--read-quality-range", "20,", "--read-length-range", "50,",
+                 "--chunk-mb", 4, "--quiet", *threads], env={"HPGQ_TRACE": "1"})
+    assert WRITER_LINE["mmap"] in r.stderr, r.stderr[-2000:]
+    passed, failed = _filter_expected(reads)
+    assert (tmp_path / "passed.fq").read_bytes() == passed
+    assert (tmp_path / "failed.fq").read_bytes() == failed
+
+
 @pytest.mark.parametrize("hook", [2, 4])
 def test_cli_writer_store_failure_is_io_error(tmp_path, hook):
     """A prefault window the file system cannot back (hook 2), or a store into
