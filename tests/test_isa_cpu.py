@@ -38,7 +38,10 @@ def kernels(tmp_path_factory):
         pytest.skip("libhpgq.so or the LLVM offload tools are missing")
     d = tmp_path_factory.mktemp("isa")
     fat = d / "fatbin.bin"
-    subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={fat}", LIB], check=True, capture_output=True)
+    # (an explicit output file: without one objcopy rewrites its input in place,
+    # under every other test that has libhpgq.so mapped)
+    subprocess.run(["objcopy", "--dump-section", f".hip_fatbin={fat}", LIB, str(d / "copy.so")], check=True,
+                   capture_output=True)
     blob = fat.read_bytes()
     starts = [m.start() for m in re.finditer(re.escape(MAGIC), blob)]
     assert starts, "no offload bundle in .hip_fatbin"
