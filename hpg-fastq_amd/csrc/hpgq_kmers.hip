@@ -223,11 +223,14 @@ __global__ void __launch_bounds__(kWG) kmer_tile_kernel(const char *seq, const i
     v4u a;
     v2u c;
   };
+  // (the b64 tail only on the odd lane of a pair: the even lane's bytes 16..23
+  // are its partner's first 8, handed over by DPP when the group is counted;
+  // the even lanes' tail offset is out of range: zeros, no traffic)
   auto window = [&](const Meta &M) __attribute__((always_inline)) {
     const uint32_t o = (uint32_t)(M.a + p0 + 16 * hl) & ~3u;
     Win W;
     W.a = __builtin_amdgcn_raw_buffer_load_b128(rs, o, 0, 0);
-    W.c = __builtin_amdgcn_raw_buffer_load_b64(rs, o + 16u, 0, 0);
+    W.c = __builtin_amdgcn_raw_buffer_load_b64(rs, hl ? o + 16u : 0x80000000u, 0, 0);
     return W;
   };
   // per step j: the alignbit shift of the visited start (30 - 2 (q + j mod
@@ -258,6 +261,14 @@ __global__ void __launch_bounds__(kWG) kmer_tile_kernel(const char *seq, const i
     uint32_t pk[5], bd[5];
     const uint32_t ab = (uint32_t)c.a & 3u;   // the window's byte offset in its first dword
                                               // (p0 and 16 hl are multiples of 4)
+    {   // even lanes: the tail from the odd partner's first 8 bytes (quad_perm [1,1,3,3])
+      const uint32_t n0 = (uint32_t)__builtin_amdgcn_mov_dpp((int)wc.a[0], 0xF5, 0xF, 0xF, false);
+      const uint32_t n1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)wc.a[1], 0xF5, 0xF, 0xF, false);
+      if (!hl) {
+        wc.c[0] = n0;
+        wc.c[1] = n1;
+      }
+    }
     const uint32_t wd[5] = {__builtin_amdgcn_alignbyte(wc.a[1], wc.a[0], ab), __builtin_amdgcn_alignbyte(wc.a[2], wc.a[1], ab),
                             __builtin_amdgcn_alignbyte(wc.a[3], wc.a[2], ab), __builtin_amdgcn_alignbyte(wc.c[0], wc.a[3], ab),
                             __builtin_amdgcn_alignbyte(wc.c[1], wc.c[0], ab)};
