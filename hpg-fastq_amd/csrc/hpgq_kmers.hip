@@ -305,6 +305,13 @@ __global__ void __launch_bounds__(kWG) kmer_tile_kernel(const char *seq, const i
   // (no exit between the two steps: a group past the last has no counted
   // read -- its offsets and mask bytes load as 0 -- and adds nothing)
   for (int64_t g = g0; g < ngroups; g += 2 * gstride) {
+    // every load drained once per iteration, on purpose: the drain keeps the T
+    // tile workgroups of a class in step, so their re-reads of a read's window
+    // hit the XCD's L2.  Exact waits (the windows of two groups in flight
+    // throughout) let them drift apart: HBM traffic 1.06x -> 2.0x, 570 -> 633
+    // us; lockstep by progress counters instead cost more than it saved
+    // (profiles/r05_kmers_waits_ab.json)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     step(g, ca, wa, rb, ra);
     step(g + gstride, cb, wb, ra, rb);
   }
