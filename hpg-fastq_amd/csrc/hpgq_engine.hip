@@ -16,6 +16,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <rccl/rccl.h>
+#include <vector>
 
 namespace {
 
@@ -37,8 +38,21 @@ struct Chain {
   bool has2 = false, has3 = false;
 };
 
-// flags words behind the counters (one memset clears both)
-enum { FL_PEND1 = 0, FL_PEND2 = 2, FL_ERR = 4, FL_WORDS = 8 };
+// flags words behind the counters (one memset clears both): deferred-read
+// counts by call parity, the longest merged window longer than lmax, the
+// longest one the tail could not hold (hpgq_sync's second pass), and that
+// pass's read count
+enum { FL_PEND1 = 0, FL_PEND2 = 2, FL_MAXLEN = 5, FL_NEED = 6, FL_REDO = 7, FL_WORDS = 8 };
+
+// a device-path call since the last sync, kept for the long-read tail's second
+// pass (hpgq_sync): its batch and the tail's end when it ran
+struct CallRec {
+  const char *seq[2], *qual[2];
+  const int32_t *idx[2];
+  int64_t n;
+  int tail_hi;
+};
+constexpr size_t kOvfChunk = 4096;   // per-call overflow flags per device chunk
 
 // adaptive first stage: a ctx whose reads may be long keeps two chains, hex
 // first (short reads; long ones deferred to wide) and wide first (long reads),
@@ -98,8 +112,18 @@ struct hpgq_ctx {
   int staged = -1;
   int64_t staged_n = 0;
   size_t staged_bytes[2] = {0, 0};
-  int32_t *h_err = nullptr;   // pinned: the error flag, copied back by hpgq_sync
+  uint32_t *h_flags = nullptr;   // pinned: the FL_WORDS flags, copied back by hpgq_sync
   ncclComm_t comm = nullptr;
+  // the long-read tail: [tail_cap][nm][8] u64 from position
+  // lmax on (EngineArgs::tail); grown by the host, never by a kernel
+  uint64_t *d_tail = nullptr;
+  int64_t tail_cap = 0;
+  uint64_t *d_gtail = nullptr;   // its sum over the ranks (hpgq_read_counters_ext)
+  size_t gtail_cap = 0;
+  uint32_t *d_scratch = nullptr;   // 16 u32 for small RCCL exchanges
+  std::vector<CallRec> calls;           // device-path calls since the last sync
+  std::vector<uint32_t *> ovf_chunks;   // their overflow flags, kOvfChunk per chunk
+  Stage redo;                           // the catch-all's follow-up instance (TAIL_ONLY pass)
 };
 
 // biased thresholds for "signed byte in [phred+lo, phred+hi]" (the kernels
@@ -371,6 +395,25 @@ static int pick_chain(hpgq_ctx *c) {
   return c->mode;
 }
 
+// The long-read tail's second pass (hpgq_sync): per 64-read unit, the reads
+// (pairs) with a mate longer than p0 -- the only ones whose windows can reach
+// past the tail a call had -- as bits + a count for the catch-all's follow-up
+// instance (F_TAIL_ONLY).  Every unit's word is written.
+__global__ void __launch_bounds__(256) tail_bits_kernel(const int32_t *idx0, const int32_t *idx1, int64_t n,
+                                                        int p0, uint64_t *bits, uint32_t *count) {
+  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  bool on = false;
+  if (r < n) {
+    on = idx0[r + 1] - idx0[r] > p0;
+    if (idx1) on = on || idx1[r + 1] - idx1[r] > p0;
+  }
+  const uint64_t b = __ballot(on);
+  if ((threadIdx.x & 63) == 0 && r < n) {
+    bits[r >> 6] = b;
+    if (b) atomicAdd(count, (uint32_t)__builtin_popcountll(b));
+  }
+}
+
 extern "C" {
 
 const char *hpgq_kernel_name(const hpgq_ctx_t *ctx) { return ctx ? ctx->ch[0].s1.name : ""; }
@@ -443,6 +486,9 @@ static int validate_params(const hpgq_params_t *p) {
   if (!p) return HPGQ_E_INVALID;
   if (p->lmax < 1 || p->lmax > HPGQ_LMAX_LIMIT) return HPGQ_E_INVALID;
   if (p->phred < 0 || p->phred > 255) return HPGQ_E_INVALID;
+  // trims come back as two 16-bit fields (trim_out): a window is at most 65535
+  if (p->edit_on && (p->edit_left_length > HPGQ_MAX_EDIT_LENGTH || p->edit_right_length > HPGQ_MAX_EDIT_LENGTH))
+    return HPGQ_E_INVALID;
   return HPGQ_OK;
 }
 
@@ -472,14 +518,19 @@ int hpgq_open(hpgq_ctx_t **out, int device, const hpgq_params_t *p) {
   HPGQ_HIP_TRY(hipMalloc(&c->d_global, c->clen * c->nm * sizeof(uint64_t)));
   HPGQ_HIP_TRY(hipMemsetAsync(c->d_state, 0, state_bytes(c), c->stream));
   HPGQ_HIP_TRY(hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking));
-  HPGQ_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&c->h_err), 64, hipHostMallocDefault));
-  *c->h_err = 0;
+  HPGQ_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&c->h_flags), FL_WORDS * 4, hipHostMallocDefault));
+  std::memset(c->h_flags, 0, FL_WORDS * 4);
+  HPGQ_HIP_TRY(hipMalloc(&c->d_scratch, 64));
   for (auto &sl : c->slot) {
     HPGQ_HIP_TRY(hipEventCreateWithFlags(&sl.copied, hipEventDisableTiming));
     HPGQ_HIP_TRY(hipEventCreateWithFlags(&sl.used, hipEventDisableTiming));
   }
   HPGQ_HIP_TRY(hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device));
   rc = plan(c, c->cus);
+  if (rc == HPGQ_OK) {   // the long-read tail's second pass: the catch-all's follow-up instance
+    catch_all(c->redo, c->nm, p->lmax, true, true);
+    rc = finish_stage(c, c->redo, catch_all_lds(c->p, c->nm), c->cus);
+  }
   if (rc) {
     hpgq_close(c);
     return rc;
@@ -519,7 +570,11 @@ void hpgq_close(hpgq_ctx_t *c) {
     if (sl.copied) (void)hipEventDestroy(sl.copied);
     if (sl.used) (void)hipEventDestroy(sl.used);
   }
-  if (c->h_err) (void)hipHostFree(c->h_err);
+  if (c->h_flags) (void)hipHostFree(c->h_flags);
+  (void)hipFree(c->d_tail);
+  (void)hipFree(c->d_gtail);
+  (void)hipFree(c->d_scratch);
+  for (uint32_t *q : c->ovf_chunks) (void)hipFree(q);
   if (c->h_report) (void)hipHostFree(c->h_report);
   if (c->cstream) (void)hipStreamDestroy(c->cstream);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -552,13 +607,68 @@ static int launch_stage(hpgq_ctx *c, const Stage &s, hpgq::EngineArgs &A) {
   return HPGQ_OK;
 }
 
-// the chain over one batch (A: batch, outputs and options filled in)
-static int launch(hpgq_ctx *c, hpgq::EngineArgs &A) {
+// Grow the long-read tail to hold positions [lmax, lmax + cap).  Waits for
+// the ctx stream first (kernels in flight add into the old tail); the new
+// entries are zero.  Host decisions only: a kernel never needs more than the
+// tail it was launched with (a longer window flags its call, see resolve).
+static int ensure_tail(hpgq_ctx *c, int64_t cap) {
+  if (cap <= c->tail_cap) return HPGQ_OK;
+  const int64_t limit = (int64_t)INT32_MAX - c->p.lmax;   // tail_hi is an int
+  if (cap > limit) return HPGQ_E_INVALID;
+  int64_t nc = std::max<int64_t>(cap, c->tail_cap + c->tail_cap / 2);
+  nc = std::min<int64_t>((nc + 255) & ~(int64_t)255, limit);
+  const size_t row = (size_t)c->nm * 8 * sizeof(uint64_t);
+  HPGQ_HIP_TRY(hipStreamSynchronize(c->stream));
+  uint64_t *d = nullptr;
+  if (hipMalloc(&d, (size_t)nc * row) != hipSuccess) return HPGQ_E_NOMEM;
+  const size_t old = (size_t)c->tail_cap * row;
+  if (old) HPGQ_HIP_TRY(hipMemcpyAsync(d, c->d_tail, old, hipMemcpyDeviceToDevice, c->stream));
+  HPGQ_HIP_TRY(hipMemsetAsync(reinterpret_cast<char *>(d) + old, 0, (size_t)nc * row - old, c->stream));
+  HPGQ_HIP_TRY(hipStreamSynchronize(c->stream));
+  (void)hipFree(c->d_tail);
+  c->d_tail = d;
+  c->tail_cap = nc;
+  return HPGQ_OK;
+}
+
+static int tail_hi(const hpgq_ctx *c) {
+  return (int)std::min<int64_t>((int64_t)c->p.lmax + c->tail_cap, INT32_MAX);
+}
+
+// the chain over one batch (A: batch, outputs and options filled in).
+// record: a device-path call, kept (batch pointers + the tail's end) for the
+// tail's second pass in case one of its windows is longer than the tail
+static int launch(hpgq_ctx *c, hpgq::EngineArgs &A, bool record) {
   if (A.num_reads <= 0) return HPGQ_OK;
   if (A.num_reads > INT32_MAX) return HPGQ_E_INVALID;   // read ids are 32-bit in the follow-up stages
   A.counters = c->d_state;
-  A.err = reinterpret_cast<int32_t *>(c->d_flags + FL_ERR);
+  A.err = nullptr;
   A.report = nullptr;
+  A.tail = c->d_tail;
+  A.tail_lo = c->p.lmax;
+  A.tail_hi = tail_hi(c);
+  A.maxlen = c->d_flags + FL_MAXLEN;
+  A.need = c->d_flags + FL_NEED;
+  A.ovf = nullptr;
+  if (record && c->p.stats_on) {
+    const size_t k = c->calls.size();
+    if (k / kOvfChunk >= c->ovf_chunks.size()) {
+      uint32_t *q = nullptr;
+      if (hipMalloc(&q, kOvfChunk * 4) != hipSuccess) return HPGQ_E_NOMEM;
+      c->ovf_chunks.push_back(q);
+      HPGQ_HIP_TRY(hipMemsetAsync(q, 0, kOvfChunk * 4, c->stream));
+    }
+    A.ovf = c->ovf_chunks[k / kOvfChunk] + k % kOvfChunk;
+    CallRec r{};
+    for (int m = 0; m < c->nm; ++m) {
+      r.seq[m] = A.seq[m];
+      r.qual[m] = A.qual[m];
+      r.idx[m] = A.idx[m];
+    }
+    r.n = A.num_reads;
+    r.tail_hi = A.tail_hi;
+    c->calls.push_back(r);
+  }
   c->reduced = false;
   const int k = pick_chain(c);
   const Chain &ch = c->ch[k];
@@ -643,7 +753,7 @@ int hpgq_run_device(hpgq_ctx_t *c, const hpgq_batch_t *b, const hpgq_batch_t *b2
   if (b2) { A.seq[1] = b2->seq; A.qual[1] = b2->quality; A.idx[1] = b2->data_indices; }
   A.mask = mask_out;
   A.trim = trim_out;
-  return launch(c, A);
+  return launch(c, A, true);
 }
 
 // hand a slot's finished outputs to the caller's arrays (its D2H is done)
@@ -760,6 +870,18 @@ int hpgq_run_host(hpgq_ctx_t *c, const hpgq_batch_t *b, const hpgq_batch_t *b2,
     bytes[m] = (size_t)(ix[n] - ix[0]);
   }
   const size_t total = host_layout(c->nm, n, bytes, off, mask_off, trim_off);
+  if (c->p.stats_on) {   // the long-read tail from the batch's own offsets: this path never needs a second pass
+    int64_t ml = 0;
+    for (int m = 0; m < c->nm; ++m) {
+      const int32_t *ix = bs[m]->data_indices;
+      if ((int64_t)bytes[m] <= (int64_t)c->p.lmax + c->tail_cap) continue;   // no read can be longer
+      for (int64_t i = 0; i < n; ++i) ml = std::max<int64_t>(ml, (int64_t)ix[i + 1] - ix[i]);
+    }
+    if (ml > (int64_t)c->p.lmax + c->tail_cap) {
+      const int rc = ensure_tail(c, ml - c->p.lmax);
+      if (rc) return rc;
+    }
+  }
   // a batch written in place by hpgq_host_batch: the same slot and layout
   // (sized by the staged byte counts), no host copy
   bool in_place = false;
@@ -822,7 +944,7 @@ static int run_host_slot(hpgq_ctx *c, hpgq_ctx::Slot &sl, const hpgq_batch_t *co
   HPGQ_HIP_TRY(hipStreamWaitEvent(c->stream, sl.copied, 0));
   A.mask = mask_out ? reinterpret_cast<uint8_t *>(sl.d + mask_off) : nullptr;
   A.trim = trim_out ? reinterpret_cast<uint32_t *>(sl.d + trim_off) : nullptr;
-  rc = launch(c, A);
+  rc = launch(c, A, false);
   if (rc) return rc;
   if (mask_out)
     HPGQ_HIP_TRY(hipMemcpyAsync(sl.h + mask_off, sl.d + mask_off, (size_t)n, hipMemcpyDeviceToHost, c->stream));
@@ -840,23 +962,103 @@ static int run_host_slot(hpgq_ctx *c, hpgq_ctx::Slot &sl, const hpgq_batch_t *co
   return HPGQ_OK;
 }
 
-int hpgq_sync(hpgq_ctx_t *c) {
-  if (!c) return HPGQ_E_INVALID;
-  HPGQ_HIP_TRY(hipSetDevice(c->device));
-  // the error flag rides back on the stream: no blocking copy after the sync
-  HPGQ_HIP_TRY(hipMemcpyAsync(c->h_err, c->d_flags + FL_ERR, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+// The long-read tail's second pass (the stream is idle, h_flags current): a
+// device-path window longer than the tail its call had (FL_NEED: the longest)
+// flagged its call; grow the tail and run each flagged call's batch again
+// through the catch-all's follow-up instance in TAIL_ONLY mode over the reads
+// with a mate longer than that call's tail end, adding the positions from
+// there on and the lengths above it -- exactly what the first pass left out
+// (long_merge).  Forgets the recorded calls either way.
+static int resolve(hpgq_ctx *c) {
+  const uint32_t need = c->h_flags[FL_NEED];
+  const size_t nc = c->calls.size();
+  if (need == 0) {
+    c->calls.clear();
+    return HPGQ_OK;
+  }
+  int rc = ensure_tail(c, (int64_t)need - c->p.lmax);
+  if (rc) return rc;
+  std::vector<uint32_t> fl(nc, 0);
+  for (size_t k0 = 0; k0 < nc; k0 += kOvfChunk)
+    HPGQ_HIP_TRY(hipMemcpy(fl.data() + k0, c->ovf_chunks[k0 / kOvfChunk], std::min(kOvfChunk, nc - k0) * 4,
+                           hipMemcpyDeviceToHost));
+  uint32_t *f = c->d_flags;
+  for (size_t k = 0; k < nc; ++k) {
+    if (!fl[k]) continue;
+    const CallRec &r = c->calls[k];
+    if ((rc = ensure_bits(c, r.n))) return rc;
+    HPGQ_HIP_TRY(hipMemsetAsync(f + FL_REDO, 0, 4, c->stream));
+    hipLaunchKernelGGL(tail_bits_kernel, dim3((unsigned)((r.n + 255) / 256)), dim3(256), 0, c->stream, r.idx[0],
+                       c->nm == 2 ? r.idx[1] : nullptr, r.n, r.tail_hi, c->d_bits1, f + FL_REDO);
+    HPGQ_HIP_TRY(hipGetLastError());
+    hpgq::EngineArgs A{};
+    fill_args(c, A);
+    A.flags |= hpgq::F_TAIL_ONLY;
+    A.num_reads = r.n;
+    for (int m = 0; m < c->nm; ++m) {
+      A.seq[m] = r.seq[m];
+      A.qual[m] = r.qual[m];
+      A.idx[m] = r.idx[m];
+    }
+    A.counters = c->d_state;
+    A.tail = c->d_tail;
+    A.tail_lo = r.tail_hi;
+    A.tail_hi = tail_hi(c);
+    A.maxlen = f + FL_MAXLEN;
+    A.need = f + FL_NEED;
+    A.unit_bits = c->d_bits1;
+    A.nunits = (r.n + 63) / 64;
+    A.unit_reads = 64;
+    A.pending = f + FL_REDO;
+    A.defer_len = INT_MAX;
+    if ((rc = launch_stage(c, c->redo, A))) return rc;
+  }
+  HPGQ_HIP_TRY(hipMemsetAsync(f + FL_NEED, 0, 4, c->stream));
+  for (size_t k0 = 0; k0 < nc; k0 += kOvfChunk)
+    HPGQ_HIP_TRY(hipMemsetAsync(c->ovf_chunks[k0 / kOvfChunk], 0, std::min(kOvfChunk, nc - k0) * 4, c->stream));
+  HPGQ_HIP_TRY(hipStreamSynchronize(c->stream));
+  c->h_flags[FL_NEED] = 0;
+  c->calls.clear();
+  return HPGQ_OK;
+}
+
+// wait for the stream with the flags riding back on it (no blocking copy
+// after the sync), deliver the host-path outputs, then the tail's second pass
+static int sync_resolve(hpgq_ctx *c) {
+  HPGQ_HIP_TRY(hipMemcpyAsync(c->h_flags, c->d_flags, FL_WORDS * 4, hipMemcpyDeviceToHost, c->stream));
   HPGQ_HIP_TRY(hipStreamSynchronize(c->stream));
   for (int k = 0; k < 2; ++k) {   // the older slot first (input order of the outputs is per slot anyway)
     hpgq_ctx::Slot &sl = c->slot[c->cur_slot ^ 1 ^ k];
     if (sl.busy) slot_deliver(sl);
   }
-  return *c->h_err ? HPGQ_E_READ_TOO_LONG : HPGQ_OK;
+  return resolve(c);
+}
+
+int hpgq_sync(hpgq_ctx_t *c) {
+  if (!c) return HPGQ_E_INVALID;
+  HPGQ_HIP_TRY(hipSetDevice(c->device));
+  return sync_resolve(c);
+}
+
+int hpgq_reserve_length(hpgq_ctx_t *c, int64_t max_len) {
+  if (!c || max_len < 0 || max_len > INT32_MAX) return HPGQ_E_INVALID;
+  if (!c->p.stats_on || max_len <= (int64_t)c->p.lmax + c->tail_cap) return HPGQ_OK;
+  HPGQ_HIP_TRY(hipSetDevice(c->device));
+  return ensure_tail(c, max_len - c->p.lmax);
 }
 
 int hpgq_reset(hpgq_ctx_t *c) {
   if (!c) return HPGQ_E_INVALID;
   HPGQ_HIP_TRY(hipSetDevice(c->device));
   HPGQ_HIP_TRY(hipMemsetAsync(c->d_state, 0, state_bytes(c), c->stream));
+  if (c->tail_cap)
+    HPGQ_HIP_TRY(hipMemsetAsync(c->d_tail, 0, (size_t)c->tail_cap * c->nm * 8 * sizeof(uint64_t), c->stream));
+  // calls before the reset need no second pass any more (their flags are
+  // cleared behind them on the stream)
+  const size_t nc = c->calls.size();
+  for (size_t k0 = 0; k0 < nc; k0 += kOvfChunk)
+    HPGQ_HIP_TRY(hipMemsetAsync(c->ovf_chunks[k0 / kOvfChunk], 0, std::min(kOvfChunk, nc - k0) * 4, c->stream));
+  c->calls.clear();
   c->reduced = false;
   return HPGQ_OK;
 }
@@ -871,12 +1073,76 @@ int hpgq_read_counters(hpgq_ctx_t *c, uint64_t *out, size_t n) {
   HPGQ_HIP_TRY(hipSetDevice(c->device));
   HPGQ_HIP_TRY(hipMemcpyAsync(out, c->reduced ? c->d_global : c->d_state, c->clen * c->nm * sizeof(uint64_t),
                               hipMemcpyDeviceToHost, c->stream));
-  HPGQ_HIP_TRY(hipStreamSynchronize(c->stream));
   // the stream has run every queued batch: their masks / trims reach the
-  // caller's arrays here too, as in hpgq_sync
-  for (int k = 0; k < 2; ++k) {
-    hpgq_ctx::Slot &sl = c->slot[c->cur_slot ^ 1 ^ k];
-    if (sl.busy) slot_deliver(sl);
+  // caller's arrays here too, as in hpgq_sync; the dense set does
+  // not depend on the tail's second pass, which runs here too
+  return sync_resolve(c);
+}
+
+int hpgq_read_counters_ext(hpgq_ctx_t *c, uint64_t *out, size_t n, int32_t *lmax_ext) {
+  if (!c || !lmax_ext) return HPGQ_E_INVALID;
+  HPGQ_HIP_TRY(hipSetDevice(c->device));
+  int rc = sync_resolve(c);
+  if (rc) return rc;
+  const int lmax = c->p.lmax, nm = c->nm;
+  const uint32_t ml = c->h_flags[FL_MAXLEN];
+  int64_t T = ml > (uint32_t)lmax ? (int64_t)ml - lmax : 0;
+  const uint64_t *src_tail = c->d_tail;
+  const bool global = c->reduced && c->comm;
+  if (global) {   // the ranks agree on the tail length, then sum their tails (out of place)
+    uint32_t t32 = (uint32_t)T;
+    HPGQ_HIP_TRY(hipMemcpyAsync(c->d_scratch, &t32, 4, hipMemcpyHostToDevice, c->stream));
+    if (ncclAllReduce(c->d_scratch, c->d_scratch + 1, 1, ncclUint32, ncclMax, c->comm, c->stream) != ncclSuccess)
+      return HPGQ_E_RCCL;
+    HPGQ_HIP_TRY(hipMemcpyAsync(&t32, c->d_scratch + 1, 4, hipMemcpyDeviceToHost, c->stream));
+    HPGQ_HIP_TRY(hipStreamSynchronize(c->stream));
+    T = t32;
+    if ((rc = ensure_tail(c, T))) return rc;
+    const size_t words = (size_t)T * nm * 8;
+    if (words > c->gtail_cap) {
+      (void)hipFree(c->d_gtail);
+      c->d_gtail = nullptr;
+      c->gtail_cap = 0;
+      if (hipMalloc(&c->d_gtail, words * 8) != hipSuccess) return HPGQ_E_NOMEM;
+      c->gtail_cap = words;
+    }
+    if (words && ncclAllReduce(c->d_tail, c->d_gtail, words, ncclUint64, ncclSum, c->comm, c->stream) != ncclSuccess)
+      return HPGQ_E_RCCL;
+    src_tail = c->d_gtail;
+  }
+  const int64_t L = lmax + T;
+  *lmax_ext = (int32_t)L;
+  if (!out) {
+    if (global) HPGQ_HIP_TRY(hipStreamSynchronize(c->stream));
+    return HPGQ_OK;
+  }
+  const size_t clen_x = hpgq_counters_len((int)L);
+  if (n < clen_x * nm) return HPGQ_E_INVALID;
+  std::vector<uint64_t> dense(c->clen * nm), tail((size_t)T * nm * 8);
+  HPGQ_HIP_TRY(hipMemcpyAsync(dense.data(), c->reduced ? c->d_global : c->d_state, dense.size() * 8,
+                              hipMemcpyDeviceToHost, c->stream));
+  if (T) HPGQ_HIP_TRY(hipMemcpyAsync(tail.data(), src_tail, tail.size() * 8, hipMemcpyDeviceToHost, c->stream));
+  HPGQ_HIP_TRY(hipStreamSynchronize(c->stream));
+  // one set per mate in the layout of lmax_ext: the dense entries, then the
+  // tail's lengths lmax + 1 .. L and positions lmax .. L - 1
+  for (int m = 0; m < nm; ++m) {
+    const uint64_t *d = dense.data() + (size_t)m * c->clen;
+    uint64_t *o = out + (size_t)m * clen_x;
+    std::memset(o, 0, clen_x * 8);
+    std::memcpy(o, d, HPGQ_NUM_SCALARS * 8);
+    o[HPGQ_S_LONG_READS] = 0;   // no merged read is longer than lmax_ext
+    std::memcpy(o + hpgq_off_hist_len((int)L), d + hpgq_off_hist_len(lmax), (size_t)(lmax + 1) * 8);
+    std::memcpy(o + hpgq_off_hist_meanq((int)L), d + hpgq_off_hist_meanq(lmax), HPGQ_MEANQ_BINS * 8);
+    std::memcpy(o + hpgq_off_hist_gc((int)L), d + hpgq_off_hist_gc(lmax), HPGQ_GC_BINS * 8);
+    std::memcpy(o + hpgq_off_pos_qsum((int)L), d + hpgq_off_pos_qsum(lmax), (size_t)lmax * 8);
+    for (int b = 0; b < 5; ++b)
+      std::memcpy(o + hpgq_off_pos_base((int)L, b), d + hpgq_off_pos_base(lmax, b), (size_t)lmax * 8);
+    for (int64_t i = 0; i < T; ++i) {
+      const uint64_t *t = tail.data() + ((size_t)i * nm + m) * 8;
+      o[hpgq_off_hist_len((int)L) + lmax + 1 + i] = t[0];
+      o[hpgq_off_pos_qsum((int)L) + lmax + i] = t[1];
+      for (int b = 0; b < 5; ++b) o[hpgq_off_pos_base((int)L, b) + lmax + i] = t[2 + b];
+    }
   }
   return HPGQ_OK;
 }

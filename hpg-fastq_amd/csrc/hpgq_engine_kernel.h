@@ -32,8 +32,9 @@
 //     shift; 5 six-bit fields (A,C,G,T,N) per position in one u32, quality
 //     sums as 16-bit pairs; every 63 reads flushed into per-workgroup LDS.
 //   * reads longer than the NCH chunks the pipeline holds take a chunk loop
-//     (long_trim / long_eval): filter and edit for any length; such a read is
-//     always longer than lmax, so stats count it as a long read (error).
+//     (long_trim / long_eval): filter and edit for any length; a merged
+//     window longer than lmax is merged by long_merge (positions < lmax on
+//     chip, the rest into the ctx's long-read tail).
 //   * the workgroup epilogue adds its LDS partials into the ctx counters with
 //     one no-return u64 global atomic per nonzero entry (no slab, no fold).
 // All arithmetic is integer; results are bit-identical to the oracle.
@@ -49,7 +50,8 @@ constexpr int kChunk = 252;       // positions per chunk (63 lanes x 4)
 
 // flags (EngineArgs::flags)
 constexpr int F_FILTER = 1, F_EDIT = 2, F_STATS = 4, F_NEED_N = 8, F_NEED_OOR = 16, F_NEED_LR = 32,
-              F_OOR_LO_NONE = 64, F_OOR_HI_NONE = 128, F_OOR_ALL = 256;
+              F_OOR_LO_NONE = 64, F_OOR_HI_NONE = 128, F_OOR_ALL = 256,
+              F_TAIL_ONLY = 512;   // the long-read tail's second pass (hpgq_sync): tail entries only
 
 // One edit side's in-range test on RAW quality dwords w (biased b = w ^ 0x80,
 // range [lo, hi1) biased), branch-free: with x = w ^ 0x80 the SWAR "x >= c"
@@ -108,6 +110,15 @@ struct EngineArgs {
   // number] for the host's choice of the next call's first stage (may be null)
   uint32_t *report;
   uint32_t report_seq;
+  // ---- the long-read tail (merged windows longer than lmax; long_merge) ----
+  // [cap][NM][8] u64 from position lmax on: entry (i, m) holds 0: mate m's
+  // reads of length lmax + 1 + i, 1: its quality sum at position lmax + i,
+  // 2..6: A C G T N there (7: unused)
+  uint64_t *tail;
+  int tail_lo, tail_hi;   // positions [lo, hi) go to the tail, lengths in (lo, hi]
+  uint32_t *maxlen;       // atomicMax: the longest merged window longer than lmax
+  uint32_t *need;         // atomicMax: a window longer than tail_hi (the tail was short)
+  uint32_t *ovf;          // set to 1 when this call has such a window (nullptr: host path)
 };
 
 // ---------------------------------------------------------------------------
@@ -640,6 +651,76 @@ __device__ __forceinline__ bool long_eval(const EngineArgs &A, const ColdParams 
   return pass;
 }
 
+// ---- a merged window longer than lmax ----------------------------------------
+// The reference merges every position of every read (src/stats_fastq.c:338-382:
+// khash keyed by j < read_length, no cap).  One wave, chunk by chunk:
+// positions < lmax into the workgroup's LDS partials pa ([6][lmax]; the quality
+// added SIGNED and unbiased -- pos_fix removes the bias only for the length
+// histogram's reads -- and the A/C/G/T/N rows, :353-372), the mean-quality and
+// GC bins into the LDS histogram hm (key = round(S / n), :316-324; 100 (G + C) /
+// n, :326-334), the acc_quality term floor(65536 S / n) into fx (lane 0), and
+// positions >= lmax plus the length into the tail with global u64 atomics
+// (positions [tail_lo, tail_hi), lengths in (tail_lo, tail_hi]).  A window
+// longer than tail_hi (a device batch beyond the tail reserved so far) flags
+// the call; hpgq_sync grows the tail and merges the rest with TAIL_ONLY.
+template <int NM>
+__device__ void long_merge(const EngineArgs &A, const MateBuf &b, const ReadRef &rw, uint32_t lane4,
+                           int lane_p0, int m, uint32_t *pa, uint32_t *hm, uint64_t &fx) {
+  const int n = rw.n, lmax = A.lmax, lo = A.tail_lo, hi = A.tail_hi;
+  const bool tail_only = A.flags & F_TAIL_ONLY;
+  const int lane = threadIdx.x & 63;
+  uint64_t sq = 0, gc = 0;
+  const int cend = tail_only ? min(n, hi) : n;
+  for (int c0 = tail_only ? (lo / kChunk) * kChunk : 0; c0 < cend; c0 += kChunk) {
+    uint32_t sw, qw;
+    chunk_words(b, rw, lane4, c0, sw, qw);
+    const int p0 = c0 + lane_p0;
+    const uint32_t mk = byte_mask(n - p0);
+    sq += __builtin_amdgcn_sad_u8(qw & mk, 0u, 0u);
+    gc += (uint32_t)__builtin_popcount(zero_bytes((sw | 0x04040404u) ^ 0x47474747u) & mk & 0x80808080u);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int p = p0 + i;
+      if (p >= n) break;
+      const uint32_t sb = (sw >> (8 * i)) & 0xFFu;
+      const int q = (int)((qw >> (8 * i)) & 0xFFu) - kQBias;   // the signed char (Q13)
+      const int bi = sb == 'A' ? 0 : sb == 'C' ? 1 : sb == 'G' ? 2 : sb == 'T' ? 3 : sb == 'N' ? 4 : -1;
+      if (p < lmax) {
+        if (!tail_only) {
+          atomicAdd(&pa[p], (uint32_t)q);
+          if (bi >= 0) atomicAdd(&pa[(1 + bi) * lmax + p], 1u);
+        }
+      } else if (p >= lo && p < hi) {
+        unsigned long long *t =
+            reinterpret_cast<unsigned long long *>(A.tail + ((size_t)(p - lmax) * NM + m) * 8);
+        atomicAdd(t + 1, (unsigned long long)(long long)q);
+        if (bi >= 0) atomicAdd(t + 2 + bi, 1ull);
+      }
+    }
+  }
+  if (!tail_only) {
+    const int64_t S = (int64_t)wave_sum64(sq) - (int64_t)kQBias * n;   // the signed quality sum
+    const uint64_t g = wave_sum64(gc);
+    if (lane == 0) {
+      const int64_t n2 = 2 * (int64_t)n;
+      const int64_t key = S >= 0 ? (2 * S + n) / n2 : -((-2 * S + n) / n2);   // C round()
+      atomicAdd(&hm[lmax + 1 + (uint32_t)(key & 255)], 1u);
+      atomicAdd(&hm[lmax + 1 + HPGQ_MEANQ_BINS + (uint32_t)((100 * g) / (uint64_t)n)], 1u);
+      const int64_t t = S * 65536;
+      fx += (uint64_t)(t / n - ((t % n != 0 && t < 0) ? 1 : 0));   // floor
+      atomicMax(A.maxlen, (uint32_t)n);
+    }
+  }
+  if (lane == 0) {
+    if (lo < n && n <= hi) {
+      atomicAdd(reinterpret_cast<unsigned long long *>(A.tail + ((size_t)(n - lmax - 1) * NM + m) * 8), 1ull);
+    } else if (n > hi) {
+      atomicMax(A.need, (uint32_t)n);
+      if (A.ovf) *A.ovf = 1u;
+    }
+  }
+}
+
 // one merged read's quality-histogram bin and acc_quality term from its biased
 // quality sum sb = S + 128 n (n > 0, n <= 1024, sb < 2^19): key = round(S / n) as C's
 // round() (halves away from zero; src/stats_fastq.c:317), bin = key & 255
@@ -858,9 +939,11 @@ __global__ void __launch_bounds__(kWG) engine_kernel(EngineArgs A) {
         ReadOut out[NM];
         uint32_t sw[NM][NCH], qw[NM][NCH], mk[NM][NCH];
         bool lng[NM];
+        ReadRef rrs[NM];
 #pragma unroll
         for (int m = 0; m < NM; ++m) {
           const ReadRef rr = ref_of(os, oq, al, ln, m, j);
+          rrs[m] = rr;
           finish<NCH>(rr, grp[slot][u][m], sw[m], qw[m]);
           int ts = 0, te = 0;
           if (GEN && (A.flags & F_EDIT)) {
@@ -891,9 +974,15 @@ __global__ void __launch_bounds__(kWG) engine_kernel(EngineArgs A) {
         }
         bool pass = out[0].pass;
         if (NM == 2) pass = pass && out[NM - 1].pass;
+        const bool tail_only = A.flags & F_TAIL_ONLY;
 #pragma unroll
         for (int m = 0; m < NM; ++m) {
-          if ((A.flags & F_STATS) && pass && !lng[m]) acc[m].add(sw[m], qw[m], mk[m]);
+          if ((A.flags & F_STATS) && pass && !lng[m] && !tail_only) acc[m].add(sw[m], qw[m], mk[m]);
+          if ((A.flags & F_STATS) && pass && lng[m]) {   // longer than lmax: merged by its own chunk loop
+            ReadRef rw = shift_ref(rrs[m], out[m].ts);
+            rw.n = out[m].wn;
+            long_merge<NM>(A, mb[m], rw, lane4, lane_p0, m, pos_acc + m * 6 * lmax, hist + m * hlen, fx16[m]);
+          }
           // wn only feeds the histograms of reads <= lmax, so 16 bits suffice
           const uint32_t info = (uint32_t)min(out[m].wn, 0xFFFF) | ((uint32_t)pass << 16) |
                                 ((uint32_t)lng[m] << 17) | ((uint32_t)(out[m].ts + out[m].te > 0) << 18);
@@ -926,7 +1015,8 @@ __global__ void __launch_bounds__(kWG) engine_kernel(EngineArgs A) {
     }
 
     // ---- unit epilogue, vectorised over lanes (lane j = read j) -------------
-    const bool valid = lane < nr;
+    // (the tail's second pass counts nothing here: the first pass did)
+    const bool valid = lane < nr && !(A.flags & F_TAIL_ONLY);
 #pragma unroll
     for (int m = 0; m < NM; ++m) {
       const uint32_t info = res_info[m];
@@ -938,7 +1028,7 @@ __global__ void __launch_bounds__(kWG) engine_kernel(EngineArgs A) {
         if (m == 0 && A.mask) A.mask[rid] = (uint8_t)pass;
         if (A.trim) A.trim[(int64_t)m * A.num_reads + rid] = res_trim[m];
       }
-      cnt[m][0] += (uint32_t)nr;
+      cnt[m][0] += (A.flags & F_TAIL_ONLY) ? 0u : (uint32_t)nr;
       cnt[m][1] += (uint32_t)__builtin_popcountll(__ballot(pass));
       cnt[m][2] += (uint32_t)__builtin_popcountll(__ballot(valid && !pass));
       cnt[m][3] += (uint32_t)__builtin_popcountll(__ballot(edited));
@@ -973,6 +1063,7 @@ __global__ void __launch_bounds__(kWG) engine_kernel(EngineArgs A) {
   }
 
   // ---- workgroup epilogue ---------------------------------------------------
+  if (A.flags & F_TAIL_ONLY) return;   // (grid-uniform: nothing on chip to add)
 #pragma unroll
   for (int m = 0; m < NM; ++m) acc[m].flush(pos_acc + m * 6 * lmax, lmax, lane_p0);
 #pragma unroll
@@ -987,8 +1078,6 @@ __global__ void __launch_bounds__(kWG) engine_kernel(EngineArgs A) {
       if (cnt[m][4]) atomicAdd(&scm[HPGQ_S_NUM_STATS], (unsigned long long)cnt[m][4]);
       if (cnt[m][5]) atomicAdd(&scm[HPGQ_S_LONG_READS], (unsigned long long)cnt[m][5]);
       if (tot) atomicAdd(&scm[HPGQ_S_ACC_MEANQ_FX16], (unsigned long long)tot);
-      // a merged read the per-position counters cannot hold: the call fails
-      if (cnt[m][5] && A.err) atomicOr(A.err, 1);
     }
   }
   __syncthreads();

@@ -44,6 +44,9 @@
 #include "hpgq_common.h"
 
 #include <algorithm>
+#include <climits>
+#include <cstring>
+#include <vector>
 
 namespace hpgq {
 namespace kmers {
@@ -344,8 +347,73 @@ __global__ void __launch_bounds__(256) kmer_reduce_kernel(const uint32_t *slab, 
   if (sum) out[(size_t)(cell / kP) * npos + p] += sum;
 }
 
+// Starts >= npos of the counted reads longer than lmax (the reference's
+// counter_by_pos grows with the read, src/stats_fastq.c:394-407): the waves
+// walk the batch 64 reads at a time (one coalesced offset load + the mask
+// bytes), and each such read is taken by its wave, lanes over its starts
+// [max(lo, npos), hi), one u64 atomic per 5-mer into the tail [cap][kNum]
+// (start npos + i).  flags[0]: the longest such read (atomicMax), flags[1]:
+// the longest whose starts reach past hi -- a device batch beyond the tail
+// reserved so far; its call's flag is set and hpgq_kmers_sync adds the rest
+// (TAIL_ONLY: starts [lo, hi) only, no maxima).  A maxlen prepass of the same
+// call (lmax > 260) that found no counted read past npos + 4 ends it at once.
+__global__ void __launch_bounds__(256) kmer_long_kernel(const char *seq, const int32_t *idx, int64_t n,
+                                                        const uint8_t *mask, int npos, const int *maxlen_pre,
+                                                        unsigned long long *tail, int lo, int hi, uint32_t *flags,
+                                                        uint32_t *ovf, int tail_only) {
+  if (maxlen_pre && *maxlen_pre < npos + kK) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t r0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64; r0 < n; r0 += nw * 64) {
+    const int64_t r = r0 + lane;
+    int32_t a = 0, len = 0;
+    if (r < n && counted(mask, r)) {
+      a = idx[r];
+      len = idx[r + 1] - a;
+    }
+    uint64_t b = __ballot(len >= npos + kK);
+    while (b) {
+      const int j = __builtin_ctzll(b);
+      b &= b - 1;
+      const int32_t aj = __builtin_amdgcn_readlane(a, j), lj = __builtin_amdgcn_readlane(len, j);
+      const int last = lj - kK;   // its last start
+      if (!tail_only && lane == 0) atomicMax(&flags[0], (uint32_t)lj);
+      const int end = min(last + 1, hi);
+      const uint8_t *s = reinterpret_cast<const uint8_t *>(seq) + aj;
+      for (int p = max(lo, npos) + lane; p < end; p += 64) {
+        int id = 0;
+        bool ok = true;
+#pragma unroll
+        for (int i = 0; i < kK; ++i) {
+          const uint8_t c = s[p + i];
+          const int code = c == 'A' ? 0 : c == 'C' ? 1 : c == 'G' ? 2 : c == 'T' ? 3 : -1;
+          ok = ok && code >= 0;
+          id = id * 4 + (code & 3);
+        }
+        if (ok) atomicAdd(&tail[(size_t)(p - npos) * kNum + id], 1ull);
+      }
+      if (last + 1 > hi && lane == 0) {
+        atomicMax(&flags[1], (uint32_t)lj);
+        if (ovf) *ovf = 1u;
+      }
+    }
+  }
+}
+
 }  // namespace kmers
 }  // namespace hpgq
+
+namespace {
+// a call since the last sync, kept for the tail's second pass
+struct KCall {
+  const char *seq;
+  const int32_t *idx;
+  const uint8_t *mask;
+  int64_t n;
+  int hi;
+};
+constexpr size_t kKOvfChunk = 4096;
+}  // namespace
 
 struct hpgq_kmers {
   int device = 0;
@@ -357,7 +425,80 @@ struct hpgq_kmers {
   uint32_t *d_slab = nullptr;   // per tile workgroup: its table of the call
   int grid = 0;
   int cus = 0;
+  // the tail: [tail_cap][kNum] u64, start npos + i; d_flags [longest long
+  // read, longest one past the tail]; h_flags their pinned copy
+  unsigned long long *d_tail = nullptr;
+  int64_t tail_cap = 0;
+  uint32_t *d_flags = nullptr, *h_flags = nullptr;
+  std::vector<KCall> calls;
+  std::vector<uint32_t *> ovf_chunks;
 };
+
+namespace {
+int k_tail_hi(const hpgq_kmers *k) { return (int)std::min<int64_t>((int64_t)k->npos + k->tail_cap, INT32_MAX); }
+
+// grow the tail to starts [npos, npos + cap) (waits for the stream; zero-extended)
+int k_ensure_tail(hpgq_kmers *k, int64_t cap) {
+  if (cap <= k->tail_cap) return HPGQ_OK;
+  const int64_t limit = (int64_t)INT32_MAX - k->npos;
+  if (cap > limit) return HPGQ_E_INVALID;
+  int64_t nc = std::max<int64_t>(cap, k->tail_cap + k->tail_cap / 2);
+  nc = std::min<int64_t>((nc + 63) & ~(int64_t)63, limit);
+  const size_t row = (size_t)hpgq::kmers::kNum * 8;
+  HPGQ_HIP_TRY(hipStreamSynchronize(k->stream));
+  unsigned long long *d = nullptr;
+  if (hipMalloc(&d, (size_t)nc * row) != hipSuccess) return HPGQ_E_NOMEM;
+  const size_t old = (size_t)k->tail_cap * row;
+  if (old) HPGQ_HIP_TRY(hipMemcpyAsync(d, k->d_tail, old, hipMemcpyDeviceToDevice, k->stream));
+  HPGQ_HIP_TRY(hipMemsetAsync(reinterpret_cast<char *>(d) + old, 0, (size_t)nc * row - old, k->stream));
+  HPGQ_HIP_TRY(hipStreamSynchronize(k->stream));
+  (void)hipFree(k->d_tail);
+  k->d_tail = d;
+  k->tail_cap = nc;
+  return HPGQ_OK;
+}
+
+int k_long_grid(const hpgq_kmers *k, int64_t n) {
+  return (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4 * (int64_t)k->cus));
+}
+
+// the tail's second pass (the stream idle, h_flags current): see hpgq.h / the engine's resolve
+int k_resolve(hpgq_kmers *k) {
+  const uint32_t need = k->h_flags[1];
+  const size_t nc = k->calls.size();
+  if (need == 0) {
+    k->calls.clear();
+    return HPGQ_OK;
+  }
+  int rc = k_ensure_tail(k, (int64_t)need - hpgq::kmers::kK + 1 - k->npos);
+  if (rc) return rc;
+  std::vector<uint32_t> fl(nc, 0);
+  for (size_t k0 = 0; k0 < nc; k0 += kKOvfChunk)
+    HPGQ_HIP_TRY(hipMemcpy(fl.data() + k0, k->ovf_chunks[k0 / kKOvfChunk], std::min(kKOvfChunk, nc - k0) * 4,
+                           hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < nc; ++i) {
+    if (!fl[i]) continue;
+    const KCall &c = k->calls[i];
+    hipLaunchKernelGGL(hpgq::kmers::kmer_long_kernel, dim3((unsigned)k_long_grid(k, c.n)), dim3(256), 0, k->stream,
+                       c.seq, c.idx, c.n, c.mask, k->npos, (const int *)nullptr, k->d_tail, c.hi, k_tail_hi(k),
+                       k->d_flags, (uint32_t *)nullptr, 1);
+    HPGQ_HIP_TRY(hipGetLastError());
+  }
+  HPGQ_HIP_TRY(hipMemsetAsync(k->d_flags + 1, 0, 4, k->stream));
+  for (size_t k0 = 0; k0 < nc; k0 += kKOvfChunk)
+    HPGQ_HIP_TRY(hipMemsetAsync(k->ovf_chunks[k0 / kKOvfChunk], 0, std::min(kKOvfChunk, nc - k0) * 4, k->stream));
+  HPGQ_HIP_TRY(hipStreamSynchronize(k->stream));
+  k->h_flags[1] = 0;
+  k->calls.clear();
+  return HPGQ_OK;
+}
+
+int k_sync_resolve(hpgq_kmers *k) {
+  HPGQ_HIP_TRY(hipMemcpyAsync(k->h_flags, k->d_flags, 8, hipMemcpyDeviceToHost, k->stream));
+  HPGQ_HIP_TRY(hipStreamSynchronize(k->stream));
+  return k_resolve(k);
+}
+}  // namespace
 
 extern "C" {
 
@@ -382,11 +523,15 @@ int hpgq_kmers_open(hpgq_kmers_t **km, int device, int lmax, void *stream) {
     k->own_stream = true;
   }
   const size_t bytes = (size_t)hpgq::kmers::kNum * (size_t)(k->npos > 0 ? k->npos : 1) * 8;
-  if (hipMalloc(&k->d_out, bytes) != hipSuccess || hipMalloc(&k->d_maxlen, sizeof(int)) != hipSuccess) {
+  if (hipMalloc(&k->d_out, bytes) != hipSuccess || hipMalloc(&k->d_maxlen, sizeof(int)) != hipSuccess ||
+      hipMalloc(&k->d_flags, 8) != hipSuccess ||
+      hipHostMalloc(reinterpret_cast<void **>(&k->h_flags), 8, hipHostMallocDefault) != hipSuccess) {
     hpgq_kmers_close(k);
     return HPGQ_E_NOMEM;
   }
+  k->h_flags[0] = k->h_flags[1] = 0;
   if (hipMemsetAsync(k->d_out, 0, bytes, k->stream) != hipSuccess ||
+      hipMemsetAsync(k->d_flags, 0, 8, k->stream) != hipSuccess ||
       hipDeviceGetAttribute(&k->cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) {
     hpgq_kmers_close(k);
     return HPGQ_E_HIP;
@@ -415,13 +560,17 @@ void hpgq_kmers_close(hpgq_kmers_t *k) {
   (void)hipFree(k->d_out);
   (void)hipFree(k->d_maxlen);
   (void)hipFree(k->d_slab);
+  (void)hipFree(k->d_tail);
+  (void)hipFree(k->d_flags);
+  if (k->h_flags) (void)hipHostFree(k->h_flags);
+  for (uint32_t *q : k->ovf_chunks) (void)hipFree(q);
   if (k->own_stream) (void)hipStreamDestroy(k->stream);
   delete k;
 }
 
 int hpgq_kmers_count_device(hpgq_kmers_t *k, const hpgq_batch_t *b, const uint8_t *mask) {
   if (!k || !b || b->num_reads < 0) return HPGQ_E_INVALID;
-  if (b->num_reads == 0 || k->npos == 0) return HPGQ_OK;
+  if (b->num_reads == 0) return HPGQ_OK;
   if (!b->seq || !b->data_indices) return HPGQ_E_INVALID;
   HPGQ_HIP_TRY(hipSetDevice(k->device));
   using namespace hpgq::kmers;
@@ -434,23 +583,39 @@ int hpgq_kmers_count_device(hpgq_kmers_t *k, const hpgq_batch_t *b, const uint8_
     // few tiles (lmax <= 260): every tile is work for reads near lmax, and
     // the prepass (~30 us per 10 M reads) would cost more than it saves
     const int *ml = nullptr;
-    if (tmax > kSpill) {
+    if (tmax > kSpill) {   // (also lets the long-read pass below end at once)
       HPGQ_HIP_TRY(hipMemsetAsync(k->d_maxlen, 0, sizeof(int), k->stream));
       hipLaunchKernelGGL(kmer_maxlen_kernel, dim3((unsigned)std::min<int64_t>((n + 4095) / 4096, 8 * k->cus)),
                          dim3(1024), 0, k->stream, ix, n, mk, k->d_maxlen);
       HPGQ_HIP_TRY(hipGetLastError());
       ml = k->d_maxlen;
     }
-    if (mk)
-      hipLaunchKernelGGL(kmer_tile_kernel<true>, dim3((unsigned)k->grid), dim3(kWG), 0, k->stream, b->seq, ix, n, mk,
-                         k->npos, ml, k->d_slab);
-    else
-      hipLaunchKernelGGL(kmer_tile_kernel<false>, dim3((unsigned)k->grid), dim3(kWG), 0, k->stream, b->seq, ix, n, mk,
-                         k->npos, ml, k->d_slab);
-    HPGQ_HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(kmer_reduce_kernel, dim3((unsigned)(((int64_t)tmax * kP * kNum + 255) / 256)), dim3(256), 0,
-                       k->stream, (const uint32_t *)k->d_slab, k->npos, ml, k->grid, k->d_out);
-    HPGQ_HIP_TRY(hipGetLastError());
+    if (k->npos > 0) {   // (lmax < 5: every start is in the tail)
+      if (mk)
+        hipLaunchKernelGGL(kmer_tile_kernel<true>, dim3((unsigned)k->grid), dim3(kWG), 0, k->stream, b->seq, ix, n, mk,
+                           k->npos, ml, k->d_slab);
+      else
+        hipLaunchKernelGGL(kmer_tile_kernel<false>, dim3((unsigned)k->grid), dim3(kWG), 0, k->stream, b->seq, ix, n, mk,
+                           k->npos, ml, k->d_slab);
+      HPGQ_HIP_TRY(hipGetLastError());
+      hipLaunchKernelGGL(kmer_reduce_kernel, dim3((unsigned)(((int64_t)tmax * kP * kNum + 255) / 256)), dim3(256), 0,
+                         k->stream, (const uint32_t *)k->d_slab, k->npos, ml, k->grid, k->d_out);
+      HPGQ_HIP_TRY(hipGetLastError());
+    }
+    {   // starts >= npos of longer reads; the call is kept for the second pass
+      const size_t i = k->calls.size();
+      if (i / kKOvfChunk >= k->ovf_chunks.size()) {
+        uint32_t *q = nullptr;
+        if (hipMalloc(&q, kKOvfChunk * 4) != hipSuccess) return HPGQ_E_NOMEM;
+        k->ovf_chunks.push_back(q);
+        HPGQ_HIP_TRY(hipMemsetAsync(q, 0, kKOvfChunk * 4, k->stream));
+      }
+      uint32_t *ovf = k->ovf_chunks[i / kKOvfChunk] + i % kKOvfChunk;
+      k->calls.push_back(KCall{b->seq, ix, mk, n, k_tail_hi(k)});
+      hipLaunchKernelGGL(kmer_long_kernel, dim3((unsigned)k_long_grid(k, n)), dim3(256), 0, k->stream, b->seq, ix, n,
+                         mk, k->npos, ml, k->d_tail, k->npos, k_tail_hi(k), k->d_flags, ovf, 0);
+      HPGQ_HIP_TRY(hipGetLastError());
+    }
   }
   return HPGQ_OK;
 }
@@ -458,14 +623,53 @@ int hpgq_kmers_count_device(hpgq_kmers_t *k, const hpgq_batch_t *b, const uint8_
 int hpgq_kmers_sync(hpgq_kmers_t *k) {
   if (!k) return HPGQ_E_INVALID;
   HPGQ_HIP_TRY(hipSetDevice(k->device));
-  HPGQ_HIP_TRY(hipStreamSynchronize(k->stream));
-  return HPGQ_OK;
+  return k_sync_resolve(k);
 }
 
 int hpgq_kmers_reset(hpgq_kmers_t *k) {
   if (!k) return HPGQ_E_INVALID;
   HPGQ_HIP_TRY(hipSetDevice(k->device));
-  HPGQ_HIP_TRY(hipMemsetAsync(k->d_out, 0, hpgq_kmers_size(k) * 8, k->stream));
+  if (hpgq_kmers_size(k)) HPGQ_HIP_TRY(hipMemsetAsync(k->d_out, 0, hpgq_kmers_size(k) * 8, k->stream));
+  if (k->tail_cap)
+    HPGQ_HIP_TRY(hipMemsetAsync(k->d_tail, 0, (size_t)k->tail_cap * hpgq::kmers::kNum * 8, k->stream));
+  HPGQ_HIP_TRY(hipMemsetAsync(k->d_flags, 0, 8, k->stream));
+  const size_t nc = k->calls.size();
+  for (size_t k0 = 0; k0 < nc; k0 += kKOvfChunk)
+    HPGQ_HIP_TRY(hipMemsetAsync(k->ovf_chunks[k0 / kKOvfChunk], 0, std::min(kKOvfChunk, nc - k0) * 4, k->stream));
+  k->calls.clear();
+  return HPGQ_OK;
+}
+
+int hpgq_kmers_reserve_length(hpgq_kmers_t *k, int64_t max_len) {
+  if (!k || max_len < 0 || max_len > INT32_MAX) return HPGQ_E_INVALID;
+  const int64_t cap = max_len - (hpgq::kmers::kK - 1) - k->npos;   // starts npos .. max_len - 5
+  if (cap <= k->tail_cap) return HPGQ_OK;
+  HPGQ_HIP_TRY(hipSetDevice(k->device));
+  return k_ensure_tail(k, cap);
+}
+
+int hpgq_kmers_read_ext(hpgq_kmers_t *k, uint64_t *by_pos, size_t n, int32_t *npos_ext) {
+  if (!k || !npos_ext) return HPGQ_E_INVALID;
+  HPGQ_HIP_TRY(hipSetDevice(k->device));
+  const int rc = k_sync_resolve(k);
+  if (rc) return rc;
+  using hpgq::kmers::kNum;
+  const uint32_t ml = k->h_flags[0];   // the longest counted read with starts >= npos
+  const int64_t T = ml ? (int64_t)ml - (hpgq::kmers::kK - 1) - k->npos : 0;
+  const int64_t P = k->npos + T;
+  *npos_ext = (int32_t)P;
+  if (!by_pos) return HPGQ_OK;
+  if (n < (size_t)kNum * (size_t)P) return HPGQ_E_INVALID;
+  std::vector<uint64_t> dense((size_t)kNum * k->npos), tail((size_t)T * kNum);
+  if (!dense.empty())
+    HPGQ_HIP_TRY(hipMemcpyAsync(dense.data(), k->d_out, dense.size() * 8, hipMemcpyDeviceToHost, k->stream));
+  if (T) HPGQ_HIP_TRY(hipMemcpyAsync(tail.data(), k->d_tail, tail.size() * 8, hipMemcpyDeviceToHost, k->stream));
+  HPGQ_HIP_TRY(hipStreamSynchronize(k->stream));
+  for (int id = 0; id < kNum; ++id) {
+    uint64_t *o = by_pos + (size_t)id * P;
+    if (k->npos) std::memcpy(o, dense.data() + (size_t)id * k->npos, (size_t)k->npos * 8);
+    for (int64_t i = 0; i < T; ++i) o[k->npos + i] = tail[(size_t)i * kNum + id];
+  }
   return HPGQ_OK;
 }
 
@@ -476,7 +680,8 @@ size_t hpgq_kmers_size(const hpgq_kmers_t *k) {
 int hpgq_kmers_read(hpgq_kmers_t *k, uint64_t *by_pos, size_t n) {
   if (!k || (!by_pos && n) || n < hpgq_kmers_size(k)) return HPGQ_E_INVALID;
   HPGQ_HIP_TRY(hipSetDevice(k->device));
-  HPGQ_HIP_TRY(hipStreamSynchronize(k->stream));
+  const int rc = k_sync_resolve(k);
+  if (rc) return rc;
   if (hpgq_kmers_size(k))
     HPGQ_HIP_TRY(hipMemcpy(by_pos, k->d_out, hpgq_kmers_size(k) * 8, hipMemcpyDeviceToHost));
   return HPGQ_OK;

@@ -86,10 +86,8 @@ __device__ __forceinline__ uint32_t line_end(const uint8_t *t, uint32_t b, uint3
   return (e > b && t[e - 1] == '\r') ? e - 1 : e;
 }
 
-__global__ void __launch_bounds__(256) record_kernel(const uint8_t *t, const uint32_t *nl, int64_t nrec,
-                                                     Rec R, int32_t *bad) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i >= nrec) return;
+// record i: its line bounds, the checks, its length (0 when malformed)
+__device__ __forceinline__ int32_t record_one(const uint8_t *t, const uint32_t *nl, int64_t i, Rec R, int32_t *bad) {
   const uint32_t start = i ? nl[4 * i - 1] + 1 : 0u;
   const uint32_t n0 = nl[4 * i], n1 = nl[4 * i + 1], n2 = nl[4 * i + 2], n3 = nl[4 * i + 3];
   const uint32_t sb = n0 + 1, se = line_end(t, sb, n1);
@@ -101,6 +99,18 @@ __global__ void __launch_bounds__(256) record_kernel(const uint8_t *t, const uin
   R.qual[i] = qb;
   R.len[i] = ok ? (int32_t)(se - sb) : 0;
   if (!ok) atomicMin(bad, (int32_t)min<int64_t>(i, 0x7FFFFFFF));
+  return ok ? (int32_t)(se - sb) : 0;
+}
+
+// bad[0]: the first malformed record (atomicMin); bad[1]: the longest record
+// (the long-read tail's reservation, hpgq_parser_max_length)
+__global__ void __launch_bounds__(256) record_kernel(const uint8_t *t, const uint32_t *nl, int64_t nrec,
+                                                     Rec R, int32_t *bad) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  int32_t len = 0;
+  if (i < nrec) len = record_one(t, nl, i, R, bad);
+  for (int o = 32; o > 0; o >>= 1) len = max(len, __shfl_xor(len, o));
+  if ((threadIdx.x & 63) == 0 && len > 0) atomicMax(bad + 1, len);
 }
 
 // one wave per record
@@ -140,6 +150,7 @@ struct hpgq_parser {
   void *d_tmp = nullptr;
   size_t tmp_cap = 0;
   int64_t last_n = 0;            // records of the last parse
+  int64_t max_len = 0;           // its longest record
 };
 
 static int grow(void **p, size_t *cap, size_t need) {
@@ -197,7 +208,7 @@ int hpgq_parser_open(hpgq_parser_t **ps, int device, void *stream) {
     HPGQ_HIP_TRY(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
     p->own_stream = true;
   }
-  HPGQ_HIP_TRY(hipMalloc(&p->d_bad, 4));
+  HPGQ_HIP_TRY(hipMalloc(&p->d_bad, 8));
   *ps = p;
   return HPGQ_OK;
 }
@@ -248,6 +259,7 @@ int hpgq_parse_device(hpgq_parser_t *p, const char *text, int64_t n, hpgq_batch_
   if (!p || !out || n < 0 || n >= ((int64_t)1 << 31)) return HPGQ_E_INVALID;
   *out = hpgq_batch_t{0, nullptr, nullptr, nullptr};
   p->last_n = 0;
+  p->max_len = 0;
   HPGQ_HIP_TRY(hipSetDevice(p->device));
   for (bool more = n > 0; more;) {   // drop trailing blank lines
     char tail[64];
@@ -296,8 +308,9 @@ int hpgq_parse_device(hpgq_parser_t *p, const char *text, int64_t n, hpgq_batch_
     p->rec_cap = c;
   }
   Rec R{p->d_rec, p->d_rec + p->rec_cap, p->d_rec + 2 * p->rec_cap, p->d_rec + 3 * p->rec_cap, p->d_len};
-  const int32_t big = 0x7FFFFFFF;
-  HPGQ_HIP_TRY(hipMemcpyAsync(p->d_bad, &big, 4, hipMemcpyHostToDevice, p->stream));
+  const int32_t init[2] = {0x7FFFFFFF, 0};   // first malformed record, longest record
+  const int32_t big = init[0];
+  HPGQ_HIP_TRY(hipMemcpyAsync(p->d_bad, init, 8, hipMemcpyHostToDevice, p->stream));
   record_kernel<<<(unsigned)((nrec + 255) / 256), 256, 0, p->stream>>>(t, p->d_nl, nrec, R, p->d_bad);
   HPGQ_HIP_TRY(hipGetLastError());
   // 4. data_indices = [0, inclusive scan of the lengths]
@@ -306,11 +319,11 @@ int hpgq_parse_device(hpgq_parser_t *p, const char *text, int64_t n, hpgq_batch_
   HPGQ_HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, tb, p->d_len, p->d_idx + 1, (int)nrec, p->stream));
   if (scan_tmp(p, tb)) return HPGQ_E_NOMEM;
   HPGQ_HIP_TRY(hipcub::DeviceScan::InclusiveSum(p->d_tmp, tb, p->d_len, p->d_idx + 1, (int)nrec, p->stream));
-  int32_t bad = 0, data_end = 0;
-  HPGQ_HIP_TRY(hipMemcpyAsync(&bad, p->d_bad, 4, hipMemcpyDeviceToHost, p->stream));
+  int32_t bad[2] = {0, 0}, data_end = 0;
+  HPGQ_HIP_TRY(hipMemcpyAsync(bad, p->d_bad, 8, hipMemcpyDeviceToHost, p->stream));
   HPGQ_HIP_TRY(hipMemcpyAsync(&data_end, p->d_idx + nrec, 4, hipMemcpyDeviceToHost, p->stream));
   HPGQ_HIP_TRY(hipStreamSynchronize(p->stream));
-  if (bad != big) return HPGQ_E_FORMAT;
+  if (bad[0] != big) return HPGQ_E_FORMAT;
   // 5. the batch bytes (+ the engine's readable slack)
   const size_t need = (size_t)data_end + HPGQ_DEVICE_SLACK + 64;
   if (need > p->data_cap) {
@@ -330,6 +343,7 @@ int hpgq_parse_device(hpgq_parser_t *p, const char *text, int64_t n, hpgq_batch_
   out->quality = reinterpret_cast<const char *>(p->d_qual);
   out->data_indices = p->d_idx;
   p->last_n = nrec;
+  p->max_len = bad[1];
   return HPGQ_OK;
 }
 
@@ -356,5 +370,7 @@ int hpgq_parse_records(hpgq_parser_t *p, uint32_t *rec_start, uint32_t *seq_star
 }
 
 void *hpgq_parser_stream(hpgq_parser_t *p) { return p ? (void *)p->stream : nullptr; }
+
+int64_t hpgq_parser_max_length(hpgq_parser_t *p) { return p ? p->max_len : 0; }
 
 }  // extern "C"

@@ -43,16 +43,17 @@ int main(int argc, char **argv) {
   }
   if (!o->quiet) cli_display(o);
 
-  const size_t clen = hpgq_counters_len(p.lmax);
-  uint64_t *counters = calloc(clen, sizeof(uint64_t));
   cli_result_t r;
-  int rc = cli_run(o, &p, counters, &r);
+  int rc = cli_run(o, &p, &r);
   if (rc) {
     fprintf(stderr, "\nError: %s (%d)\n", hpgq_strerror(rc), rc);
-    free(counters);
+    free(r.counters);
     cli_free(o);
     return 1;
   }
+  /* (the full-length set: layout of r.lmax = max(--lmax, longest merged read)) */
+  const uint64_t *counters = r.counters;
+  const size_t clen = hpgq_counters_len(r.lmax) * (p.paired ? 2 : 1);
   if (o->counters_out) {
     FILE *f = fopen(o->counters_out, "wb");
     if (!f || fwrite(counters, sizeof(uint64_t), clen, f) != clen) rc = 1;
@@ -72,7 +73,7 @@ int main(int argc, char **argv) {
       rc = 1;
     if (f) fclose(f);
   }
-  if (cmd == CMD_STATS && cli_report(o, &p, counters, &r)) rc = 1;
+  if (cmd == CMD_STATS && cli_report(o, &p, &r)) rc = 1;
 
   if (!o->quiet) {
     printf("\n\nRESULTS\n");
@@ -106,7 +107,7 @@ int main(int argc, char **argv) {
            r.seconds > 0 ? r.num_reads / r.seconds / 1e6 : 0.0, r.num_gpus, r.num_gpus == 1 ? "" : "s");
     printf("=================================================\n");
   }
-  free(counters);
+  free(r.counters);
   free(r.kmers);
   free(r.cg_seq);
   free(r.cg_q);

@@ -71,6 +71,8 @@ int cli_parse_range(int *min, int *max, const char *range, const char *msg);
 
 /* pipeline: returns 0 or a negative HPGQ_E* code */
 typedef struct {
+  uint64_t *counters;       /* the merged counter set(s) at full length (malloc'd) */
+  int lmax;                 /* their layout's lmax: max(--lmax, longest merged read) */
   uint64_t num_reads, num_passed, num_failed, num_edited;
   double seconds, fastq_bytes;
   uint64_t *kmers;          /* --kmers: by_pos [HPGQ_NUM_KMERS][kmers_npos] (malloc'd) */
@@ -82,10 +84,9 @@ typedef struct {
   int writer;               /* filter / edit outputs: 1 mapped files (parallel copy), 2 stream writer */
 } cli_result_t;
 
-int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, cli_result_t *res);
+int cli_run(const cli_options_t *o, const hpgq_params_t *p, cli_result_t *res);
 
 /* src/stats_report.c: summary + data files (+ k-mer files when res->kmers) */
-int cli_report(const cli_options_t *o, const hpgq_params_t *p, const uint64_t *counters,
-               const cli_result_t *res);
+int cli_report(const cli_options_t *o, const hpgq_params_t *p, const cli_result_t *res);
 
 #endif

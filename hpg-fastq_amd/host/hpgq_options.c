@@ -303,6 +303,11 @@ cli_options_t *cli_parse(int command, const char *exec_name, int argc, char **ar
     printf("\nError: Nothing to edit, no edit options specified !\n");
     usage(o);
   }
+  /* trims are two 16-bit fields (libhpgq's trim_out): HPGQ_MAX_EDIT_LENGTH */
+  if (command == CMD_EDIT && (o->left_length > HPGQ_MAX_EDIT_LENGTH || o->right_length > HPGQ_MAX_EDIT_LENGTH)) {
+    printf("\nError: --left-length and --right-length must be at most %d\n", HPGQ_MAX_EDIT_LENGTH);
+    exit(-1);
+  }
   return o;
 }
 

@@ -830,6 +830,11 @@ static int worker_chunk(worker_t *W, slot_t *s) {
     rc = hpgq_device_alloc(W->device, (void **)&W->d_mask, W->dcap);
     if (rc == 0) rc = hpgq_device_alloc(W->device, (void **)&W->d_trim, W->dcap * 4);
   }
+  if (rc == 0) {   /* the long-read tails for the unit's longest record: no second pass */
+    const int64_t ml = hpgq_parser_max_length(W->ps);
+    rc = hpgq_reserve_length(W->ctx, ml);
+    if (rc == 0 && W->km) rc = hpgq_kmers_reserve_length(W->km, ml);
+  }
   if (rc == 0) rc = hpgq_run_device(W->ctx, &b, NULL, need_mask ? W->d_mask : NULL, edit ? W->d_trim : NULL);
   if (rc == 0 && W->km) rc = hpgq_kmers_count_device(W->km, &b, o->filter_on ? W->d_mask : NULL);
   if (rc == 0 && writes) {
@@ -890,7 +895,23 @@ static void *worker_main(void *arg) {
   return NULL;
 }
 
-int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, cli_result_t *res) {
+/* dst (nm sets, layout of lmax ld) += src (nm sets, layout of lmax ls <= ld):
+ * the workers' full-length counter sets (hpgq_read_counters_ext) */
+static void add_relayout(uint64_t *dst, int ld, const uint64_t *src, int ls, int nm) {
+  for (int m = 0; m < nm; ++m) {
+    uint64_t *d = dst + (size_t)m * hpgq_counters_len(ld);
+    const uint64_t *x = src + (size_t)m * hpgq_counters_len(ls);
+    for (int i = 0; i < HPGQ_NUM_SCALARS; ++i) d[i] += x[i];
+    for (int i = 0; i <= ls; ++i) d[hpgq_off_hist_len(ld) + i] += x[hpgq_off_hist_len(ls) + i];
+    for (int i = 0; i < HPGQ_MEANQ_BINS; ++i) d[hpgq_off_hist_meanq(ld) + i] += x[hpgq_off_hist_meanq(ls) + i];
+    for (int i = 0; i < HPGQ_GC_BINS; ++i) d[hpgq_off_hist_gc(ld) + i] += x[hpgq_off_hist_gc(ls) + i];
+    for (int i = 0; i < ls; ++i) d[hpgq_off_pos_qsum(ld) + i] += x[hpgq_off_pos_qsum(ls) + i];
+    for (int b = 0; b < 5; ++b)
+      for (int i = 0; i < ls; ++i) d[hpgq_off_pos_base(ld, b) + i] += x[hpgq_off_pos_base(ls, b) + i];
+  }
+}
+
+int cli_run(const cli_options_t *o, const hpgq_params_t *p, cli_result_t *res) {
   pipe_t P;
   memset(&P, 0, sizeof(P));
   P.trace = getenv("HPGQ_TRACE") != NULL;
@@ -997,31 +1018,48 @@ int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, 
     rc = P.error < 0 && P.error != HPGQ_E_FORMAT && P.error != HPGQ_E_IO ? HPGQ_E_INVALID : P.error;
 
   /* the read-sharded merge: device counters, k-mer and CGR tables summed over
-   * the workers (u64; CGR u32, which wraps like the reference's tables) */
-  const size_t clen = hpgq_counters_size(W[0].ctx);
-  uint64_t *part = rc == 0 ? calloc(clen, sizeof(uint64_t)) : NULL;
-  if (rc == 0 && !part) rc = HPGQ_E_NOMEM;
-  if (rc == 0) memset(counters, 0, clen * sizeof(uint64_t));
+   * the workers (u64; CGR u32, which wraps like the reference's tables).  The
+   * counters and k-mer tables come at full length (the long-read tails,
+   * hpgq_read_counters_ext / hpgq_kmers_read_ext): each worker's in the
+   * layout of its own longest read, summed into the longest one's */
+  const int nm = p->paired ? 2 : 1;
+  int L = p->lmax, KP = 0;
   for (int w = 0; w < G && rc == 0; ++w) {
-    rc = hpgq_sync(W[w].ctx);   /* surfaces HPGQ_E_READ_TOO_LONG */
-    if (rc == 0) rc = hpgq_read_counters(W[w].ctx, part, clen);
-    for (size_t i = 0; rc == 0 && i < clen; ++i) counters[i] += part[i];
+    int32_t lw = 0;
+    rc = hpgq_read_counters_ext(W[w].ctx, NULL, 0, &lw);
+    if (lw > L) L = lw;
+    if (rc == 0 && o->kmers_on) rc = hpgq_kmers_read_ext(W[w].km, NULL, 0, &lw);
+    if (o->kmers_on && lw > KP) KP = lw;
+  }
+  res->lmax = L;
+  res->counters = rc == 0 ? calloc(hpgq_counters_len(L) * nm, sizeof(uint64_t)) : NULL;
+  if (rc == 0 && !res->counters) rc = HPGQ_E_NOMEM;
+  for (int w = 0; w < G && rc == 0; ++w) {
+    int32_t lw = 0;
+    rc = hpgq_read_counters_ext(W[w].ctx, NULL, 0, &lw);
+    uint64_t *part = rc == 0 ? calloc(hpgq_counters_len(lw) * nm, sizeof(uint64_t)) : NULL;
+    if (rc == 0 && !part) rc = HPGQ_E_NOMEM;
+    if (rc == 0) rc = hpgq_read_counters_ext(W[w].ctx, part, hpgq_counters_len(lw) * nm, &lw);
+    if (rc == 0) add_relayout(res->counters, L, part, lw, nm);
+    free(part);
     res->num_reads += W[w].num_reads;
     res->fastq_bytes += W[w].fastq_bytes;
     res->cg_exact_calls += W[w].cg_exact_calls;
   }
-  free(part);
   if (rc == 0 && o->kmers_on) {
-    const size_t kn = hpgq_kmers_size(W[0].km);
-    res->kmers_npos = p->lmax > HPGQ_KMER_K - 1 ? p->lmax - (HPGQ_KMER_K - 1) : 0;
-    res->kmers = calloc(kn + 1, sizeof(uint64_t));
-    uint64_t *kp = calloc(kn + 1, sizeof(uint64_t));
-    if (!res->kmers || !kp) rc = HPGQ_E_NOMEM;
+    res->kmers_npos = KP;
+    res->kmers = calloc((size_t)HPGQ_NUM_KMERS * KP + 1, sizeof(uint64_t));
+    if (!res->kmers) rc = HPGQ_E_NOMEM;
     for (int w = 0; w < G && rc == 0; ++w) {
-      rc = hpgq_kmers_read(W[w].km, kp, kn);
-      for (size_t i = 0; rc == 0 && i < kn; ++i) res->kmers[i] += kp[i];
+      int32_t pw = 0;
+      rc = hpgq_kmers_read_ext(W[w].km, NULL, 0, &pw);
+      uint64_t *kp = rc == 0 ? calloc((size_t)HPGQ_NUM_KMERS * pw + 1, sizeof(uint64_t)) : NULL;
+      if (rc == 0 && !kp) rc = HPGQ_E_NOMEM;
+      if (rc == 0) rc = hpgq_kmers_read_ext(W[w].km, kp, (size_t)HPGQ_NUM_KMERS * pw, &pw);
+      for (int id = 0; rc == 0 && id < HPGQ_NUM_KMERS; ++id)
+        for (int j = 0; j < pw; ++j) res->kmers[(size_t)id * KP + j] += kp[(size_t)id * pw + j];
+      free(kp);
     }
-    free(kp);
   }
   if (rc == 0 && o->cg_on) {
     const size_t cells = (size_t)1 << (2 * o->k_cg);
@@ -1050,9 +1088,9 @@ int cli_run(const cli_options_t *o, const hpgq_params_t *p, uint64_t *counters, 
             (long long)k, 1e3 * P.tr[k][0], 1e3 * P.tr[k][1], P.tw[k], 1e3 * P.tr[k][2], 1e3 * P.tr[k][4],
             1e3 * P.tr[k][5], 1e3 * P.tr[k][3], 1e3 * P.tr[k][6], 1e3 * P.tr[k][7]);
   if (rc == 0) {
-    res->num_passed = counters[HPGQ_S_NUM_PASSED];
-    res->num_failed = counters[HPGQ_S_NUM_FAILED];
-    res->num_edited = counters[HPGQ_S_NUM_EDITED];
+    res->num_passed = res->counters[HPGQ_S_NUM_PASSED];
+    res->num_failed = res->counters[HPGQ_S_NUM_FAILED];
+    res->num_edited = res->counters[HPGQ_S_NUM_EDITED];
   }
 
 done:

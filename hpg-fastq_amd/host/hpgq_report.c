@@ -144,9 +144,10 @@ static int report_cg(const cli_options_t *o, const char *base, const cli_result_
   return rc;
 }
 
-int cli_report(const cli_options_t *o, const hpgq_params_t *p, const uint64_t *c,
-               const cli_result_t *res) {
-  const int lmax = p->lmax, phred = p->phred;
+int cli_report(const cli_options_t *o, const hpgq_params_t *p, const cli_result_t *res) {
+  /* the full-length set: every merged read at every position (res->lmax >= --lmax) */
+  const uint64_t *c = res->counters;
+  const int lmax = res->lmax, phred = p->phred;
   const char *slash = strrchr(o->in_filename, '/');
   const char *base = slash ? slash + 1 : o->in_filename;
   hpgq_summary_t s;

@@ -9,7 +9,7 @@ from ._abi import (  # noqa: F401
     LIB_PATH, lib, HpgqError, Params, Batch, Synth, Summary,
     NUM_SCALARS, S_NUM_INPUT, S_NUM_PASSED, S_NUM_FAILED, S_NUM_EDITED,
     S_NUM_STATS, S_ACC_MEANQ_FX16, S_LONG_READS, MEANQ_BINS, GC_BINS,
-    NO_VALUE, MIN_VALUE, MAX_VALUE, LMAX_LIMIT, DEVICE_SLACK, CGR_ALL_READS, CGR_ONLY_VALID_READS, CGR_PATH_AUTO, CGR_PATH_EXACT,
+    NO_VALUE, MIN_VALUE, MAX_VALUE, LMAX_LIMIT, MAX_EDIT_LENGTH, DEVICE_SLACK, CGR_ALL_READS, CGR_ONLY_VALID_READS, CGR_PATH_AUTO, CGR_PATH_EXACT,
     counters_len, layout, check, params_default, exported_symbols,
 )
 from .engine import Engine, ChaosGame, Kmers, Parser, summary, complete_prefix  # noqa: F401

@@ -9,6 +9,7 @@ LIB_PATH = os.environ.get("HPGQ_LIB_PATH") or os.path.join(os.path.dirname(_HERE
 
 NO_VALUE, MIN_VALUE, MAX_VALUE = -1, 0, 100000
 LMAX_LIMIT = 1024
+MAX_EDIT_LENGTH = 65535   # edit windows: trims are two 16-bit fields
 DEVICE_SLACK = 8   # readable bytes past the data end of device seq/quality buffers
 NUM_SCALARS = 8
 (S_NUM_INPUT, S_NUM_PASSED, S_NUM_FAILED, S_NUM_EDITED,
@@ -24,7 +25,7 @@ ROUTES = {"auto": ROUTE_AUTO, "single": ROUTE_CATCH_ALL, "tri": ROUTE_FIRST_TRI,
           "auto_fixed": ROUTE_AUTO | ROUTE_NO_ADAPTIVE}
 
 ERRORS = {0: "ok", -1: "invalid argument", -2: "HIP runtime error", -3: "out of memory",
-          -4: "read longer than lmax", -5: "no HIP device", -6: "RCCL error",
+          -4: "read longer than lmax (not returned since round 6)", -5: "no HIP device", -6: "RCCL error",
           -7: "invalid ctx state", -8: "malformed FASTQ text"}
 
 
@@ -106,6 +107,8 @@ _SIGS = [
     ("hpgq_host_batch", C.c_int, [C.c_void_p, C.c_int64, C.c_size_t, C.c_size_t,
                                   C.POINTER(Batch), C.POINTER(Batch)]),
     ("hpgq_sync", C.c_int, [C.c_void_p]),
+    ("hpgq_reserve_length", C.c_int, [C.c_void_p, C.c_int64]),
+    ("hpgq_read_counters_ext", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_int32)]),
     ("hpgq_reset", C.c_int, [C.c_void_p]),
     ("hpgq_counters_size", C.c_size_t, [C.c_void_p]),
     ("hpgq_read_counters", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
@@ -149,6 +152,8 @@ _SIGS = [
     ("hpgq_kmers_size", C.c_size_t, [C.c_void_p]),
     ("hpgq_kmers_read", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
     ("hpgq_kmers_device", C.c_void_p, [C.c_void_p]),
+    ("hpgq_kmers_reserve_length", C.c_int, [C.c_void_p, C.c_int64]),
+    ("hpgq_kmers_read_ext", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_int32)]),
     ("hpgq_synth_length", C.c_int32, [C.POINTER(Synth), C.c_int64]),
     ("hpgq_synth_indices_host", C.c_int, [C.POINTER(Synth), C.c_int64, C.c_int64, C.c_void_p]),
     ("hpgq_synth_device", C.c_int, [C.POINTER(Synth), C.c_int64, C.c_int64, C.c_void_p,
@@ -160,6 +165,7 @@ _SIGS = [
     ("hpgq_parse_device", C.c_int, [C.c_void_p, C.c_void_p, C.c_int64, C.POINTER(Batch)]),
     ("hpgq_parse_records", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     ("hpgq_parser_stream", C.c_void_p, [C.c_void_p]),
+    ("hpgq_parser_max_length", C.c_int64, [C.c_void_p]),
     ("hpgq_device_count", C.c_int, []),
     ("hpgq_device_numa_node", C.c_int, [C.c_int]),
     ("hpgq_strerror", C.c_char_p, [C.c_int]),

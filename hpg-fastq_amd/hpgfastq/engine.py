@@ -117,11 +117,27 @@ class Engine:
     def reset(self):
         check(lib.hpgq_reset(self._h), "hpgq_reset")
 
+    def reserve_length(self, max_len):
+        """hpgq_reserve_length: the long-read tail for merged reads up to max_len."""
+        check(lib.hpgq_reserve_length(self._h, int(max_len)), "hpgq_reserve_length")
+
     def counters(self):
         n = lib.hpgq_counters_size(self._h)
         out = np.zeros(n, dtype=np.uint64)
         check(lib.hpgq_read_counters(self._h, _ptr(out), n), "hpgq_read_counters")
         return out
+
+    def counters_ext(self):
+        """hpgq_read_counters_ext -> (counters of every merged read at full
+        length in the layout of lmax_ext, lmax_ext).  Collective after
+        allreduce() (every rank calls it)."""
+        L = C.c_int32(0)
+        check(lib.hpgq_read_counters_ext(self._h, None, 0, C.byref(L)), "hpgq_read_counters_ext")
+        out = np.zeros(counters_len(L.value) * self.nsets, dtype=np.uint64)
+        L2 = C.c_int32(0)
+        check(lib.hpgq_read_counters_ext(self._h, _ptr(out), out.size, C.byref(L2)), "hpgq_read_counters_ext")
+        assert L2.value == L.value
+        return out, L.value
 
     def counters_device_ptr(self):
         return lib.hpgq_counters_device(self._h)
@@ -321,6 +337,17 @@ class Kmers:
         check(lib.hpgq_kmers_read(self._h, _ptr(out), out.size), "hpgq_kmers_read")
         return out
 
+    def reserve_length(self, max_len):
+        check(lib.hpgq_kmers_reserve_length(self._h, int(max_len)), "hpgq_kmers_reserve_length")
+
+    def by_pos_ext(self):
+        """hpgq_kmers_read_ext: every start, [1024, npos_ext]."""
+        P = C.c_int32(0)
+        check(lib.hpgq_kmers_read_ext(self._h, None, 0, C.byref(P)), "hpgq_kmers_read_ext")
+        out = np.zeros((1024, P.value), dtype=np.uint64)
+        check(lib.hpgq_kmers_read_ext(self._h, _ptr(out), out.size, C.byref(P)), "hpgq_kmers_read_ext")
+        return out
+
 
 def complete_prefix(buf, at_eof=False):
     """hpgq_fastq_complete_prefix: bytes of `buf` holding whole FASTQ records."""
@@ -360,6 +387,11 @@ class Parser:
         check(lib.hpgq_parse_host(self._h, text, len(text), C.byref(b)), "hpgq_parse_host")
         self.num_reads = int(b.num_reads)
         return b
+
+    @property
+    def max_length(self):
+        """The longest record of the last parse (hpgq_parser_max_length)."""
+        return int(lib.hpgq_parser_max_length(self._h))
 
     def records(self):
         n = self.num_reads

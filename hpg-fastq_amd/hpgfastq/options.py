@@ -6,7 +6,7 @@ src/filter_fastq.c:195-206 and src/edit_fastq.c:148-171.  The C++ CLI
 (hpg-fastq_amd/host) implements the same rules; these Python twins let the
 tests exercise them without a GPU.
 """
-from ._abi import NO_VALUE, MIN_VALUE, MAX_VALUE, params_default
+from ._abi import NO_VALUE, MIN_VALUE, MAX_VALUE, MAX_EDIT_LENGTH, params_default
 
 
 class RangeError(ValueError):
@@ -117,6 +117,8 @@ def edit_params(lmax=256, stats=False, **o):
     fon = filter_on({k: v for k, v in o.items()
                      if k not in ("left_length", "left_quality_range",
                                   "right_length", "right_quality_range")})
+    if max(f["left_length"], f["right_length"]) > MAX_EDIT_LENGTH:   # trims: two 16-bit fields
+        raise RangeError(f"--left-length and --right-length must be at most {MAX_EDIT_LENGTH}")
     e = dict(edit_left_length=f["left_length"], edit_min_left_quality=f["min_left_quality"],
              edit_max_left_quality=f["max_left_quality"],
              edit_right_length=f["right_length"], edit_min_right_quality=f["min_right_quality"],

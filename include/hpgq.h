@@ -46,8 +46,14 @@ extern "C" {
 #define HPGQ_PHRED33 33
 #define HPGQ_PHRED64 64
 
-/* longest read the per-position counters can hold (dense arrays) */
+/* largest lmax: the dense per-position counters a ctx keeps on chip.
+ * Reads of ANY length are merged: positions >= lmax of a longer read go to the
+ * ctx's long-read tail (hpgq_read_counters_ext), like the reference's khash
+ * maps, which have no length cap (src/stats_fastq.c:289-382). */
 #define HPGQ_LMAX_LIMIT 1024
+/* longest edit window (edit_left_length / edit_right_length): trims are
+ * returned as two 16-bit fields (trim_out, hpgq_run_device) */
+#define HPGQ_MAX_EDIT_LENGTH 65535
 /* Device sequence / quality buffers must stay readable for this many bytes
  * past their last read (seq + data_indices[num_reads]): the engine fetches
  * unaligned 8-byte windows.  The bytes are never used. */
@@ -58,7 +64,8 @@ extern "C" {
 #define HPGQ_E_INVALID         (-1)   /* bad argument / parameter            */
 #define HPGQ_E_HIP             (-2)   /* HIP runtime error                    */
 #define HPGQ_E_NOMEM           (-3)   /* device or host allocation failed     */
-#define HPGQ_E_READ_TOO_LONG   (-4)   /* a merged read longer than lmax      */
+#define HPGQ_E_READ_TOO_LONG   (-4)   /* not returned since round 6: reads of any
+                                         length merge (kept for the ABI)        */
 #define HPGQ_E_NO_DEVICE       (-5)   /* no HIP device                        */
 #define HPGQ_E_RCCL            (-6)   /* RCCL communicator / collective error */
 #define HPGQ_E_STATE           (-7)   /* call not valid in this ctx state     */
@@ -98,7 +105,8 @@ typedef struct hpgq_batch {
  */
 typedef struct hpgq_params {
   int32_t phred;              /* 33 or 64                                    */
-  int32_t lmax;               /* per-position array length, 1..HPGQ_LMAX_LIMIT */
+  int32_t lmax;               /* dense per-position length, 1..HPGQ_LMAX_LIMIT
+                                 (longer reads: the long-read tail)          */
 
   int32_t stats_on;           /* accumulate stats counters                   */
   int32_t filter_on;          /* apply the filter (else every read passes)   */
@@ -113,7 +121,8 @@ typedef struct hpgq_params {
   int32_t right_length, min_right_quality, max_right_quality;
   int32_t max_N;
 
-  /* fastq_edit_options_new(left_len, minL, maxL, right_len, minR, maxR, 0,0,0) */
+  /* fastq_edit_options_new(left_len, minL, maxL, right_len, minR, maxR, 0,0,0);
+   * the lengths are at most HPGQ_MAX_EDIT_LENGTH (hpgq_open: HPGQ_E_INVALID) */
   int32_t edit_left_length, edit_min_left_quality, edit_max_left_quality;
   int32_t edit_right_length, edit_min_right_quality, edit_max_right_quality;
 } hpgq_params_t;
@@ -140,6 +149,15 @@ void hpgq_params_init(hpgq_params_t *p);
  * hpgq_counters_summary().  A paired ctx holds two sets back to back
  * (mate 1, mate 2).  Everything is an exact integer sum, so shards merge by
  * plain addition.
+ *
+ * Reads longer than lmax.  The reference merges every position of every read
+ * (src/stats_fastq.c:338-382, khash keyed by j < read_length).  A merged read
+ * of length L > lmax adds its positions < lmax, its mean-quality and GC bins
+ * and every scalar to the set above (hpgq_read_counters) and counts in
+ * HPGQ_S_LONG_READS; its positions >= lmax and its length go to the ctx's
+ * long-read tail.  hpgq_read_counters_ext returns both as ONE set in the
+ * layout above for lmax_ext = max(lmax, longest merged read) -- the set an
+ * lmax of lmax_ext would have held (HPGQ_S_LONG_READS 0).
  */
 #define HPGQ_S_NUM_INPUT      0  /* reads seen                                 */
 #define HPGQ_S_NUM_PASSED     1  /* reads that passed (== input if no filter)  */
@@ -147,7 +165,9 @@ void hpgq_params_init(hpgq_params_t *p);
 #define HPGQ_S_NUM_EDITED     3  /* reads whose trim removed >= 1 base         */
 #define HPGQ_S_NUM_STATS      4  /* reads merged into stats (counters->num_reads) */
 #define HPGQ_S_ACC_MEANQ_FX16 5  /* sum of floor(65536*sumQraw/len) (acc_quality) */
-#define HPGQ_S_LONG_READS     6  /* merged reads longer than lmax (error)      */
+#define HPGQ_S_LONG_READS     6  /* merged reads longer than lmax: their positions
+                                    >= lmax and length are in the long-read tail
+                                    (0 in an extended set)                    */
 #define HPGQ_S_RESERVED       7
 #define HPGQ_NUM_SCALARS      8
 
@@ -240,11 +260,31 @@ int  hpgq_run_host(hpgq_ctx_t *ctx, const hpgq_batch_t *b, const hpgq_batch_t *b
 int  hpgq_host_batch(hpgq_ctx_t *ctx, int64_t num_reads, size_t nbytes, size_t nbytes2,
                      hpgq_batch_t *b, hpgq_batch_t *b2);
 
-/* Wait for all work on the ctx stream.  HPGQ_E_READ_TOO_LONG when stats are on
- * and a read that passed the filter is longer than lmax (the per-position
- * counters cannot hold it; it is counted in HPGQ_S_LONG_READS).  Without
- * stats, reads of any length are filtered and trimmed. */
+/* Wait for all work on the ctx stream (and deliver hpgq_run_host outputs).
+ * Reads of any length are filtered, trimmed and merged.  The long-read tail
+ * grows on the host: hpgq_run_host sizes it from the batch's own offsets before
+ * the launch; hpgq_run_device cannot see them, so a device batch holding a
+ * merged read longer than lmax + the tail reserved so far has that read's
+ * excess positions merged HERE, by a second pass over the batch -- such a
+ * device batch must stay valid until the next hpgq_sync / hpgq_read_counters /
+ * hpgq_read_counters_ext / hpgq_reset (hpgq_reserve_length avoids the second
+ * pass).  Never HPGQ_E_READ_TOO_LONG. */
 int  hpgq_sync(hpgq_ctx_t *ctx);
+
+/* Reserve the long-read tail for merged reads up to max_len bases (no-op when
+ * max_len <= lmax or already reserved; waits for the ctx stream when it
+ * grows the tail).  The CLI calls it with each parse unit's longest record
+ * (hpgq_parser_max_length). */
+int  hpgq_reserve_length(hpgq_ctx_t *ctx, int64_t max_len);
+
+/* The counters of every merged read at full length: nm sets in the layout of
+ * hpgq_counters_len(*lmax_ext), lmax_ext = max(lmax, longest merged read)
+ * (HPGQ_S_LONG_READS 0; every other entry as an lmax of lmax_ext would give).
+ * out == NULL: only *lmax_ext (size query).  Synchronises like
+ * hpgq_read_counters.  After hpgq_allreduce the sum over the ranks, and then it
+ * is COLLECTIVE: every rank of the communicator calls it (the ranks agree on
+ * lmax_ext and sum their tails with two RCCL all-reduces). */
+int  hpgq_read_counters_ext(hpgq_ctx_t *ctx, uint64_t *out, size_t n, int32_t *lmax_ext);
 
 /* Zero the ctx counters (async on the ctx stream). */
 int  hpgq_reset(hpgq_ctx_t *ctx);
@@ -416,9 +456,13 @@ int  hpgq_cgr_write_images(const char *report_dir, const char *fq_path, int k,
  * Build-defined (the per-read k-mer code is in the absent bioinfo-libs;
  * DESIGN.md §2.5): 5-mers of exact uppercase A/C/G/T, id = sum code_i *
  * 4^(4-i) with A=0 C=1 G=2 T=3, counted at every start position
- * p <= len-5 (p < lmax-4) of every counted read.  by_pos is
- * [HPGQ_NUM_KMERS][lmax-4] u64 (counter_by_pos); a k-mer's counter is its row
- * sum.
+ * p <= len-5 of every counted read.  by_pos is [HPGQ_NUM_KMERS][npos] u64
+ * (counter_by_pos); a k-mer's counter is its row sum.  hpgq_kmers_read gives
+ * the dense starts p < npos = lmax-4; starts >= npos of longer reads (the
+ * reference's counter_by_pos grows with the read, src/stats_fastq.c:394-407)
+ * are in the tail, and hpgq_kmers_read_ext returns all of them as
+ * [HPGQ_NUM_KMERS][npos_ext], npos_ext = max(lmax, longest counted read) - 4.
+ * The tail's reservation and second pass work as the engine's (hpgq_sync).
  */
 typedef struct hpgq_kmers hpgq_kmers_t;
 
@@ -437,6 +481,10 @@ size_t hpgq_kmers_size(const hpgq_kmers_t *km);
 int  hpgq_kmers_read(hpgq_kmers_t *km, uint64_t *by_pos, size_t n);
 /* device pointer of by_pos (for an external all-reduce) */
 uint64_t *hpgq_kmers_device(hpgq_kmers_t *km);
+/* tail for counted reads up to max_len bases (cf. hpgq_reserve_length) */
+int  hpgq_kmers_reserve_length(hpgq_kmers_t *km, int64_t max_len);
+/* every start: [HPGQ_NUM_KMERS][*npos_ext] (by_pos == NULL: size query) */
+int  hpgq_kmers_read_ext(hpgq_kmers_t *km, uint64_t *by_pos, size_t n, int32_t *npos_ext);
 
 /* ---------------------------------------------------------------------- */
 /* FASTQ text -> device batch (the parsing half of the producer's          */
@@ -469,6 +517,9 @@ int  hpgq_parse_device(hpgq_parser_t *ps, const char *text_dev, int64_t n, hpgq_
 int  hpgq_parse_records(hpgq_parser_t *ps, uint32_t *rec_start, uint32_t *seq_start,
                         uint32_t *plus_start, uint32_t *qual_start);
 void *hpgq_parser_stream(hpgq_parser_t *ps);
+/* the longest record of the last parse (0 when empty): the engine's and the
+ * k-mer counter's hpgq_*reserve_length before they run the batch */
+int64_t hpgq_parser_max_length(hpgq_parser_t *ps);
 
 /* ---------------------------------------------------------------------- */
 /* synthetic input (bench / tests): counter-based, identical on host & GPU */

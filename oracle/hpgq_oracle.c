@@ -187,23 +187,30 @@ static int o_filter(const hpgq_params_t *p, const unsigned char *s,
  *   acc_quality (float, :297)    -> exact fixed point sum, HPGQ_S_ACC_MEANQ_FX16 =
  *                                 sum of floor(65536*S/n), two's complement
  * len 0 reads get no quality/GC bin (quirk Q8: the reference divides by zero).
+ * The reference has no length cap (khash keyed by j < read_length).  This
+ * dense set holds lengths <= lmax and positions < lmax: a read longer than
+ * lmax counts in HPGQ_S_LONG_READS and merges everything but its length and
+ * its positions >= lmax (what the engine keeps in its long-read tail; an lmax
+ * of at least the longest read gives the full set, hpgq_read_counters_ext).
  */
 static void o_merge(uint64_t *c, int lmax, const unsigned char *s,
                     const unsigned char *q, int32_t n) {
   c[HPGQ_S_NUM_STATS]++;
-  if (n > lmax) { c[HPGQ_S_LONG_READS]++; return; }
-  c[hpgq_off_hist_len(lmax) + n]++;
+  if (n > lmax) c[HPGQ_S_LONG_READS]++;
+  else c[hpgq_off_hist_len(lmax) + n]++;
   int64_t sraw = 0;
   uint64_t gc = 0;
   uint64_t *pq = c + hpgq_off_pos_qsum(lmax);
   for (int32_t j = 0; j < n; j++) {
     sraw += o_q(q[j]);
+    if (s[j] == 'C' || s[j] == 'G') gc++;
+    if (j >= lmax) continue;
     pq[j] += (uint64_t)(int64_t)o_q(q[j]);   /* u64 wrap = the int sum's two's complement */
     int b = -1;
     switch (s[j]) {
       case 'A': b = HPGQ_BASE_A; break;
-      case 'C': b = HPGQ_BASE_C; gc++; break;
-      case 'G': b = HPGQ_BASE_G; gc++; break;
+      case 'C': b = HPGQ_BASE_C; break;
+      case 'G': b = HPGQ_BASE_G; break;
       case 'T': b = HPGQ_BASE_T; break;
       case 'N': b = HPGQ_BASE_N; break;
       default: break;
@@ -421,7 +428,8 @@ static inline int o_kcode(unsigned char c) {
 }
 
 /* by_pos[HPGQ_NUM_KMERS][lmax-4] += counts of b's reads with mask[i] == 1
- * (all reads when mask is NULL) */
+ * (all reads when mask is NULL); starts p >= lmax-4 are left out (an lmax of
+ * at least the longest read gives them all, hpgq_kmers_read_ext) */
 int oracle_kmers(const hpgq_batch_t *b, const uint8_t *mask, int lmax, uint64_t *by_pos) {
   const int npos = lmax > HPGQ_KMER_K - 1 ? lmax - (HPGQ_KMER_K - 1) : 0;
   if (!b || b->num_reads < 0 || lmax < 1) return HPGQ_E_INVALID;

@@ -110,21 +110,25 @@ def passes(p, s, q):
 
 
 def merge(c, lay, lmax, s, q):
-    """Consumer merge of one read, src/stats_fastq.c:283-382."""
+    """Consumer merge of one read, src/stats_fastq.c:283-382 (no length cap
+    there; this dense set keeps lengths <= lmax and positions < lmax, and a
+    longer read counts in S_LONG_READS and merges everything else)."""
     n = len(s)
     c[S_NUM_STATS] += 1
     if n > lmax:
         c[S_LONG_READS] += 1
-        return
-    c[lay["hist_len"] + n] += 1
+    else:
+        c[lay["hist_len"] + n] += 1
     gc = 0
     for j in range(n):
-        c[lay["pos_qsum"] + j] += sq(q[j])
         ch = chr(s[j])
-        if ch in BASES:
-            c[lay["pos_" + ch] + j] += 1
         if ch in "GC":
             gc += 1
+        if j >= lmax:
+            continue
+        c[lay["pos_qsum"] + j] += sq(q[j])
+        if ch in BASES:
+            c[lay["pos_" + ch] + j] += 1
     if n > 0:
         sraw = sum(sq(x) for x in q)
         c[lay["hist_meanq"] + (c_round_div(sraw, n) & 255)] += 1

@@ -25,6 +25,18 @@ import oracle_lib as O  # noqa: E402  (input generator only: O.synth)
 
 R = 20000   # reads per rank
 CB = 5000   # reads per chaos-game fill call
+LONG = {0: [300, 3000], 1: [151, 9000, 700]}   # the long-read ctx's long reads per rank
+
+
+def long_reads(rank):
+    """Rank r's shard for the long-read ctx: 2,000 synthetic 150 bp reads with
+    LONG[r] appended (each rank's longest read differs: the ranks must agree on
+    lmax_ext in hpgq_read_counters_ext)."""
+    base = O.synth(2000, seed=5, L=150, first=rank * 2000)
+    rng = np.random.default_rng(100 + rank)
+    extra = [(bytes(rng.choice(np.frombuffer(b"ACGTN", np.uint8), L).astype(np.uint8)),
+              bytes((33 + rng.integers(2, 42, L)).astype(np.uint8))) for L in LONG[rank]]
+    return O.Reads.from_pairs(base.pairs() + extra)
 
 
 def params():
@@ -37,7 +49,7 @@ def params():
 def uids(rank, outdir):
     path = os.path.join(outdir, "uids")
     if rank == 0:
-        ids = b"".join(H.engine.comm_unique_id() for _ in range(3))
+        ids = b"".join(H.engine.comm_unique_id() for _ in range(4))
         with open(path + ".tmp", "wb") as f:
             f.write(ids)
         os.rename(path + ".tmp", path)
@@ -47,7 +59,7 @@ def uids(rank, outdir):
             raise SystemExit("rank %d: no unique ids from rank 0" % rank)
         time.sleep(0.05)
     ids = open(path, "rb").read()
-    return [ids[i * 128:(i + 1) * 128] for i in range(3)]
+    return [ids[i * 128:(i + 1) * 128] for i in range(4)]
 
 
 def main():
@@ -74,6 +86,17 @@ def main():
             e.allreduce()
             e.allreduce()
             out[name + "_sum"] = e.counters()
+    # reads longer than lmax on both ranks: the full-length counters after the
+    # all-reduce (hpgq_read_counters_ext, collective: both ranks call it)
+    lr = long_reads(rank)
+    with H.Engine(H.stats_params(lmax=150)) as e:
+        e.comm_init(world, rank, ids[3])
+        e.process(lr.seq, lr.qual, lr.idx)
+        out["lr_own_ext"], L = e.counters_ext()
+        e.allreduce()
+        out["lr_sum"] = e.counters()
+        out["lr_sum_ext"], Lg = e.counters_ext()
+        out["lr_L"] = np.array([L, Lg])
     cg = H.ChaosGame(7, 33)
     cg.comm_init(world, rank, ids[2])
     out["cgr_ranks"] = cg.comm_count()

@@ -34,7 +34,9 @@ int main(int argc, char **argv) {
   fclose(f);
   cli_result_t res;
   memset(&res, 0, sizeof(res));
-  const int rc = cli_report(o, &p, c, &res);
+  res.counters = c;   /* (the layout of lmax: what the CLI's full-length merge hands over) */
+  res.lmax = lmax;
+  const int rc = cli_report(o, &p, &res);
   free(c);
   cli_free(o);
   return rc ? 1 : 0;

@@ -94,6 +94,14 @@ def test_invalid_arguments_rejected():
     p = H.params_default(lmax=H.LMAX_LIMIT + 1)
     h = C.c_void_p()
     assert H.lib.hpgq_open(C.byref(h), 0, C.byref(p)) in (-1, -5)
+    # an edit window past 16 bits (trims are ts | te << 16): invalid before any device call
+    for f in ("edit_left_length", "edit_right_length"):
+        p = H.params_default(lmax=150, edit_on=1, **{f: H.MAX_EDIT_LENGTH + 1})
+        assert H.lib.hpgq_open(C.byref(h), 0, C.byref(p)) == -1
+    p = H.params_default(lmax=150, edit_on=1, edit_left_length=H.MAX_EDIT_LENGTH)
+    assert H.lib.hpgq_open(C.byref(h), 0, C.byref(p)) in (0, -5)
+    if h.value:
+        H.lib.hpgq_close(h)
 
 
 def _no_gpu():

@@ -247,11 +247,24 @@ def test_cli_kat_stats(tmp_path):
     check_partial(np.fromfile(ctr, np.uint64), kat["stats"], kat["lmax"], H.layout(kat["lmax"]))
 
 
-def test_cli_read_too_long(tmp_path):
-    reads = O.synth(100, seed=3, L=150)
+def test_cli_reads_longer_than_lmax(tmp_path):
+    """--lmax only sizes the on-chip counters: 150 bp reads at --lmax 100 give
+    the full-length counters (the oracle at 150) and the report over them
+    (round 5 ended such a run with "read longer than lmax")."""
+    reads = O.synth(3000, seed=3, L=150)
     fq = _write(tmp_path, reads)
-    r = run_cli(["stats", "-f", fq, "-o", tmp_path, "--lmax", 100, "--quiet"], check=False)
-    assert r.returncode != 0 and "longer than lmax" in r.stderr
+    ctr = tmp_path / "ctr.bin"
+    run_cli(["stats", "-f", fq, "-o", tmp_path, "--lmax", 100, "--counters-out", ctr, "--quiet"])
+    _, _, want = O.run(H.stats_params(lmax=150), reads)
+    np.testing.assert_array_equal(np.fromfile(ctr, np.uint64), want)
+
+
+def test_cli_edit_length_limit(tmp_path):
+    reads = O.synth(10, seed=3, L=150)
+    fq = _write(tmp_path, reads)
+    r = run_cli(["edit", "-f", fq, "-o", tmp_path, "--left-length", 65536, "--left-quality-range", "20,",
+                 "--quiet"], check=False)
+    assert r.returncode != 0 and "at most 65535" in r.stdout
 
 
 @pytest.mark.parametrize("filt", [False, True])

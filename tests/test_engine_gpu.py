@@ -185,13 +185,24 @@ def test_all_fail_and_empty_batch():
         assert e.counters().sum() == 0
 
 
-def test_read_too_long_reports_error():
+def test_reads_longer_than_lmax_merge():
+    """Reads longer than lmax are merged (round 6; the reference has no cap,
+    src/stats_fastq.c:338-382): the dense set equals the oracle at lmax (the
+    long reads' positions < lmax, bins and scalars, HPGQ_S_LONG_READS), the
+    full-length set the oracle at the longest read (tests/test_longreads_gpu.py
+    covers every path and length)."""
     reads = O.synth(100, seed=1, L=200)
     p = H.stats_params(lmax=150)
     with H.Engine(p) as e:
-        with pytest.raises(H.HpgqError) as ei:
-            e.process(reads.seq, reads.qual, reads.idx)
-        assert ei.value.code == -4
+        e.process(reads.seq, reads.qual, reads.idx)
+        dense = e.counters()
+        ext, L = e.counters_ext()
+    _, _, c_o = O.run(p, reads)
+    np.testing.assert_array_equal(dense, c_o)
+    assert int(dense[H.S_LONG_READS]) > 0 and L == 200
+    p.lmax = 200
+    _, _, c_x = O.run(p, reads)
+    np.testing.assert_array_equal(ext, c_x)
 
 
 def test_accumulates_across_batches_and_offsets(kernel_choice):
@@ -540,16 +551,21 @@ def test_mixed_lengths_paired(geo_choice):
 
 
 def test_long_read_over_65535_bases():
-    """A read longer than 16 bits: stats on -> HPGQ_E_READ_TOO_LONG (the old
-    kernel packed the length into 16 bits and misread it); filter only -> the
+    """A read longer than 16 bits (the round-1 kernel packed the length into 16
+    bits and misread it): stats merge it at full length; filter only -> the
     chunk loop filters it like the oracle."""
     big = O.synth(1, seed=3, L=65636, trunc_pct=0)
     small = O.synth(300, seed=4, L=150)
     reads = O.Reads.from_pairs([(bytes(big.seq), bytes(big.qual))] + small.pairs())
-    with H.Engine(H.stats_params(lmax=1024)) as e:
-        with pytest.raises(H.HpgqError) as ei:
-            e.process(reads.seq, reads.qual, reads.idx)
-        assert ei.value.code == -4
+    p = H.stats_params(lmax=1024)
+    with H.Engine(p) as e:
+        e.process(reads.seq, reads.qual, reads.idx)
+        dense = e.counters()
+        ext, L = e.counters_ext()
+    np.testing.assert_array_equal(dense, O.run(p, reads)[2])
+    assert L == 65636
+    p.lmax = L
+    np.testing.assert_array_equal(ext, O.run(p, reads)[2])
     p = H.filter_params(lmax=150, read_quality_range="20,", max_N=100)
     assert_same(p, reads)
 

@@ -105,9 +105,8 @@ def test_random_option_combination(case, monkeypatch):
     rng = np.random.default_rng(1000 + case)
     p, cmd, o = _params(rng)
     n = int(rng.integers(1, 6000))
-    # a merged read longer than lmax is an error (HPGQ_E_READ_TOO_LONG): with
-    # stats on, reads stay within lmax; filter / edit take any length
-    cap = p.lmax if p.stats_on else p.lmax + 120
+    # reads of any length: up to 120 bases past lmax (the stats' long-read tail)
+    cap = p.lmax + 120
     phred = p.phred
     r1 = _reads(rng, n, p.lmax, phred, cap)
     r2 = _reads(rng, n, p.lmax, phred, cap) if p.paired else None
@@ -132,6 +131,7 @@ def test_random_option_combination(case, monkeypatch):
             if p.paired:
                 trim[n + lo:n + hi] = t[hi - lo:]
         c_g = e.counters()
+        ext, lmax_ext = e.counters_ext()
         chain = e.kernel_chain
     info = f"case {case} ({route}): {cmd} paired={p.paired} lmax={p.lmax} n={n} cut={cut} {o} chain={chain}"
     np.testing.assert_array_equal(mask, m_o, err_msg=info)
@@ -141,3 +141,9 @@ def test_random_option_combination(case, monkeypatch):
         bad = np.nonzero(c_g != c_o)[0]
         raise AssertionError(f"{info}: counters differ at {bad[:10]} gpu={c_g[bad[:10]]} "
                              f"oracle={c_o[bad[:10]]}")
+    # the full-length set: the oracle at the longest merged window
+    px = H.Params.from_buffer_copy(p)
+    px.lmax = lmax_ext
+    _, _, c_x = O.run(px, r1, r2)
+    assert int(c_x[H.S_LONG_READS]) == 0, info
+    np.testing.assert_array_equal(ext, c_x, err_msg=info)

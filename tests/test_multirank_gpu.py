@@ -74,6 +74,25 @@ def test_rccl_two_ranks_counters_and_tables(tmp_path):
             # the all-reduced sum (twice: out of place, no double count)
             np.testing.assert_array_equal(res[r][name + "_sum"], want)
         assert int(want[H.S_NUM_INPUT]) == WORLD * R
+    # the long-read ctx: each rank's own full-length set, and the collective
+    # full-length sum at the longest read of ANY rank
+    p = H.stats_params(lmax=150)
+    Lg = max(max(v) for v in rccl_rank.LONG.values())
+    want_dense = np.zeros(H.counters_len(150), np.uint64)
+    want_ext = np.zeros(H.counters_len(Lg), np.uint64)
+    for r in range(WORLD):
+        lr = rccl_rank.long_reads(r)
+        want_dense += O.run(p, lr)[2]
+        Lr = max(rccl_rank.LONG[r])
+        assert list(res[r]["lr_L"]) == [Lr, Lg]
+        px = H.Params.from_buffer_copy(p)
+        px.lmax = Lr
+        np.testing.assert_array_equal(res[r]["lr_own_ext"], O.run(px, lr)[2])
+        px.lmax = Lg
+        want_ext += O.run(px, lr)[2]
+    for r in range(WORLD):
+        np.testing.assert_array_equal(res[r]["lr_sum"], want_dense)
+        np.testing.assert_array_equal(res[r]["lr_sum_ext"], want_ext)
     dim2 = 128 * 128
     tables = (np.zeros(dim2, np.uint32), np.zeros(dim2, np.uint32), np.zeros(1, np.uint32))
     for r in range(WORLD):

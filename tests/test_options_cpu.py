@@ -68,6 +68,9 @@ def test_edit_moves_left_right_into_edit_fields():
     assert p.left_length == 0 and p.right_length == 0   # filter's windows forced off
     with pytest.raises(RangeError):
         H.edit_params(lmax=150, read_length_range="10,")   # nothing to edit
+    with pytest.raises(RangeError):   # trims are two 16-bit fields
+        H.edit_params(lmax=150, left_length=65536, left_quality_range="20,")
+    assert H.edit_params(lmax=150, right_length=65535, right_quality_range="20,").edit_right_length == 65535
 
 
 def test_quality_encoding():
