@@ -129,6 +129,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end CLI leg (C2)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-reads", type=int, default=None,
+                    help="reads of the CPU baseline's sample (default 2 M; 400 k for CGR)")
     ap.add_argument("--lmax", type=int, default=None, help="override the config's lmax")
     ap.add_argument("--route", default=None,
                     help="A/B only: engine kernel route (hpgq_debug_set_route: auto, single, tri, hex, "
@@ -217,6 +219,16 @@ def native_oracle():
     return lib, build
 
 
+def cgroup_cpu_quota():
+    """Cores' worth of CPU time this job may use (cgroup v2 cpu.max), or None
+    when unlimited / unknown: the GPU box may cap a job below its visible cores."""
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else round(int(q) / int(period), 2)
+    except (OSError, ValueError):
+        return None
+
+
 def omp_threads(default):
     """This job's CPU share from OMP_NUM_THREADS (its first field: nested
     OpenMP lists such as '16,1' are valid), else `default`."""
@@ -242,7 +254,7 @@ def cpu_baseline(args, params):
     threads = max(1, min(omp_threads(ncores), ncores))
     L = args.read_length
     cgr = args.config in ("c5", "c5_valid")
-    n = 400_000 if cgr else 2_000_000
+    n = args.cpu_reads or (400_000 if cgr else 2_000_000)
     mates = 2 if params.paired else 1
     bufs = []
     for m in range(mates):
@@ -308,6 +320,15 @@ def cpu_baseline(args, params):
     assert run() == 0
     el1 = time.perf_counter() - t1
     out["value_1thread"] = round(n / el1 / 1e6, 3)
+    # the whole host, SURVEY §8d's "threads = nproc": every visible core for a
+    # short run (context: the line's value above is this GPU's CPU share; the
+    # job's cgroup quota, when the box sets one, is stated beside it)
+    if args.config != "c2_kmers":
+        nt[0] = ncores
+        da, ea = timed(budget=max(1.0, args.cpu_seconds / 3))
+        out["value_allcores"] = round(da / ea / 1e6, 3)
+        out["cores_allcores"] = ncores
+        out["cpu_quota_cores"] = cgroup_cpu_quota()
     nt[0] = threads
     c1 = ""
     if args.config == "c2":
@@ -322,7 +343,8 @@ def cpu_baseline(args, params):
     out["sample"] = (f"{n} synthetic {L} bp {'pairs' if mates == 2 else 'reads'} (seed "
                      f"{args.seed}, same generator and options), {done // n} passes in "
                      f"{el:.1f} s; {what}, {threads} OpenMP threads (this GPU's CPU share; "
-                     f"{ncores} visible); value_1thread: one pass on 1 thread ({el1:.1f} s){c1}")
+                     f"{ncores} visible); value_1thread: one pass on 1 thread ({el1:.1f} s); "
+                     f"value_allcores: the same on all {ncores} visible cores{c1}")
     return out
 
 
@@ -750,6 +772,8 @@ def dry_run_rank(args, world, rank):
                 sys.exit(3)
         out = result_line(args, cfg, world, None, 0, None, None, "u8", extra)
         out["dry_run"] = True
+        if world == 1 and not args.no_cpu_baseline:   # the CPU leg needs no device
+            out["cpu_baseline"] = cpu_baseline(args, params_for(args.config, args.read_length))
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -783,6 +807,12 @@ def main():
         dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=900))
     torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)
+    if world > 1:   # ranks on one GPU fail BEFORE RCCL init, warmup and timing
+        pci, uuid = device_id(local_dev)
+        err = check_distinct_devices(rank_table(dist, world, {"rank": rank, "pci": pci, "uuid": uuid}),
+                                     args.share_device)
+        if err:
+            rank_fail(3, err if rank == 0 else None)
 
     L = args.read_length
     cgr = args.config in ("c5", "c5_valid")
@@ -904,9 +934,6 @@ def main():
                                          "el_s": round(el, 6),
                                          "avg_launch_us": round(timed_ms / (args.steps * nb) * 1e3, 1)})
         el = max(g["el_s"] for g in ranks)
-        err = check_distinct_devices(ranks, args.share_device)
-        if err:
-            rank_fail(3, err if rank == 0 else None)
 
     # sanity: every read accounted for (after the all-reduce: every rank's reads)
     if kmers:

@@ -181,7 +181,7 @@ int mapout_error(mapout_t *m) {
 /* ---- SIGBUS guard ---------------------------------------------------------- */
 
 static __thread sigjmp_buf *g_jb;   /* the guarded call on this thread, if any */
-static pthread_once_t g_once = PTHREAD_ONCE_INIT;
+static pthread_mutex_t g_mu = PTHREAD_MUTEX_INITIALIZER;
 static struct sigaction g_prev;
 
 static void on_sigbus(int sig, siginfo_t *si, void *uc) {
@@ -199,17 +199,28 @@ static void on_sigbus(int sig, siginfo_t *si, void *uc) {
   raise(SIGBUS);
 }
 
-static void install(void) {
-  struct sigaction sa;
-  memset(&sa, 0, sizeof(sa));
-  sa.sa_sigaction = on_sigbus;
-  sa.sa_flags = SA_SIGINFO;
-  sigemptyset(&sa.sa_mask);
-  sigaction(SIGBUS, &sa, &g_prev);
+static int is_ours(const struct sigaction *a) { return (a->sa_flags & SA_SIGINFO) && a->sa_sigaction == on_sigbus; }
+
+/* on_sigbus is the SIGBUS handler at every guarded copy: installed at the
+ * first one, and again whenever a runtime or library installed its own since
+ *  -- that one then becomes the handler unguarded faults chain to */
+static void ensure_installed(void) {
+  struct sigaction cur;
+  if (sigaction(SIGBUS, NULL, &cur) == 0 && is_ours(&cur)) return;
+  pthread_mutex_lock(&g_mu);
+  if (sigaction(SIGBUS, NULL, &cur) != 0 || !is_ours(&cur)) {
+    struct sigaction sa;
+    memset(&sa, 0, sizeof(sa));
+    sa.sa_sigaction = on_sigbus;
+    sa.sa_flags = SA_SIGINFO;
+    sigemptyset(&sa.sa_mask);
+    sigaction(SIGBUS, &sa, &g_prev);
+  }
+  pthread_mutex_unlock(&g_mu);
 }
 
 int mapout_guard(void (*fn)(void *), void *arg) {
-  pthread_once(&g_once, install);
+  ensure_installed();
   sigjmp_buf jb;
   if (sigsetjmp(jb, 1)) {   /* (the mask is restored: SIGBUS unblocked again) */
     g_jb = NULL;

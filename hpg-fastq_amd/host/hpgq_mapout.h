@@ -11,16 +11,19 @@
  *     allocate twice the input before a record is written;
  *   - the first window of each output is reserved (populated) before the
  *     mapping is used, else the stream writer runs;
- *   - prefault threads populate the outputs (MADV_POPULATE_WRITE, or
- *     fallocate where that is missing, or nothing where neither is
- *     supported) a window ahead of the records placed
- *     so far: a file system that cannot back a page makes that call fail
- *     (HPGQ_E_IO) instead of a store raising SIGBUS, and the copiers store
- *     into pages that are already there (a first-touch fault per 4 KB page is
- *     what bounded the round-4 writer);
+ *   - by default nothing past that first window is reserved: the copiers
+ *     fault the pages in, and every copy runs under the SIGBUS guard below;
+ *   - optional prefault threads (--prefault-threads N, default none: they
+ *     measured slower than none on the GPU boxes) populate the
+ *     outputs (MADV_POPULATE_WRITE, or fallocate where that is missing, or
+ *     nothing where neither is supported) a window ahead of the records
+ *     placed so far, so a file system that cannot back a page makes that call
+ *     fail (HPGQ_E_IO) instead of a store raising SIGBUS;
  *   - every copy runs under a SIGBUS guard (mapout_guard): a store the file
- *     system still cannot back (another writer filled it after the check)
- *     ends that copy with HPGQ_E_IO instead of killing the process.
+ *     system cannot back (no room; another writer filled it after the check)
+ *     ends that copy with HPGQ_E_IO instead of killing the process.  The
+ *     guard's handler is re-installed at any copy that finds another SIGBUS
+ *     handler in its place.
  */
 #ifndef HPGQ_MAPOUT_H
 #define HPGQ_MAPOUT_H

@@ -9,6 +9,7 @@
  * (quirk Q11).
  */
 #define _GNU_SOURCE
+#include <errno.h>
 #include <getopt.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -116,6 +117,19 @@ static int exists(const char *path) {
   return path && stat(path, &st) == 0;
 }
 
+/* a whole-string decimal in [lo, hi], else the usage error (atoi
+ * turned garbage into 0 or the default) */
+static int count_arg(const cli_options_t *o, const char *flag, const char *s, int lo, int hi) {
+  char *end = NULL;
+  errno = 0;
+  const long v = strtol(s, &end, 10);
+  if (errno || end == s || *end != '\0' || v < lo || v > hi) {
+    printf("\nError: --%s must be an integer in %d..%d (%s)\n", flag, lo, hi, s);
+    usage(o);
+  }
+  return (int)v;
+}
+
 enum {
   O_THREADS = 1000, O_BATCH, O_QENC, O_KMERS, O_LRANGE, O_QRANGE, O_LLEN, O_LQRANGE, O_RLEN,
   O_RQRANGE, O_MAXN, O_MAXOOQ, O_GPU, O_LMAX, O_CHUNK, O_PRINT, O_COUNTERS, O_QUIET,
@@ -218,9 +232,15 @@ cli_options_t *cli_parse(int command, const char *exec_name, int argc, char **ar
       case O_CGOUT: o->cg_out = strdup(optarg); break;
       case O_QUIET: o->quiet = 1; break;
       case O_STREAMW: o->stream_writer = 1; break;
-      case O_WHOOK: o->writer_hook = atoi(optarg); break;   /* (tests: hpgq_mapout.h MAPOUT_HOOK_*) */
-      case O_COPYT: o->copy_threads = atoi(optarg); break;
-      case O_PFT: o->prefault_threads = atoi(optarg); break;
+      case O_WHOOK:   /* tests only: hpgq_mapout.h MAPOUT_HOOK_* force the writer's failure paths */
+        if (!getenv("HPGQ_WRITER_TEST_HOOKS")) {
+          printf("\nError: --writer-test-hook is a test option (set HPGQ_WRITER_TEST_HOOKS=1)\n");
+          usage(o);
+        }
+        o->writer_hook = count_arg(o, "writer-test-hook", optarg, 0, 7);
+        break;
+      case O_COPYT: o->copy_threads = count_arg(o, "copy-threads", optarg, 0, 64); break;
+      case O_PFT: o->prefault_threads = count_arg(o, "prefault-threads", optarg, 0, 4); break;
       default: usage(o);
     }
   }

@@ -667,7 +667,7 @@ static void stop_copiers(pipe_t *P) {
  * 3, until they are copied) */
 static int place_and_copy(pipe_t *P, slot_t *s, int *handed) {
   copy_part_t *part = s->parts;
-  int n = P->o->num_threads;
+  int n = P->ncopiers;   /* one part per copier thread (--copy-threads, default --num-threads) */
   const int64_t per_min = 16384;   /* records per copier at least */
   if (n > MAX_COPIERS) n = MAX_COPIERS;
   if ((int64_t)n > s->nreads / per_min + 1) n = (int)(s->nreads / per_min + 1);

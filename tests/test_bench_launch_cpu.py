@@ -59,13 +59,28 @@ def test_distinct_device_check():
 
 
 def test_one_gpu_line_shape_unchanged():
-    r = _bench("--gpus", "1", "--launch-dry-run", "--reads", "5000")
+    r = _bench("--gpus", "1", "--launch-dry-run", "--reads", "5000", "--no-cpu-baseline")
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["n_gpus"] == 1
     assert set(line) - {"dry_run"} == LINE_KEYS
     assert "rccl_ranks" not in line["config"]   # only N > 1 lines carry it
     assert "ranks" not in line["config"]
+
+
+def test_one_gpu_line_cpu_baseline_keys():
+    """The one-GPU line's CPU leg (no device needed): the oracle on this GPU's
+    CPU share, on one thread, and on every visible core (VERDICT r5 item 5:
+    SURVEY §8d's threads = nproc), with the C1 and reference-architecture legs."""
+    r = _bench("--gpus", "1", "--launch-dry-run", "--reads", "5000", "--cpu-seconds", "0.3",
+               "--cpu-reads", "20000")
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    cb = line["cpu_baseline"]
+    assert {"value", "cores", "kind", "value_1thread", "value_allcores", "cores_allcores",
+            "cpu_quota_cores", "c1_stats_mreads_s", "refarch", "sample"} <= set(cb)
+    assert cb["cores_allcores"] == len(os.sched_getaffinity(0)) and cb["value_allcores"] > 0
+    assert cb["kind"] == "port" and "visible cores" in cb["sample"]
 
 
 def test_gpus_world_size_mismatch_fails():

@@ -47,9 +47,25 @@ def test_cli_params_match_python_options(cmd, flags, py):
     ["filter", "--print-params", "--kmers", "--max-N", "1"],   # --kmers is a stats flag
     ["stats", "-f", "/nonexistent.fq"],
     ["bogus"],
+    # thread counts are whole integers in range (atoi took garbage as 0)
+    ["filter", "--print-params", "--max-N", "1", "--copy-threads", "abc"],
+    ["filter", "--print-params", "--max-N", "1", "--copy-threads", "65"],
+    ["filter", "--print-params", "--max-N", "1", "--prefault-threads", "5"],
+    ["filter", "--print-params", "--max-N", "1", "--prefault-threads", "2x"],
+    # the writer's failure hooks are a test option (HPGQ_WRITER_TEST_HOOKS)
+    ["filter", "--print-params", "--max-N", "1", "--writer-test-hook", "1"],
+    # edit windows are at most 65535 bases (trims are two 16-bit fields)
+    ["edit", "--print-params", "--left-length", "65536", "--left-quality-range", "20,"],
 ])
 def test_cli_rejects(args):
     assert run_cli(args, check=False).returncode != 0
+
+
+def test_cli_accepts_valid_writer_options():
+    print_params("filter", "--max-N", "1", "--copy-threads", "8", "--prefault-threads", "4")
+    r = run_cli(["filter", "--print-params", "--max-N", "1", "--writer-test-hook", "2"],
+                env={"HPGQ_WRITER_TEST_HOOKS": "1"})
+    assert r.returncode == 0
 
 
 def test_cli_lmax_option():

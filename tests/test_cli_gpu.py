@@ -141,7 +141,8 @@ def test_cli_writer_reservation_failure_uses_stream_writer(tmp_path):
     reads = O.synth(15000, seed=31, L=150)
     fq = _write(tmp_path, reads)
     r = run_cli(["filter", "-f", fq, "-o", tmp_path, "--read-quality-range", "20,", "--read-length-range", "50,",
-                 "--chunk-mb", 1, "--quiet", "--writer-test-hook", 1], env={"HPGQ_TRACE": "1"})
+                 "--chunk-mb", 1, "--quiet", "--writer-test-hook", 1],
+               env={"HPGQ_TRACE": "1", "HPGQ_WRITER_TEST_HOOKS": "1"})
     assert WRITER_LINE["stream"] in r.stderr, r.stderr[-2000:]
     passed, failed = _filter_expected(reads)
     assert (tmp_path / "passed.fq").read_bytes() == passed
@@ -176,7 +177,8 @@ def test_cli_writer_store_failure_is_io_error(tmp_path, hook):
     r = run_cli(["filter", "-f", fq, "-o", tmp_path, "--read-quality-range", "20,", "--read-length-range", "50,",
                  "--chunk-mb", 1, "--quiet", "--writer-test-hook", hook,
                  # (the default prefaults nothing past the first window: hook 2 needs the threads)
-                 *(["--prefault-threads", 2] if hook == 2 else [])], check=False, env={"HPGQ_TRACE": "1"})
+                 *(["--prefault-threads", 2] if hook == 2 else [])], check=False,
+                env={"HPGQ_TRACE": "1", "HPGQ_WRITER_TEST_HOOKS": "1"})
     assert r.returncode == 1, (r.returncode, r.stderr[-2000:])   # (a SIGBUS death would be -7)
     assert WRITER_LINE["mmap"] in r.stderr
     assert "Error: file i/o error (-9)" in r.stderr, r.stderr[-2000:]

@@ -134,6 +134,34 @@ def test_paired_end(geo_choice):
     assert c[H.S_NUM_PASSED] == c[ln + H.S_NUM_PASSED]
 
 
+@pytest.mark.parametrize("left,right,lq,rq", [
+    (1, 1, "22,", "18,36"), (8, 31, "22,35", "18,"), (13, 32, "22,", "18,36"), (16, 32, "20,30", "18,36"),
+    (17, 33, "22,", "18,"), (16, 0, "22,35", None), (0, 32, None, "18,36"), (14, 20, "45,", "0,10")])
+def test_paired_edit_window_sizes(left, right, lq, rq, geo_choice):
+    """the paired-end trims -- the TDMA windows of the first stage
+    (engine_tri_kernel<3, 2, edit, hex>), left lengths 13-16, bounded and empty
+    ranges on both sides (the bounded-range branch), windows past the usual 16 /
+    32 bytes, and each mate batch starting with a read shorter than 32 bytes
+    (its right window would begin before the buffer)."""
+    r1 = O.synth(6000, seed=50 + left + right, L=150, trunc_pct=60, mate=0)
+    r2 = O.synth(6000, seed=50 + left + right, L=150, trunc_pct=60, mate=1)
+    lowhi = bytes([33 + 5] * 7 + [33 + 30] * 6 + [33 + 8] * 7)
+    r1 = O.Reads.from_pairs([(b"ACGTN" * 4, lowhi)] + r1.pairs())
+    r2 = O.Reads.from_pairs([(b"TTGCA" * 3, lowhi[5:])] + r2.pairs())
+    kw = {}
+    if left:
+        kw.update(left_length=left, left_quality_range=lq)
+    if right:
+        kw.update(right_length=right, right_quality_range=rq)
+    p = H.edit_params(lmax=150, stats=True, **kw)
+    p.paired = 1
+    c = assert_same(p, r1, r2)
+    assert c[H.S_NUM_EDITED] > 0
+    if geo_choice == "auto":
+        with H.Engine(p) as e:
+            assert e.kernel_chain.startswith("hpgq::engine_tri_kernel<3, 2, edit, hex>"), e.kernel_chain
+
+
 def test_paired_edit(geo_choice):
     r1 = O.synth(5000, seed=8, L=150, mate=0)
     r2 = O.synth(5000, seed=8, L=150, mate=1)
