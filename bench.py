@@ -974,6 +974,9 @@ def main():
     extra = {"route": args.route} if args.route else {}
     if ranks is not None:
         extra["ranks"] = ranks
+    else:   # which GPU ran it: profiles are checked against this line's clock (tools/profile_report.py)
+        pci, uuid = device_id(local_dev)
+        extra["device"] = {"index": local_dev, "pci": pci, "uuid": uuid}
     if args.share_device:
         extra["shared_device"] = f"{world} ranks on {ndev} device(s): functional run, not a scaling number"
     out = result_line(args, cfg, world, el, total, roofline, rccl_ranks, "f64" if cgr else "u8", extra)

@@ -53,6 +53,38 @@ def counters(sub, kerns):
     return dict(agg), " + ".join(sorted(last))
 
 
+def clock_check(stats_csv, line, kerns):
+    """the traced kernel time must fit the SAME run's bench
+    clock.  The dominant kernel (largest total in the trace's --stats) averaged
+    over the TIMED launches (the last steps x launches-per-step of the kernel
+    trace beside the stats file; the untimed warmup's first launches run at a
+    lower clock) x launches per step must be <= the line's ms_per_step, else
+    the profile is marked box_mismatch (a trace from a slower box than the
+    line, or a line that is not this run's)."""
+    if not (stats_csv and line):
+        return None
+    rows = [r for r in csv.DictReader(open(stats_csv)) if any(k in r["Name"] for k in kerns)]
+    if not rows:
+        return None
+    dom = max(rows, key=lambda r: float(r["TotalDurationNs"]))
+    c = line["config"]
+    per_step = -(-int(c.get("reads_per_gpu", 0)) // max(1, int(c.get("batch_reads", 1))))
+    avg, launches = float(dom["AverageNs"]), "all launches (--stats)"
+    tr = glob.glob(os.path.join(os.path.dirname(stats_csv), "*kernel_trace.csv"))
+    if tr:
+        d = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+                   for r in csv.DictReader(open(tr[0])) if r["Kernel_Name"] == dom["Name"])
+        k = int(line["steps"]) * per_step
+        if len(d) >= k:
+            avg, launches = sum(x for _, x in d[-k:]) / k, f"the last {k} launches (the timed steps)"
+    k_ms = avg * per_step / 1e6
+    ok = k_ms <= float(line["ms_per_step"]) * 1.0005
+    return {"kernel": dom["Name"][:120], "kernel_avg_us": round(avg / 1e3, 2), "averaged_over": launches,
+            "launches_per_step": per_step, "kernel_ms_per_step": round(k_ms, 4),
+            "bench_ms_per_step": line["ms_per_step"], "device": c.get("device"),
+            "status": "consistent" if ok else "box_mismatch"}
+
+
 def bench_line(path):
     if not os.path.exists(path):
         return None
@@ -89,12 +121,19 @@ def main():
         PROF = os.path.join(ROOT, a.prof) if not os.path.isabs(a.prof) else a.prof
     os.makedirs(OUT, exist_ok=True)
     stats = glob.glob(os.path.join(PROF, "trace", "**", "run_kernel_stats.csv"), recursive=True)
+    main_check = clock_check(stats[0] if stats else None, bench_line(os.path.join(PROF, "bench.json")), ENG)
+    if main_check:
+        print("clock check (driver command):", json.dumps(main_check))
+        if main_check["status"] != "consistent":
+            raise SystemExit("profile_report: the kernel trace does not fit its own bench clock (box_mismatch)")
     if stats:
         shutil.copy(stats[0], os.path.join(OUT, f"{a.round}_bench_kernel_stats.csv"))
         for r in csv.DictReader(open(stats[0])):
             if a.kernel in r["Name"]:
                 print("kernel-trace avg ns:", r["AverageNs"], "calls", r["Calls"])
     b = bench_line(os.path.join(PROF, "bench.json"))
+    if b and main_check:
+        b["clock_check"] = main_check
     if b:
         json.dump(b, open(os.path.join(OUT, f"{a.round}_bench.json"), "w"), indent=1)
         print("bench value", b["value"], "avg_launch_us", b["roofline"]["avg_launch_us"])
@@ -129,6 +168,12 @@ def main():
         src = (f"profiles/{a.round}_pmc_engine_{cfg}.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, "
                "separate passes, same session)")
         cb = bench_line(os.path.join(PROF, f"bench_{cfg}.json"))
+        bt = glob.glob(os.path.join(PROF, f"btrace_{cfg}", "**", "run_kernel_stats.csv"), recursive=True)
+        chk = clock_check(bt[0] if bt else None, cb, KERNELS[cfg])
+        if cb and chk:
+            cb["clock_check"] = chk
+            if chk["status"] != "consistent":
+                print(f"{cfg}: BOX MISMATCH", json.dumps(chk))
         if cb:
             cb["roofline"]["traffic"] = rec["hbm_bytes_per_launch"]
             cb["roofline"]["traffic_source"] = src
@@ -137,7 +182,6 @@ def main():
             b["roofline"]["traffic"] = rec["hbm_bytes_per_launch"]
             b["roofline"]["traffic_source"] = src
             json.dump(b, open(os.path.join(OUT, f"{a.round}_bench.json"), "w"), indent=1)
-        bt = glob.glob(os.path.join(PROF, f"btrace_{cfg}", "**", "run_kernel_stats.csv"), recursive=True)
         if bt:
             shutil.copy(bt[0], os.path.join(OUT, f"{a.round}_bench_{cfg}_kernel_stats.csv"))
         for name in (f"{a.round}_pmc_engine_{cfg}.json", f"pmc_engine_{cfg}.json"):
