@@ -200,7 +200,15 @@ def _load():
                           "(the HIP engine has no CPU fallback)")
     lib = C.CDLL(LIB_PATH)
     for name, res, args in _SIGS:
-        fn = getattr(lib, name)
+        try:
+            fn = getattr(lib, name)
+        except AttributeError:
+            # (an older build loaded for an A/B timing run through HPGQ_LIB_PATH
+            # may predate an entry point; the in-tree library must have them all,
+            # tests/test_abi_cpu.py)
+            if os.environ.get("HPGQ_LIB_PATH"):
+                continue
+            raise
         fn.restype = res
         fn.argtypes = args
     return lib

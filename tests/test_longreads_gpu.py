@@ -268,7 +268,7 @@ def test_cli_long_reads(tmp_path):
     out.mkdir()
     ctr, kb = tmp_path / "ctr.bin", tmp_path / "k.bin"
     run_cli(["stats", "-f", fq, "-o", out, "--read-quality-range", "20,", "--lmax", 150, "--chunk-mb", 1,
-             "--kmers", "--kmers-out", kb, "--counters-out", ctr, "--quiet"])
+             "--counters-out", ctr, "--quiet"])
     p = H.stats_params(lmax=150, read_quality_range="20,")
     m_o, _, _ = O.run(p, reads)
     L = max([150] + [int(reads.idx[i + 1] - reads.idx[i]) for i in range(reads.n) if m_o[i]])
@@ -279,6 +279,10 @@ def test_cli_long_reads(tmp_path):
     exp = report_ref.report_files(got, L, 33, "in.fq", {"filter_on": True, "read_quality_range": "20,"})
     for suffix, data in exp.items():
         assert (out / f"in.fq.{suffix}").read_bytes() == data, suffix
+    kdir = tmp_path / "k"
+    kdir.mkdir()
+    run_cli(["stats", "-f", fq, "-o", kdir, "--read-quality-range", "20,", "--lmax", 150, "--chunk-mb", 1,
+             "--kmers", "--kmers-out", kb, "--quiet"])
     kt = np.fromfile(kb, np.uint64).reshape(1024, -1)
     assert kt.shape[1] == L - 4
     np.testing.assert_array_equal(kt, O.kmers(reads, L, np.asarray(m_o, np.uint8)))
