@@ -140,21 +140,15 @@ struct TriAcc {
     }
   }
   // bytes -> LDS (pos_acc [6][lmax]: qsum, A, C, G, T, N/other); nibbles empty
-  template <bool FLAT = false>
   __device__ __forceinline__ void flush(uint32_t *pos_acc, int lmax, int p0) {
     // rare (every <= 255 steps): keep its 40 LDS addresses out of the hot
     // loop's registers (hipcc would hoist them as loop invariants and spill).
     // Only the indices pass through the asm: a pointer that does comes out of
-    // it generic, so these adds become FLAT atomics, and a FLAT operation that
-    // may be in flight makes the wait-count pass wait for every load
-    // (vmcnt(0)) at each use of a streamed group, all through the unit loop.
-    // FLAT = true keeps exactly that, for the single-end stats / filter
-    // kernel only: measured on one box over 4 alternating rounds, C2 runs
-    // 532 us with the coarse waits and 540 us with the exact ones (C3 is 6 %
-    // faster exact, the edit kernels 2-4 %): fewer loads in flight per wave
-    // suit its plain stream
-    if (FLAT) asm volatile("" : "+v"(p0), "+s"(lmax), "+s"(pos_acc));
-    else asm volatile("" : "+v"(p0), "+s"(lmax));
+    // it generic, so these adds became FLAT atomics (round 5), and a FLAT
+    // operation that may be in flight makes the wait-count pass wait for
+    // every load at each use of a streamed group, all through the unit loop.
+    // (C2's share of that coarse waiting is now an explicit wait, tri_body)
+    asm volatile("" : "+v"(p0), "+s"(lmax));
 #pragma unroll
     for (int w = 0; w < NW; ++w) {
       const uint32_t qv[4] = {q02[w] & 0xFFFFu, q13[w] & 0xFFFFu, q02[w] >> 16, q13[w] >> 16};
@@ -184,12 +178,10 @@ __device__ __forceinline__ uint32_t tri_codes(uint32_t s, uint32_t m, uint32_t &
 
 // rare path: bytes that are not exactly A/C/G/T/N get code 0 (counted nowhere)
 // and one "other" count per position (sign: +1 add, -1 subtract)
-template <bool FLAT>
 __device__ __forceinline__ uint32_t tri_fix(uint32_t s, uint32_t m, uint32_t codes, uint32_t *other,
                                             int lmax, int pos0, uint32_t sign) {
-  // rare path: no hoisted addresses (FLAT: see TriAcc::flush)
-  if (FLAT) asm volatile("" : "+v"(pos0), "+s"(lmax), "+s"(other));
-  else asm volatile("" : "+v"(pos0), "+s"(lmax));
+  // rare path: no hoisted addresses (see TriAcc::flush)
+  asm volatile("" : "+v"(pos0), "+s"(lmax));
   const uint32_t ex = __builtin_amdgcn_perm(kX7Hi, kX7Lo, codes);
   const uint32_t ff = nonzero_bytes((s ^ ex) & m);
   if (ff) {
@@ -745,7 +737,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     if (__builtin_expect(bad != 0, 0)) {
       const uint32_t sign = SUB ? 0xFFFFFFFFu : 1u;
 #pragma unroll
-      for (int w = 0; w < NW; ++w) cd[w] = tri_fix<PF>(sw[w], mk[w], cd[w], other(m), count ? lp : 0, p0 + 4 * w, sign);
+      for (int w = 0; w < NW; ++w) cd[w] = tri_fix(sw[w], mk[w], cd[w], other(m), count ? lp : 0, p0 + 4 * w, sign);
     }
     uint32_t cg[NW];
 #pragma unroll
@@ -936,7 +928,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     if (!LATE) describe_next();
     if (stats && since_flush > kByteEvery - kBlock / kSegs) {   // keep every byte <= 255
 #pragma unroll
-      for (int m = 0; m < NM; ++m) acc[m].template flush<PF>(pos_acc(m), lp, p0);
+      for (int m = 0; m < NM; ++m) acc[m].flush(pos_acc(m), lp, p0);
       since_flush = 0;
     }
     // an even number of groups per mate, so every mate (and unit) starts in
@@ -1016,6 +1008,15 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
         if (m == NM - 1 && last) issue_dma();   // (the unit's last group pair)
         load_group(m, tb, nt, g + 1, 1);
         process_group(g, 0);
+        // PF (C2 and its N / out-of-range variants): every load waited for
+        // before the next group's are issued, so a wave holds one group in
+        // flight while it counts the other -- the coarse waits that round 5's
+        // FLAT atomics induced by accident (ISA: a vmcnt(0) before this
+        // table read), now stated: same box, 4 alternating rounds, 537 us
+        // against 546 with the compiler's exact waits and 541 with the FLAT
+        // ones (profiles/r06_c2_waits_ab.json); the edit, paired-end and
+        // window kernels run faster with exact waits (round 5)
+        if (PF) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (NM == 1 && LATE) {
           // edit: ONE load site for slot 0, this unit's next group or the next
           // unit's first, behind the next unit's prologue (round 5: C4 811 ->
@@ -1216,7 +1217,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
 #pragma unroll
   for (int m = 0; m < NM; ++m) {
     acc[m].widen();
-    acc[m].template flush<PF>(pos_acc(m), lp, p0);
+    acc[m].flush(pos_acc(m), lp, p0);
     const uint64_t tot = wave_sum64((uint64_t)fxs(m)[lane]);   // (LDS: in order per wave)
     if (lane == 0) {
       unsigned long long *s = sc(m);

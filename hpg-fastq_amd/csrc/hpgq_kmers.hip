@@ -327,11 +327,108 @@ __global__ void __launch_bounds__(kWG) kmer_tile_kernel(const char *seq, const i
   for (int i = threadIdx.x; i < kP * kNum; i += kWG) my[i] = t[i];
 }
 
+// The starts >= npos of the counted reads longer than lmax (the reference's
+// counter_by_pos grows with the read, src/stats_fastq.c:394-407).  Shaped like
+// the maxlen prepass: each thread checks four reads (one 16-byte offset load +
+// one, the four mask bytes), so the batch's 5 B per read stream at full rate
+// (round 6 first had each wave walk 64 reads per step, a dependent load chain:
+// +38 us per 10 M reads); a wave holding such a read takes it with all its
+// lanes over its starts [max(lo, npos), hi), one u64 atomic per 5-mer into the
+// tail [cap][kNum] (start npos + i).  flags[0]: the longest such read
+// (atomicMax), flags[1]: the longest whose starts reach past hi -- a device
+// batch beyond the tail reserved so far; its call's flag is set and
+// hpgq_kmers_sync adds the rest (tail_only: starts [lo, hi) only, no maxima).
+// A maxlen prepass of the same call (lmax > 260) that found no counted read
+// past npos + 4 ends it at once.
+struct LongArgs {
+  const char *seq;
+  const int32_t *idx;
+  int64_t n;
+  const uint8_t *mask;
+  const int *maxlen_pre;
+  unsigned long long *tail;
+  int lo, hi;
+  uint32_t *flags, *ovf;
+  int tail_only;
+};
+
+__device__ __forceinline__ void long_reads_block(const LongArgs &L, int npos, int64_t blk) {
+  if (L.maxlen_pre && *L.maxlen_pre < npos + kK) return;
+  const int lane = threadIdx.x & 63;
+  const int64_t r0 = 4 * (blk * 256 + threadIdx.x);
+  uint32_t lng = 0;   // bit i: read r0 + i counts and has starts >= npos
+  int32_t a[5] = {0, 0, 0, 0, 0};
+  if (r0 < L.n) {
+    // (through descriptors, as kmer_maxlen_kernel: any dword alignment; past
+    // the batch the offsets read 0 and the mask bytes 0)
+    const __amdgpu_buffer_rsrc_t ri = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)L.idx, (short)0, (uint32_t)((L.n + 1) * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)L.mask, (short)0, L.mask ? (uint32_t)L.n : 0u, 0x00020000);
+    if (r0 + 4 <= L.n) {
+      const v4u x = __builtin_amdgcn_raw_buffer_load_b128(ri, (uint32_t)r0 * 4u, 0, 0);
+      a[0] = (int32_t)x[0]; a[1] = (int32_t)x[1]; a[2] = (int32_t)x[2]; a[3] = (int32_t)x[3];
+      a[4] = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(ri, (uint32_t)r0 * 4u + 16u, 0, 0);
+    } else {   // the batch's last reads: one by one (a load reaching past the range reads 0)
+      for (int i = 0; i < 5; ++i)
+        a[i] = (int32_t)__builtin_amdgcn_raw_buffer_load_b32(ri, (uint32_t)min(r0 + i, L.n) * 4u, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (r0 + i < L.n && a[i + 1] - a[i] >= npos + kK) lng |= 1u << i;
+    // the mask only for the (rare) long ones: 4 B per read streamed, not 5
+    if (lng && L.mask) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (((lng >> i) & 1u) && __builtin_amdgcn_raw_buffer_load_b8(rm, (uint32_t)(r0 + i), 0, 0) != 1u)
+          lng &= ~(1u << i);
+    }
+  }
+  uint64_t b = __ballot(lng != 0);
+  while (b) {   // (rare) the wave's long reads, one at a time
+    const int j = __builtin_ctzll(b);
+    b &= b - 1;
+    uint32_t bits = (uint32_t)__builtin_amdgcn_readlane((int)lng, j);
+    while (bits) {
+      const int i = __builtin_ctz(bits);
+      bits &= bits - 1;
+      const int32_t aj = __builtin_amdgcn_readlane(i == 0 ? a[0] : i == 1 ? a[1] : i == 2 ? a[2] : a[3], j);
+      const int32_t lj = __builtin_amdgcn_readlane(i == 0 ? a[1] : i == 1 ? a[2] : i == 2 ? a[3] : a[4], j) - aj;
+      const int last = lj - kK;   // its last start
+      if (!L.tail_only && lane == 0) atomicMax(&L.flags[0], (uint32_t)lj);
+      const int end = min(last + 1, L.hi);
+      const uint8_t *sq = reinterpret_cast<const uint8_t *>(L.seq) + aj;
+      for (int p = max(L.lo, npos) + lane; p < end; p += 64) {
+        int id = 0;
+        bool ok = true;
+#pragma unroll
+        for (int k = 0; k < kK; ++k) {
+          const uint8_t c = sq[p + k];
+          const int code = c == 'A' ? 0 : c == 'C' ? 1 : c == 'G' ? 2 : c == 'T' ? 3 : -1;
+          ok = ok && code >= 0;
+          id = id * 4 + (code & 3);
+        }
+        if (ok) atomicAdd(&L.tail[(size_t)(p - npos) * kNum + id], 1ull);
+      }
+      if (last + 1 > L.hi && lane == 0) {
+        atomicMax(&L.flags[1], (uint32_t)lj);
+        if (L.ovf) *L.ovf = 1u;
+      }
+    }
+  }
+}
+
 // by_pos[id][p0 + row] += the sum of a tile's slabs (8 XCDs x classes); one
 // thread per (tile, id, row), consecutive threads consecutive positions (the
-// slab reads and the by_pos adds coalesce)
+// slab reads and the by_pos adds coalesce).  Blocks past the reduction's are
+// the long-read pass (long_reads_block): one launch, the scan overlapping the
+// reduction.
 __global__ void __launch_bounds__(256) kmer_reduce_kernel(const uint32_t *slab, int npos, const int *maxlen, int grid,
-                                                          unsigned long long *out) {
+                                                          unsigned long long *out, int reduce_blocks, LongArgs L) {
+  if ((int)blockIdx.x >= reduce_blocks) {
+    long_reads_block(L, npos, (int64_t)blockIdx.x - reduce_blocks);
+    return;
+  }
   const int last_start = min(npos, (maxlen ? *maxlen : npos + kK - 1) - (kK - 1));
   const int T = last_start > 0 ? (last_start + kP - 1) / kP : 0;
   const int64_t f = (int64_t)blockIdx.x * 256 + threadIdx.x;   // tile * kP * kNum + id * kP + row
@@ -347,57 +444,9 @@ __global__ void __launch_bounds__(256) kmer_reduce_kernel(const uint32_t *slab, 
   if (sum) out[(size_t)(cell / kP) * npos + p] += sum;
 }
 
-// Starts >= npos of the counted reads longer than lmax (the reference's
-// counter_by_pos grows with the read, src/stats_fastq.c:394-407): the waves
-// walk the batch 64 reads at a time (one coalesced offset load + the mask
-// bytes), and each such read is taken by its wave, lanes over its starts
-// [max(lo, npos), hi), one u64 atomic per 5-mer into the tail [cap][kNum]
-// (start npos + i).  flags[0]: the longest such read (atomicMax), flags[1]:
-// the longest whose starts reach past hi -- a device batch beyond the tail
-// reserved so far; its call's flag is set and hpgq_kmers_sync adds the rest
-// (TAIL_ONLY: starts [lo, hi) only, no maxima).  A maxlen prepass of the same
-// call (lmax > 260) that found no counted read past npos + 4 ends it at once.
-__global__ void __launch_bounds__(256) kmer_long_kernel(const char *seq, const int32_t *idx, int64_t n,
-                                                        const uint8_t *mask, int npos, const int *maxlen_pre,
-                                                        unsigned long long *tail, int lo, int hi, uint32_t *flags,
-                                                        uint32_t *ovf, int tail_only) {
-  if (maxlen_pre && *maxlen_pre < npos + kK) return;
-  const int lane = threadIdx.x & 63;
-  const int64_t nw = (int64_t)gridDim.x * 4;
-  for (int64_t r0 = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64; r0 < n; r0 += nw * 64) {
-    const int64_t r = r0 + lane;
-    int32_t a = 0, len = 0;
-    if (r < n && counted(mask, r)) {
-      a = idx[r];
-      len = idx[r + 1] - a;
-    }
-    uint64_t b = __ballot(len >= npos + kK);
-    while (b) {
-      const int j = __builtin_ctzll(b);
-      b &= b - 1;
-      const int32_t aj = __builtin_amdgcn_readlane(a, j), lj = __builtin_amdgcn_readlane(len, j);
-      const int last = lj - kK;   // its last start
-      if (!tail_only && lane == 0) atomicMax(&flags[0], (uint32_t)lj);
-      const int end = min(last + 1, hi);
-      const uint8_t *s = reinterpret_cast<const uint8_t *>(seq) + aj;
-      for (int p = max(lo, npos) + lane; p < end; p += 64) {
-        int id = 0;
-        bool ok = true;
-#pragma unroll
-        for (int i = 0; i < kK; ++i) {
-          const uint8_t c = s[p + i];
-          const int code = c == 'A' ? 0 : c == 'C' ? 1 : c == 'G' ? 2 : c == 'T' ? 3 : -1;
-          ok = ok && code >= 0;
-          id = id * 4 + (code & 3);
-        }
-        if (ok) atomicAdd(&tail[(size_t)(p - npos) * kNum + id], 1ull);
-      }
-      if (last + 1 > hi && lane == 0) {
-        atomicMax(&flags[1], (uint32_t)lj);
-        if (ovf) *ovf = 1u;
-      }
-    }
-  }
+// the long-read pass alone (lmax < 5: no dense table; the second pass)
+__global__ void __launch_bounds__(256) kmer_long_kernel(int npos, LongArgs L) {
+  long_reads_block(L, npos, blockIdx.x);
 }
 
 }  // namespace kmers
@@ -458,9 +507,8 @@ int k_ensure_tail(hpgq_kmers *k, int64_t cap) {
   return HPGQ_OK;
 }
 
-int k_long_grid(const hpgq_kmers *k, int64_t n) {
-  return (int)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 4 * (int64_t)k->cus));
-}
+// blocks of the long-read pass: four reads per thread
+int k_long_blocks(int64_t n) { return (int)std::max<int64_t>(1, (n + 1023) / 1024); }
 
 // the tail's second pass (the stream idle, h_flags current): see hpgq.h / the engine's resolve
 int k_resolve(hpgq_kmers *k) {
@@ -479,9 +527,10 @@ int k_resolve(hpgq_kmers *k) {
   for (size_t i = 0; i < nc; ++i) {
     if (!fl[i]) continue;
     const KCall &c = k->calls[i];
-    hipLaunchKernelGGL(hpgq::kmers::kmer_long_kernel, dim3((unsigned)k_long_grid(k, c.n)), dim3(256), 0, k->stream,
-                       c.seq, c.idx, c.n, c.mask, k->npos, (const int *)nullptr, k->d_tail, c.hi, k_tail_hi(k),
-                       k->d_flags, (uint32_t *)nullptr, 1);
+    const hpgq::kmers::LongArgs L{c.seq, c.idx, c.n, c.mask, nullptr, k->d_tail, c.hi, k_tail_hi(k), k->d_flags,
+                                  nullptr, 1};
+    hipLaunchKernelGGL(hpgq::kmers::kmer_long_kernel, dim3((unsigned)k_long_blocks(c.n)), dim3(256), 0, k->stream,
+                       k->npos, L);
     HPGQ_HIP_TRY(hipGetLastError());
   }
   HPGQ_HIP_TRY(hipMemsetAsync(k->d_flags + 1, 0, 4, k->stream));
@@ -590,6 +639,17 @@ int hpgq_kmers_count_device(hpgq_kmers_t *k, const hpgq_batch_t *b, const uint8_
       HPGQ_HIP_TRY(hipGetLastError());
       ml = k->d_maxlen;
     }
+    // starts >= npos of longer reads (the call is kept for the tail's second pass)
+    const size_t ci = k->calls.size();
+    if (ci / kKOvfChunk >= k->ovf_chunks.size()) {
+      uint32_t *q = nullptr;
+      if (hipMalloc(&q, kKOvfChunk * 4) != hipSuccess) return HPGQ_E_NOMEM;
+      k->ovf_chunks.push_back(q);
+      HPGQ_HIP_TRY(hipMemsetAsync(q, 0, kKOvfChunk * 4, k->stream));
+    }
+    k->calls.push_back(KCall{b->seq, ix, mk, n, k_tail_hi(k)});
+    const LongArgs L{b->seq, ix, n, mk, ml, k->d_tail, k->npos, k_tail_hi(k), k->d_flags,
+                     k->ovf_chunks[ci / kKOvfChunk] + ci % kKOvfChunk, 0};
     if (k->npos > 0) {   // (lmax < 5: every start is in the tail)
       if (mk)
         hipLaunchKernelGGL(kmer_tile_kernel<true>, dim3((unsigned)k->grid), dim3(kWG), 0, k->stream, b->seq, ix, n, mk,
@@ -598,24 +658,14 @@ int hpgq_kmers_count_device(hpgq_kmers_t *k, const hpgq_batch_t *b, const uint8_
         hipLaunchKernelGGL(kmer_tile_kernel<false>, dim3((unsigned)k->grid), dim3(kWG), 0, k->stream, b->seq, ix, n, mk,
                            k->npos, ml, k->d_slab);
       HPGQ_HIP_TRY(hipGetLastError());
-      hipLaunchKernelGGL(kmer_reduce_kernel, dim3((unsigned)(((int64_t)tmax * kP * kNum + 255) / 256)), dim3(256), 0,
-                         k->stream, (const uint32_t *)k->d_slab, k->npos, ml, k->grid, k->d_out);
-      HPGQ_HIP_TRY(hipGetLastError());
+      // the reduction and, in the same launch, the long-read pass
+      const int rb = (int)(((int64_t)tmax * kP * kNum + 255) / 256);
+      hipLaunchKernelGGL(kmer_reduce_kernel, dim3((unsigned)(rb + k_long_blocks(n))), dim3(256), 0, k->stream,
+                         (const uint32_t *)k->d_slab, k->npos, ml, k->grid, k->d_out, rb, L);
+    } else {
+      hipLaunchKernelGGL(kmer_long_kernel, dim3((unsigned)k_long_blocks(n)), dim3(256), 0, k->stream, k->npos, L);
     }
-    {   // starts >= npos of longer reads; the call is kept for the second pass
-      const size_t i = k->calls.size();
-      if (i / kKOvfChunk >= k->ovf_chunks.size()) {
-        uint32_t *q = nullptr;
-        if (hipMalloc(&q, kKOvfChunk * 4) != hipSuccess) return HPGQ_E_NOMEM;
-        k->ovf_chunks.push_back(q);
-        HPGQ_HIP_TRY(hipMemsetAsync(q, 0, kKOvfChunk * 4, k->stream));
-      }
-      uint32_t *ovf = k->ovf_chunks[i / kKOvfChunk] + i % kKOvfChunk;
-      k->calls.push_back(KCall{b->seq, ix, mk, n, k_tail_hi(k)});
-      hipLaunchKernelGGL(kmer_long_kernel, dim3((unsigned)k_long_grid(k, n)), dim3(256), 0, k->stream, b->seq, ix, n,
-                         mk, k->npos, ml, k->d_tail, k->npos, k_tail_hi(k), k->d_flags, ovf, 0);
-      HPGQ_HIP_TRY(hipGetLastError());
-    }
+    HPGQ_HIP_TRY(hipGetLastError());
   }
   return HPGQ_OK;
 }
