@@ -2,7 +2,9 @@
 // (built once per geometry with -DHPGQ_GEO=0|1|2, so the three compile in
 // parallel).  Occupancy per variant (MINW, waves per SIMD) is the highest at
 // which the variant's registers fit without spills: single-end 4 (tri 5),
-// paired-end 3 (two mates' accumulators), see DESIGN.md §4.1.  Every
+// paired-end 3 (two mates' accumulators), single-end edit 3 (its next trim
+// windows held in VGPRs, tri_body EG; 4 with the extra scans or as a
+// follow-up), see DESIGN.md §4.1.  Every
 // combination of paired-end, edit and the extra filter scans has an instance.
 #include <cstdio>
 
@@ -26,15 +28,16 @@ constexpr int kSeW = HPGQ_SE_WAVES;          // single-end
 #endif
 constexpr int kPeW = HPGQ_PE_WAVES;          // paired-end
 #ifndef HPGQ_EDIT_WAVES
-#define HPGQ_EDIT_WAVES kSeW
+#define HPGQ_EDIT_WAVES 3
 #endif
-constexpr int kEdW = HPGQ_EDIT_WAVES;        // single-end edit
+constexpr int kEdW = HPGQ_EDIT_WAVES;        // single-end edit (its trim windows in VGPRs a group early: tri_body EG)
+constexpr int kEdXW = kSeW;                  // single-end edit with extra filter scans
 constexpr const char *kGeoName = G == GEO_TRI ? "tri" : (G == GEO_HEX ? "hex" : "wide");
 
 template <bool F, int XM, bool EDIT>
 const void *x_kernel(int nm) {
   return nm == 2 ? (const void *)engine_tri_x_kernel<kPeW, 2, G, F, XM, EDIT>
-                 : (const void *)engine_tri_x_kernel<EDIT ? kEdW : kSeW, 1, G, F, XM, EDIT>;
+                 : (const void *)engine_tri_x_kernel<EDIT ? kEdXW : kSeW, 1, G, F, XM, EDIT>;
 }
 
 template <bool F, bool EDIT>
@@ -46,7 +49,7 @@ const void *x_kernel_for(int nm, int xm) {
 template <bool F>
 SegChoice pick(int nm, bool edit, int xm, char *name, size_t cap) {
   const void *fn = nullptr;
-  const int w = nm == 2 ? kPeW : (edit ? kEdW : kSeW);
+  const int w = nm == 2 ? kPeW : (edit ? (xm || F ? kEdXW : kEdW) : kSeW);
   if (xm) {
     fn = edit ? x_kernel_for<F, true>(nm, xm) : x_kernel_for<F, false>(nm, xm);
     std::snprintf(name, cap, "hpgq::engine_tri_x_kernel<%d, %d, %s%s%s%s%s>", w, nm, kGeoName,
@@ -55,7 +58,7 @@ SegChoice pick(int nm, bool edit, int xm, char *name, size_t cap) {
   } else {
     if (nm == 2) fn = edit ? (const void *)engine_tri_kernel<kPeW, 2, true, G, F>
                            : (const void *)engine_tri_kernel<kPeW, 2, false, G, F>;
-    else if (edit) fn = (const void *)engine_tri_kernel<kEdW, 1, true, G, F>;
+    else if (edit) fn = (const void *)engine_tri_kernel<F ? kSeW : kEdW, 1, true, G, F>;
     else fn = (const void *)engine_tri_kernel<kSeW, 1, false, G, F>;
     std::snprintf(name, cap, "hpgq::engine_tri_kernel<%d, %d, %s, %s%s>", w, nm, edit ? "edit" : "filter", kGeoName,
                   F ? ", follow" : "");

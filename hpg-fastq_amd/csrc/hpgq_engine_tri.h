@@ -430,6 +430,14 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   // fetched earlier, are evicted before the stream comes back for them: HBM
   // traffic 1.34 -> 1.40x, C4 824 -> 840 us), so single-end keeps the gathers.
   constexpr bool TDMA = EDIT && !FOLLOW && NM == 2 && XM == 0;
+  // EG (single-end edit, first stage, no extra scans; 3 waves per SIMD, which
+  // leave the registers): the next unit's trim windows gathered into VGPRs at
+  // the top of this unit's last group pair -- a group of work before the
+  // prologue that finishes them, instead of a round trip the prologue waits
+  // for.  Round 6, one box, 3 alternating rounds: C4 844 us against 850 (the
+  // same at 4 waves per SIMD spilled 7 VGPRs and ran slower, round 5; the
+  // extra-scan kernels, c4_noor, ran 2.9 % slower with it and keep 4 waves)
+  constexpr bool EG = EDIT && !FOLLOW && NM == 1 && XM == 0;
   if (FOLLOW && follow_up_idle(A)) return;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x;
@@ -578,7 +586,8 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   // and deferred reads get length 0 and out-of-range offsets.  Returns this
   // lane's lengths (the epilogue needs them) and the deferred-lane mask.
   auto load_block = [&](const Unit &U, int tb, uint32_t (&len)[NM], uint32_t (&tw)[NM], uint64_t &dm,
-                        const int32_t (&ia)[NM], const int32_t (&ie)[NM], bool dma) __attribute__((always_inline)) {
+                        const int32_t (&ia)[NM], const int32_t (&ie)[NM], bool dma,
+                        const TrimLoads *pre = nullptr) __attribute__((always_inline)) {
     const bool on = lane < U.nr;
     const uint32_t rid = (uint32_t)(U.u * ublock) + (FOLLOW ? scratch[lane] : (uint32_t)lane);
     bool dfr = false;
@@ -625,12 +634,14 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       for (int m = 0; m < NM; ++m)
         tl[m] = trim_issue(cold, rq[m], live ? bq[m] + ia[m] : (int)0xC0000000, ie[m] - ia[m]);
     }
+    const bool pre_ok = EG && pre != nullptr && trim_usual(cold);   // EG: issued by gather_next
+    if (pre_ok) tl[0] = *pre;
 #pragma unroll
     for (int m = 0; m < NM; ++m) {
       int a = ia[m], e = ie[m];
       tw[m] = 0;
       if (EDIT) {   // trim here, then describe the trimmed window
-        tw[m] = !live ? 0u : usual ? trim_finish(cold, tl[m], e - a) : trim_word(cold, rq[m], bq[m] + a, e - a);
+        tw[m] = !live ? 0u : (usual || pre_ok) ? trim_finish(cold, tl[m], e - a) : trim_word(cold, rq[m], bq[m] + a, e - a);
         if (A.trim && live) A.trim[(size_t)m * (size_t)A.num_reads + rid] = tw[m];
         a += (int)(tw[m] & 0xFFFFu);
         e -= (int)(tw[m] >> 16);
@@ -915,12 +926,19 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     auto issue_dma = [&]() __attribute__((always_inline)) {
       if (tdma && nxt.u >= 0) dma_windows(nxt);
     };
+    TrimLoads pre_tl;   // EG: the next unit's trim windows, issued a group early
+    auto gather_next = [&]() __attribute__((always_inline)) {
+      if (!EG || !trim_usual(cold_all)) return;
+      const bool on = lane < nxt.nr;
+      const bool live = on && !(ie[0] - ia[0] > dlim);
+      pre_tl = trim_issue(cold_all, rq[0], live ? bq[0] + ia[0] : (int)0xC0000000, ie[0] - ia[0]);
+    };
     auto describe_next = [&]() __attribute__((always_inline)) {
       // (the DMA is the youngest VMEM operation here: issued inside the pair's
       // first process_pair after its loads were waited for, or -- a wholly
       // deferred unit -- just before)
       if (tdma) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      load_block(nxt, tb ^ 1, lenn, twn, dmn, ia, ie, true);
+      load_block(nxt, tb ^ 1, lenn, twn, dmn, ia, ie, true, EG ? &pre_tl : nullptr);
       nn2 = it.next();
       fetch_idx(nn2, ia, ie);
       nnt = steps_of(nxt, dmn);
@@ -1006,6 +1024,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       for (int g = 0; g < ngroups; g += 2) {
         const bool last = g + 2 >= ngroups;
         if (m == NM - 1 && last) issue_dma();   // (the unit's last group pair)
+        if (EG && last) gather_next();
         load_group(m, tb, nt, g + 1, 1);
         process_group(g, 0);
         // PF (C2 and its N / out-of-range variants): every load waited for
@@ -1091,6 +1110,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       load_group_pe(tb ^ 1, nnt, 0, 0);   // a wholly deferred unit: straight to the next
     } else {
       issue_dma();
+      gather_next();
       if (LATE) describe_next();
       load_group(0, tb ^ 1, nnt, 0, 0);   // a wholly deferred unit: straight to the next
     }

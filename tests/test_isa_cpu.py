@@ -4,10 +4,10 @@ segmented engine kernels keep the properties DESIGN.md §4.1 measured.
 Round 5 found that two rare LDS adds had become FLAT atomics (their pointer
 went through an empty asm and came out generic); a FLAT operation that may be
 in flight makes hipcc's wait-count pass wait for EVERY load at each later use,
-all through the unit loop.  Only the single-end stats / filter kernels (tri_body's
-`PF` ones: C2 and its N / out-of-range variants) keep them, because C2 measured
-faster with the coarse waits; every edit, paired-end, window-scan and
-follow-up kernel must carry none.
+all through the unit loop.  Round 5 kept that accident in the single-end stats
+/ filter kernel (C2), which measured faster with the coarse waits; round 6
+states C2's wait explicitly in the source (tri_body, PF) and every segmented
+kernel must carry no FLAT load or atomic.
 """
 import os
 import re
