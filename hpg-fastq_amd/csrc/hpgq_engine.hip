@@ -254,7 +254,8 @@ static size_t seg_lds(const hpgq_params_t &p, int nm, int xm, int pos, bool foll
   // unit's trim windows, 3 x block x 16 B per mate, tri_body TDMA)
   const bool tdma = p.edit_on && !follow && nm == 2 && xm == 0;
   const size_t dma_words = tdma ? (size_t)nm * 3 * (size_t)block * 4 : 0;
-  return (size_t)nm * mate_words * 4 + 16 + 17 * 16 +
+  // (after the byte-mask table: the reciprocal table [pos + 1] of the epilogue's divisions)
+  return (size_t)nm * mate_words * 4 + 16 + 17 * 16 + ((size_t)pos + 1) * 4 +
          (size_t)hpgq::kWaves * ((size_t)nm * (2 * 256 + 64 * lists + hpgq::kFxWords) + 64 + 4 + dma_words) * 4;
 }
 

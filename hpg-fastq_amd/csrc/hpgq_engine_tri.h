@@ -44,6 +44,10 @@
 #pragma once
 #include "hpgq_engine_kernel.h"
 
+#ifndef HPGQ_GT_DIST
+#define HPGQ_GT_DIST 0   // GT in tri_body: groups ahead the trim windows are gathered (0: off)
+#endif
+
 namespace hpgq {
 
 constexpr int kTriSlack = 8;    // readable bytes past the data end the loads may touch
@@ -56,7 +60,11 @@ constexpr int kTriSlack = 8;    // readable bytes past the data end the loads ma
 // (one no-return ds_add_u64 per unit) instead of a VGPR pair held across the
 // loop: the paired-end edit kernel spilled exactly those pairs, a scratch
 // load + store per unit and mate (~200 MB of scratch writes per 10 M pairs).
-constexpr int kFxWords = 128;   // per wave and mate: 64 u64
+// (32 slots, lane & 31, since round 6: two lanes add into each, which frees
+// the LDS the reciprocal table takes without costing the paired-end edit
+// kernel its third workgroup per CU)
+constexpr int kFxSlots = 32;
+constexpr int kFxWords = 2 * kFxSlots;   // per wave and mate: kFxSlots u64
 
 constexpr int GEO_TRI = 0, GEO_HEX = 1, GEO_WIDE = 2;
 constexpr int X_NOOR = 1, X_LR = 2;   // extra filter scans (engine_tri_x_kernel)
@@ -372,6 +380,31 @@ __device__ __forceinline__ uint32_t trim_word(const ColdParams &C, __amdgpu_buff
   return (uint32_t)ts | ((uint32_t)te << 16);
 }
 
+// floor(x / n) for a read length 1 <= n <= 252 from rc = ceil(2^32 / n) (the
+// kernel's rtab; n = 1 has rc = 0 and one1 = 1): q = mulhi(x, rc) is exact
+// while x * (n - 1) < 2^32 (the error of rc times x stays below one unit of
+// 1 / n), which holds for every numerator of the unit epilogue (biased
+// quality sums < 2^16, 100 x G+C, remainders << 16 < n 2^16)
+__device__ __forceinline__ uint32_t div_len(uint32_t x, uint32_t rc, uint32_t one1) {
+  return __umulhi(x, rc) + __umul24(x, one1);
+}
+
+// meanq_terms (hpgq_engine_kernel.h) for the segmented kernels' reads (n <=
+// 252) by div_len: one multiply-high per quotient instead of a 32-bit division
+// (round 6: ~65 VALU per unit epilogue and mate)
+__device__ __forceinline__ void meanq_terms_rc(uint32_t sb, uint32_t n, uint32_t rc, uint32_t one1, uint32_t &bin,
+                                               uint64_t &fx) {
+  const uint32_t off = (uint32_t)kQBias * n;
+  const uint32_t q = div_len(sb, rc, one1), rem = sb - __umul24(q, n);
+  if (__builtin_expect(sb >= off, 1)) {
+    bin = q + (2 * rem >= n ? 1u : 0u) - (uint32_t)kQBias;   // (2 sb + n) / (2 n) - 128
+  } else {
+    const uint32_t t = off - sb, qt = div_len(t, rc, one1), rt = t - __umul24(qt, n);
+    bin = (256u - (qt + (2 * rt >= n ? 1u : 0u))) & 255u;
+  }
+  fx = ((uint64_t)q << 16) + div_len(rem << 16, rc, one1) - ((uint64_t)kQBias << 16);
+}
+
 template <int M>
 struct MateTag {
   static constexpr int value = M;
@@ -409,7 +442,13 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   // (edit, follow-up: their registers would spill; the window variant alone
   // fails few reads and ran 4 % slower with it: 692 vs 665 us per 10 M reads)
   constexpr bool PF = NM == 1 && !EDIT && !FOLLOW && XM != X_LR;
-  constexpr bool LATE = EDIT;   // the unit prologue's place (see the unit loop)
+  // GT (single-end edit, first stage, no extra scans; HPGQ_GT_DIST groups
+  // ahead, 0 = off): trims per GROUP, finished right before the group's loads
+  // from windows gathered GTD groups earlier (gt_issue / gt_patch below); the
+  // unit prologue then reads no quality and runs a unit ahead like C2's
+  constexpr int GTD = (EDIT && NM == 1 && !FOLLOW && XM == 0) ? HPGQ_GT_DIST : 0;
+  constexpr bool GT = GTD > 0;
+  constexpr bool LATE = EDIT && !GT;   // the unit prologue's place (see the unit loop)
   constexpr bool TABLEN = !FOLLOW;   // epilogue lengths / trims from the read table
   // PEU (paired-end): a group is ONE step of both mates (grp[slot][m]); both
   // are added, the pair is decided from both scans at once (ds_bpermute), and
@@ -422,6 +461,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   constexpr int NW = GG::kNW, kSegs = GG::kSegs, kSegW = GG::kSegW, kBlock = GG::kBlock, kU = GG::kU;
   static_assert(4 * kU <= kNibbleEvery && kBlock / kSegs - 4 * kU <= kNibbleEvery, "nibble widening");
   static_assert(kSegs * kSegW <= 64 && kBlock < 64 && kBlock % kSegs == 0, "geometry");
+  constexpr bool kMidWiden = kBlock / kSegs > 4 * kU;   // more steps per unit than 4 groups
   // TDMA (paired-end edit, first stage, no extra scans -- whose LDS would not
   // fit at 3 workgroups per CU): a unit's trim windows come from LDS, DMA'd
   // there during the unit before's last group pair, instead of gathers whose
@@ -437,7 +477,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   // for.  Round 6, one box, 3 alternating rounds: C4 844 us against 850 (the
   // same at 4 waves per SIMD spilled 7 VGPRs and ran slower, round 5; the
   // extra-scan kernels, c4_noor, ran 2.9 % slower with it and keep 4 waves)
-  constexpr bool EG = EDIT && !FOLLOW && NM == 1 && XM == 0;
+  constexpr bool EG = EDIT && !FOLLOW && NM == 1 && XM == 0 && !GT;
   if (FOLLOW && follow_up_idle(A)) return;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x;
@@ -527,7 +567,8 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     return reinterpret_cast<unsigned long long *>(scratch + 64 + 4 + m * kFxWords);
   };
 #pragma unroll
-  for (int m = 0; m < NM; ++m) fxs(m)[lane] = 0ull;
+  for (int m = 0; m < NM; ++m)
+    if (lane < kFxSlots) fxs(m)[lane] = 0ull;
   // byte masks by valid-byte count c = clamp(n - p0, 0, 4 NW): mtab[c][w]
   // (one LDS read per step instead of a clamp and a 64-bit shift per word)
   uint32_t *mtab = base + tab_words + kWaves * kWaveWords;   // 16 B aligned
@@ -535,6 +576,10 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     const int nb = min(max(i / NW - 4 * (i % NW), 0), 4);
     mtab[i] = nb == 4 ? 0xFFFFFFFFu : (1u << (8 * nb)) - 1u;
   }
+  // the epilogue's divisions by a read's length n <= kPos as multiply-highs:
+  // rtab[n] = ceil(2^32 / n) (0 for n = 1, see div_len)
+  uint32_t *rtab = mtab + 17 * 4;
+  for (int i = tid; i <= GG::kPos; i += kWG) rtab[i] = i <= 1 ? 0u : 0xFFFFFFFFu / (uint32_t)i + 1u;
   for (int i = tid; i < NM * mate_words; i += kWG) base[i] = 0;
   __syncthreads();
 
@@ -618,6 +663,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     const ColdParams &cold = cold_all;
     const bool fromdma = TDMA && dma && trim_usual(cold);
     const bool usual = EDIT && (fromdma || (NM == 2 && trim_usual(cold)));
+    const bool grouped = GT && trim_usual(cold);   // (GT: untrimmed here, trimmed per group)
     if (fromdma) {
 #pragma unroll
       for (int m = 0; m < NM; ++m) {
@@ -641,8 +687,10 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       int a = ia[m], e = ie[m];
       tw[m] = 0;
       if (EDIT) {   // trim here, then describe the trimmed window
-        tw[m] = !live ? 0u : (usual || pre_ok) ? trim_finish(cold, tl[m], e - a) : trim_word(cold, rq[m], bq[m] + a, e - a);
-        if (A.trim && live) A.trim[(size_t)m * (size_t)A.num_reads + rid] = tw[m];
+        tw[m] = !live || grouped       ? 0u
+                : (usual || pre_ok) ? trim_finish(cold, tl[m], e - a)
+                                    : trim_word(cold, rq[m], bq[m] + a, e - a);
+        if (A.trim && live && !grouped) A.trim[(size_t)m * (size_t)A.num_reads + rid] = tw[m];
         a += (int)(tw[m] & 0xFFFFu);
         e -= (int)(tw[m] >> 16);
         if (e < a) e = a;
@@ -663,9 +711,9 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   auto steps_of = [&](const Unit &U, uint64_t dm) __attribute__((always_inline)) {
     return __builtin_popcountll(dm) == U.nr ? 0 : (U.nr + kSegs - 1) / kSegs;
   };
-  // lane -> its segment's read (entry `src` of mate m's read table tb)
-  auto gather = [&](int m, int tb, int src, TriPending<NW> &pd) __attribute__((always_inline)) {
-    const v4u rec = *reinterpret_cast<const v4u *>(tab(m, tb) + 4 * src);
+  // lane -> its segment's read (the entry `eoff` bytes into mate m's read table tb)
+  auto gather_at = [&](int m, int tb, uint32_t eoff, TriPending<NW> &pd) __attribute__((always_inline)) {
+    const v4u rec = *reinterpret_cast<const v4u *>(reinterpret_cast<const uint8_t *>(tab(m, tb)) + eoff);
     pd.n = rec.z;
     if (NW == 2) {
       const v2u a = __builtin_amdgcn_raw_buffer_load_b64(rs[m], rec.x + lane8, 0, 0);
@@ -681,6 +729,27 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       }
     }
   };
+  auto gather = [&](int m, int tb, int src, TriPending<NW> &pd) __attribute__((always_inline)) {
+    gather_at(m, tb, 16u * (uint32_t)src, pd);
+  };
+  // step t's entry of this lane: kSegs t + seg (< kBlock + kSegs <= 64 for every
+  // lane, idle ones included); a step past the unit end (t >= nt) reads entry
+  // kBlock + seg, which no read of a unit fills (length 0, offsets out of
+  // range: it adds nothing and loads nothing; a follow-up unit -- wide, 60 --
+  // holds at most the 54 reads of a tri / hex unit, plan_chain).  The step part is uniform, so
+  // the address is one VALU add (round 6; a clamp and a select were 5)
+  const uint32_t seg16 = 16u * (uint32_t)seg;
+  // segment end of step t -> list[kSegs t + seg] (the step part uniform: one
+  // VALU add for the address, not a 64-bit multiply-add)
+  // (the empty asm keeps hipcc from folding the two into a v_mad_u64_u32)
+  auto put_end = [&](uint32_t *list, int t, uint32_t v) __attribute__((always_inline)) {
+    uint32_t so = (uint32_t)(4 * kSegs * t);
+    asm volatile("" : "+s"(so));
+    *reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(list) + (seg16 >> 2) + so) = v;
+  };
+  auto step_off = [&](int t, int ntt) __attribute__((always_inline)) {
+    return seg16 + (t < ntt ? (uint32_t)(16 * kSegs * t) : (uint32_t)(16 * kBlock));
+  };
 
   TriPending<NW> grp[2][kU];
   // issue group g (kU steps) of mate m; steps past the unit end gather
@@ -688,15 +757,14 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   auto load_group = [&](int m, int tb, int nt, int g, int slot) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
-      const int t = g * kU + u;
-      gather(m, tb, t < nt ? min(kSegs * t + seg, 63) : 63, grp[slot][u]);
+      gather_at(m, tb, step_off(g * kU + u, nt), grp[slot][u]);
     }
   };
 
   // PEU: group g = step g of both mates
   auto load_group_pe = [&](int tbx, int ntx, int g, int slot) __attribute__((always_inline)) {
 #pragma unroll
-    for (int m = 0; m < NM; ++m) gather(m, tbx, g < ntx ? min(kSegs * g + seg, 63) : 63, grp[slot][m]);
+    for (int m = 0; m < NM; ++m) gather_at(m, tbx, step_off(g, ntx), grp[slot][m]);
   };
 
   // byte masks of the lane's words for the positions < p0 + c (c clamped to [0, 4 NW])
@@ -898,13 +966,97 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     mate(MateTag<0>{});
     if (NM == 2) mate(MateTag<NM - 1>{});
   };
+  // GT (single-end edit, usual windows): the trims of group x's kSegs kU reads
+  // are finished right before the group's loads (gt_patch) from windows
+  // gathered GTD groups earlier (gt_issue) by four lanes per read (lane 4r + p
+  // of the group's read r: p = 0 the first 16 quality bytes, p = 1, 2 the two
+  // halves of the 32 ending at the read's end, p = 3 idle; one b128 each) into
+  // buffer x & 1 (ngroups is even, so the parity runs on across units); the
+  // finished trims patch the group's read-table records.  A group whose
+  // windows were not gathered ahead (the first, and after a unit whose
+  // follower was not described yet) gathers them on the spot (the tag).
+  const bool gt = GT && trim_usual(cold_all);
+  v4u gw[2] = {v4u{0u, 0u, 0u, 0u}, v4u{0u, 0u, 0u, 0u}};
+  int gtag[2] = {-1, -1};   // (uniform) unit * 8 + group whose windows buffer b holds
+  auto gt_issue = [&](int b, int tbx, int grp, int tag) __attribute__((always_inline)) {
+    const int r = lane >> 2, p = lane & 3, idx = kSegs * kU * grp + r;
+    uint32_t addr = 0xC0000000u;   // (out of range: zeros, no traffic)
+    if (p < 3 && r < kSegs * kU && idx < 64) {
+      const v4u rec = *reinterpret_cast<const v4u *>(tab(0, tbx) + 4 * idx);
+      const int n = (int)(rec.z & 0xFFFFu), off = (int)(rec.y | ((rec.z >> 20) & 3u));
+      const int pa = max(off + n - 32, 0);
+      const bool want = p == 0 ? cold_all.e_left_len > 0 : cold_all.e_right_len > 0;
+      if (n > 0 && want && !(rec.y & 0x80000000u)) addr = (uint32_t)(p == 0 ? off : pa + 16 * (p - 1));
+    }
+    gw[b] = __builtin_amdgcn_raw_buffer_load_b128(rq[0], addr, 0, 0);
+    gtag[b] = tag;
+  };
+  auto gt_patch = [&](int b, int tbx, int grp, int tag, size_t ubase) __attribute__((always_inline)) {
+    if (gtag[b] != tag) gt_issue(b, tbx, grp, tag);
+    const int r = lane >> 2, p = lane & 3, idx = kSegs * kU * grp + r;
+    const bool act = r < kSegs * kU && idx < 64;
+    v4u rec = v4u{0x80000000u, 0x80000000u, 0u, 0u};
+    if (act) rec = *reinterpret_cast<const v4u *>(tab(0, tbx) + 4 * idx);
+    const int n = (int)(rec.z & 0xFFFFu), off = (int)(rec.y | ((rec.z >> 20) & 3u));
+    const int pa = max(off + n - 32, 0), hi = off + n - pa;   // hi: 32 but at the buffer's start
+    // this lane's side: the left window's constants on p = 0, the right's else
+    const TrimSide &L = cold_all.tl, &R = cold_all.tr;
+    const bool left = p == 0;
+    const v4u g4 = gw[b];
+    const uint32_t w4[4] = {g4.x, g4.y, g4.z, g4.w};
+    uint32_t ok[4];
+    if (trim_hi_none(L) && trim_hi_none(R)) {
+      const TrimSide S{left ? L.lq : R.lq, left ? L.l7 : R.l7, 0u, kQFlip};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ok[k] = trim_side_ok<true>(w4[k], S);
+    } else {
+      const TrimSide S{left ? L.lq : R.lq, left ? L.l7 : R.l7, left ? L.hq : R.hq, left ? L.h7 : R.h7};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) ok[k] = trim_side_ok<false>(w4[k], S);
+    }
+    int v;
+    if (left) {   // first in-range index (large when none)
+      uint32_t f = ~0u;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) f = min(f, (ffbl_raw(ok[k]) >> 3) + 4u * k);
+      v = (int)min(f, 0x3FFFFFFFu);
+    } else {      // last in-range index of the 32-byte tail (negative when none)
+      const int bo = 16 * (p - 1);
+      if (__builtin_expect(hi < 32, 0)) {   // a read at the buffer's start: bytes >= hi are the next read's
+#pragma unroll
+        for (int k = 0; k < 4; ++k) ok[k] &= byte_mask(hi - bo - 4 * k);
+      }
+      v = -1;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v = max(v, bo + 4 * k + 3 - (int)(ffbh_raw(ok[k]) >> 3));
+    }
+    const int v1 = __builtin_amdgcn_mov_dpp(v, 0x55, 0xF, 0xF, false);   // quad lane 1
+    const int v2 = __builtin_amdgcn_mov_dpp(v, 0xAA, 0xF, 0xF, false);   // quad lane 2
+    const bool live = act && !(rec.y & 0x80000000u);
+    if (left && live) {
+      const int ts = min(v, min(cold_all.e_left_len, n));
+      const int te = max(min(min(cold_all.e_right_len, n - ts), hi - 1 - max(v1, v2)), 0);
+      const uint32_t t = (uint32_t)ts | ((uint32_t)te << 16);
+      if (t) {
+        const uint32_t xs = (rec.x | ((rec.z >> 16) & 3u)) + (uint32_t)ts;
+        const uint32_t xq = (uint32_t)off + (uint32_t)ts, nn = (uint32_t)(n - ts - te);
+        *reinterpret_cast<v4u *>(tab(0, tbx) + 4 * idx) =
+            v4u{xs & ~3u, xq & ~3u, nn | ((xs & 3u) << 16) | ((xq & 3u) << 20), t};
+      }
+      if (A.trim) A.trim[ubase + (size_t)idx] = t;
+    }
+    __builtin_amdgcn_wave_barrier();   // (the group's loads read the records: LDS is in order per wave)
+  };
+  auto ngroups_of = [&](int nts) __attribute__((always_inline)) { return ((nts + kU - 1) / kU + 1) & ~1; };
   if (cur.u >= 0) {
     fetch_idx(cur, ia, ie);
     load_block(cur, tb, len, tw, dm, ia, ie, false);
     nxt = it.next();
     fetch_idx(nxt, ia, ie);
+    if (gt) gt_patch(0, tb, 0, cur.u * 8, (size_t)cur.u * kBlock);
     if (PEU) load_group_pe(tb, steps_of(cur, dm), 0, 0);
     else load_group(0, tb, steps_of(cur, dm), 0, 0);
+    if (gt && GTD < ngroups_of(steps_of(cur, dm))) gt_issue(GTD & 1, tb, GTD, cur.u * 8 + GTD);
   }
   constexpr uint64_t not_seg_first = not_seg_first_mask<G>();   // lanes j with j % kSegs != 0
   while (cur.u >= 0) {
@@ -951,7 +1103,21 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     }
     // an even number of groups per mate, so every mate (and unit) starts in
     // slot 0 (the padding group gathers length-0 reads)
-    const int ngroups = ((nt + kU - 1) / kU + 1) & ~1;
+    const int ngroups = ngroups_of(nt);
+    // GT: the windows of the group GTD after group x of this unit (nx false)
+    // or of the next one (nx true); past the next unit nothing is described yet
+    auto gt_ahead = [&](bool nx, int x) __attribute__((always_inline)) {
+      if (!gt) return;
+      int y = x + GTD;
+      if (!nx) {
+        if (y < ngroups) {
+          gt_issue(y & 1, tb, y, cur.u * 8 + y);
+          return;
+        }
+        y -= ngroups;
+      }
+      if (nxt.u >= 0 && y < ngroups_of(nnt)) gt_issue(y & 1, tb ^ 1, y, nxt.u * 8 + y);
+    };
 
     auto run_mate = [&](auto mtag) __attribute__((always_inline)) {
       constexpr int m = decltype(mtag)::value;
@@ -966,18 +1132,18 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
           const uint32_t x = account(MateTag<m>{}, grp[slot][u], stats && !PF, AddTag{}, x2, x3, sv);
           const uint32_t P = wave_scan(x);
           // segment ends (the last lane of each segment) -> wends[kSegs t + seg], no wait needed
-          if (ls == kSegW - 1 && seg < kSegs && t < nt) wends(m)[kSegs * t + seg] = P;
+          if (ls == kSegW - 1 && seg < kSegs && t < nt) put_end(wends(m), t, P);
           uint32_t P2 = 0, P3 = 0;
           if (NX) {
             P2 = wave_scan(x2);
-            if (ls == kSegW - 1 && seg < kSegs && t < nt) wends2(m)[kSegs * t + seg] = P2;
+            if (ls == kSegW - 1 && seg < kSegs && t < nt) put_end(wends2(m), t, P2);
           }
           if (LR) {
             if (w_direct) {   // the segment's first lane holds the whole window sum
-              if (ls == 0 && seg < kSegs && t < nt) wends3(m)[kSegs * t + seg] = x3;
+              if (ls == 0 && seg < kSegs && t < nt) put_end(wends3(m), t, x3);
             } else {
               P3 = wave_scan(x3);
-              if (ls == kSegW - 1 && seg < kSegs && t < nt) wends3(m)[kSegs * t + seg] = P3;
+              if (ls == kSegW - 1 && seg < kSegs && t < nt) put_end(wends3(m), t, P3);
             }
           }
           if (PF && stats) {
@@ -1025,7 +1191,9 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
         const bool last = g + 2 >= ngroups;
         if (m == NM - 1 && last) issue_dma();   // (the unit's last group pair)
         if (EG && last) gather_next();
+        if (gt) gt_patch(1, tb, g + 1, cur.u * 8 + g + 1, (size_t)cur.u * kBlock);
         load_group(m, tb, nt, g + 1, 1);
+        gt_ahead(false, g + 1);
         process_group(g, 0);
         // PF (C2 and its N / out-of-range variants): every load waited for
         // before the next group's are issued, so a wave holds one group in
@@ -1036,13 +1204,17 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
         // ones (profiles/r06_c2_waits_ab.json); the edit, paired-end and
         // window kernels run faster with exact waits (round 5)
         if (PF) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (NM == 1 && LATE) {
+        if (NM == 1 && (LATE || GT)) {
           // edit: ONE load site for slot 0, this unit's next group or the next
           // unit's first, behind the next unit's prologue (round 5: C4 811 ->
           // 806 us; C2, whose else-branch is a plain load, ran 1.5 % slower
           // this way and keeps the if / else)
-          if (last) describe_next();
-          load_group(0, last ? tb ^ 1 : tb, last ? nnt : nt, last ? 0 : g + 2, 0);
+          if (LATE && last) describe_next();
+          const int t0 = last ? tb ^ 1 : tb, g0 = last ? 0 : g + 2;
+          const int u0 = last ? nxt.u : cur.u;
+          if (gt && u0 >= 0) gt_patch(0, t0, g0, u0 * 8 + g0, (size_t)u0 * kBlock);
+          load_group(0, t0, last ? nnt : nt, g0, 0);
+          gt_ahead(last, g0);
         } else if (!last) {
           load_group(m, tb, nt, g + 2, 0);
         } else {
@@ -1050,7 +1222,9 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
         }
         process_group(g + 1, 1);
         // nibbles hold at most 15 steps: widen after groups 0-3 and at the end
-        if (stats && g == 2) acc[m].widen();
+        // (a unit of at most 4 groups -- hex -- only at the end: round 6, the
+        // second widen of zero nibbles was 48 VALU per unit)
+        if (kMidWiden && stats && g == 2) acc[m].widen();
       }
       if (stats) acc[m].widen();
     };
@@ -1070,7 +1244,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       };
       const uint32_t x0 = account(MateTag<0>{}, grp[slot][0], stats, AddTag{}, d2, d3, dsv);
       const uint32_t P0 = wave_scan(x0);
-      if (ls == kSegW - 1 && seg < kSegs && t < nt) wends(0)[kSegs * t + seg] = P0;
+      if (ls == kSegW - 1 && seg < kSegs && t < nt) put_end(wends(0), t, P0);
       const bool pass0 = !dec || read_ok(P0, x0, grp[slot][0].n);   // (only a bool lives on)
       const uint32_t x1 = account(MateTag<m1>{}, grp[slot][m1], stats, AddTag{}, d2, d3, dsv);
       // TDMA: the next unit's windows, issued once this group's loads have been
@@ -1079,7 +1253,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       // would drain it on the spot (vmcnt counts in order)
       if (dma_after) issue_dma();
       const uint32_t P1 = wave_scan(x1);
-      if (ls == kSegW - 1 && seg < kSegs && t < nt) wends(m1)[kSegs * t + seg] = P1;
+      if (ls == kSegW - 1 && seg < kSegs && t < nt) put_end(wends(m1), t, P1);
       if (!dec) return;
       const bool pass = pass0 && read_ok(P1, x1, grp[slot][m1].n);
       if (__builtin_expect(__ballot(!pass) != 0, 0) && !pass) {   // (lanes of a failed pair only)
@@ -1096,7 +1270,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
         if (LATE && last) describe_next();
         load_group_pe(last ? tb ^ 1 : tb, last ? nnt : nt, last ? 0 : g + 2, 0);
         process_pair(g + 1, 1, false);
-        if (stats && ((g + 2) & 7) == 0)   // nibbles hold at most 15 steps
+        if (stats && ((g + 2) & 7) == 0 && g + 2 < ng)   // nibbles hold at most 15 steps (the end widens too)
           for (int m = 0; m < NM; ++m) acc[m].widen();
       }
       if (stats)
@@ -1112,7 +1286,9 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       issue_dma();
       gather_next();
       if (LATE) describe_next();
+      if (gt && nxt.u >= 0) gt_patch(0, tb ^ 1, 0, nxt.u * 8, (size_t)nxt.u * kBlock);
       load_group(0, tb ^ 1, nnt, 0, 0);   // a wholly deferred unit: straight to the next
+      gt_ahead(true, 0);
     }
     since_flush += nt;
 
@@ -1177,10 +1353,11 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
           if (wn > 0) {
             uint32_t bin;
             uint64_t fx;
-            meanq_terms(s, wn, bin, fx);
+            const uint32_t rc = rtab[wn], one1 = wn == 1u ? 1u : 0u;
+            meanq_terms_rc(s, wn, rc, one1, bin, fx);
             atomicAdd(&h[lp + 1 + bin], 1u);
-            atomicAdd(&h[lp + 1 + HPGQ_MEANQ_BINS + (100 * gc) / wn], 1u);
-            atomicAdd(&fxs(m)[lane], (unsigned long long)fx);   // (no return: ds_add_u64)
+            atomicAdd(&h[lp + 1 + HPGQ_MEANQ_BINS + div_len(100 * gc, rc, one1)], 1u);
+            atomicAdd(&fxs(m)[lane & (kFxSlots - 1)], (unsigned long long)fx);   // (no return: ds_add_u64)
           }
         }
       }
@@ -1238,7 +1415,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   for (int m = 0; m < NM; ++m) {
     acc[m].widen();
     acc[m].flush(pos_acc(m), lp, p0);
-    const uint64_t tot = wave_sum64((uint64_t)fxs(m)[lane]);   // (LDS: in order per wave)
+    const uint64_t tot = wave_sum64(lane < kFxSlots ? (uint64_t)fxs(m)[lane] : 0ull);   // (LDS: in order per wave)
     if (lane == 0) {
       unsigned long long *s = sc(m);
       if (cnt_in) atomicAdd(&s[HPGQ_S_NUM_INPUT], (unsigned long long)cnt_in);
