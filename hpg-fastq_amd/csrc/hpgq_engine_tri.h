@@ -44,10 +44,6 @@
 #pragma once
 #include "hpgq_engine_kernel.h"
 
-#ifndef HPGQ_GT_DIST
-#define HPGQ_GT_DIST 0   // GT in tri_body: groups ahead the trim windows are gathered (0: off)
-#endif
-
 namespace hpgq {
 
 constexpr int kTriSlack = 8;    // readable bytes past the data end the loads may touch
@@ -442,13 +438,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   // (edit, follow-up: their registers would spill; the window variant alone
   // fails few reads and ran 4 % slower with it: 692 vs 665 us per 10 M reads)
   constexpr bool PF = NM == 1 && !EDIT && !FOLLOW && XM != X_LR;
-  // GT (single-end edit, first stage, no extra scans; HPGQ_GT_DIST groups
-  // ahead, 0 = off): trims per GROUP, finished right before the group's loads
-  // from windows gathered GTD groups earlier (gt_issue / gt_patch below); the
-  // unit prologue then reads no quality and runs a unit ahead like C2's
-  constexpr int GTD = (EDIT && NM == 1 && !FOLLOW && XM == 0) ? HPGQ_GT_DIST : 0;
-  constexpr bool GT = GTD > 0;
-  constexpr bool LATE = EDIT && !GT;   // the unit prologue's place (see the unit loop)
+  constexpr bool LATE = EDIT;   // the unit prologue's place (see the unit loop)
   constexpr bool TABLEN = !FOLLOW;   // epilogue lengths / trims from the read table
   // PEU (paired-end): a group is ONE step of both mates (grp[slot][m]); both
   // are added, the pair is decided from both scans at once (ds_bpermute), and
@@ -477,7 +467,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   // for.  Round 6, one box, 3 alternating rounds: C4 844 us against 850 (the
   // same at 4 waves per SIMD spilled 7 VGPRs and ran slower, round 5; the
   // extra-scan kernels, c4_noor, ran 2.9 % slower with it and keep 4 waves)
-  constexpr bool EG = EDIT && !FOLLOW && NM == 1 && XM == 0 && !GT;
+  constexpr bool EG = EDIT && !FOLLOW && NM == 1 && XM == 0;
   if (FOLLOW && follow_up_idle(A)) return;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int tid = threadIdx.x;
@@ -663,7 +653,6 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     const ColdParams &cold = cold_all;
     const bool fromdma = TDMA && dma && trim_usual(cold);
     const bool usual = EDIT && (fromdma || (NM == 2 && trim_usual(cold)));
-    const bool grouped = GT && trim_usual(cold);   // (GT: untrimmed here, trimmed per group)
     if (fromdma) {
 #pragma unroll
       for (int m = 0; m < NM; ++m) {
@@ -687,10 +676,8 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       int a = ia[m], e = ie[m];
       tw[m] = 0;
       if (EDIT) {   // trim here, then describe the trimmed window
-        tw[m] = !live || grouped       ? 0u
-                : (usual || pre_ok) ? trim_finish(cold, tl[m], e - a)
-                                    : trim_word(cold, rq[m], bq[m] + a, e - a);
-        if (A.trim && live && !grouped) A.trim[(size_t)m * (size_t)A.num_reads + rid] = tw[m];
+        tw[m] = !live ? 0u : (usual || pre_ok) ? trim_finish(cold, tl[m], e - a) : trim_word(cold, rq[m], bq[m] + a, e - a);
+        if (A.trim && live) A.trim[(size_t)m * (size_t)A.num_reads + rid] = tw[m];
         a += (int)(tw[m] & 0xFFFFu);
         e -= (int)(tw[m] >> 16);
         if (e < a) e = a;
@@ -966,97 +953,14 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     mate(MateTag<0>{});
     if (NM == 2) mate(MateTag<NM - 1>{});
   };
-  // GT (single-end edit, usual windows): the trims of group x's kSegs kU reads
-  // are finished right before the group's loads (gt_patch) from windows
-  // gathered GTD groups earlier (gt_issue) by four lanes per read (lane 4r + p
-  // of the group's read r: p = 0 the first 16 quality bytes, p = 1, 2 the two
-  // halves of the 32 ending at the read's end, p = 3 idle; one b128 each) into
-  // buffer x & 1 (ngroups is even, so the parity runs on across units); the
-  // finished trims patch the group's read-table records.  A group whose
-  // windows were not gathered ahead (the first, and after a unit whose
-  // follower was not described yet) gathers them on the spot (the tag).
-  const bool gt = GT && trim_usual(cold_all);
-  v4u gw[2] = {v4u{0u, 0u, 0u, 0u}, v4u{0u, 0u, 0u, 0u}};
-  int gtag[2] = {-1, -1};   // (uniform) unit * 8 + group whose windows buffer b holds
-  auto gt_issue = [&](int b, int tbx, int grp, int tag) __attribute__((always_inline)) {
-    const int r = lane >> 2, p = lane & 3, idx = kSegs * kU * grp + r;
-    uint32_t addr = 0xC0000000u;   // (out of range: zeros, no traffic)
-    if (p < 3 && r < kSegs * kU && idx < 64) {
-      const v4u rec = *reinterpret_cast<const v4u *>(tab(0, tbx) + 4 * idx);
-      const int n = (int)(rec.z & 0xFFFFu), off = (int)(rec.y | ((rec.z >> 20) & 3u));
-      const int pa = max(off + n - 32, 0);
-      const bool want = p == 0 ? cold_all.e_left_len > 0 : cold_all.e_right_len > 0;
-      if (n > 0 && want && !(rec.y & 0x80000000u)) addr = (uint32_t)(p == 0 ? off : pa + 16 * (p - 1));
-    }
-    gw[b] = __builtin_amdgcn_raw_buffer_load_b128(rq[0], addr, 0, 0);
-    gtag[b] = tag;
-  };
-  auto gt_patch = [&](int b, int tbx, int grp, int tag, size_t ubase) __attribute__((always_inline)) {
-    if (gtag[b] != tag) gt_issue(b, tbx, grp, tag);
-    const int r = lane >> 2, p = lane & 3, idx = kSegs * kU * grp + r;
-    const bool act = r < kSegs * kU && idx < 64;
-    v4u rec = v4u{0x80000000u, 0x80000000u, 0u, 0u};
-    if (act) rec = *reinterpret_cast<const v4u *>(tab(0, tbx) + 4 * idx);
-    const int n = (int)(rec.z & 0xFFFFu), off = (int)(rec.y | ((rec.z >> 20) & 3u));
-    const int pa = max(off + n - 32, 0), hi = off + n - pa;   // hi: 32 but at the buffer's start
-    // this lane's side: the left window's constants on p = 0, the right's else
-    const TrimSide &L = cold_all.tl, &R = cold_all.tr;
-    const bool left = p == 0;
-    const v4u g4 = gw[b];
-    const uint32_t w4[4] = {g4.x, g4.y, g4.z, g4.w};
-    uint32_t ok[4];
-    if (trim_hi_none(L) && trim_hi_none(R)) {
-      const TrimSide S{left ? L.lq : R.lq, left ? L.l7 : R.l7, 0u, kQFlip};
-#pragma unroll
-      for (int k = 0; k < 4; ++k) ok[k] = trim_side_ok<true>(w4[k], S);
-    } else {
-      const TrimSide S{left ? L.lq : R.lq, left ? L.l7 : R.l7, left ? L.hq : R.hq, left ? L.h7 : R.h7};
-#pragma unroll
-      for (int k = 0; k < 4; ++k) ok[k] = trim_side_ok<false>(w4[k], S);
-    }
-    int v;
-    if (left) {   // first in-range index (large when none)
-      uint32_t f = ~0u;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) f = min(f, (ffbl_raw(ok[k]) >> 3) + 4u * k);
-      v = (int)min(f, 0x3FFFFFFFu);
-    } else {      // last in-range index of the 32-byte tail (negative when none)
-      const int bo = 16 * (p - 1);
-      if (__builtin_expect(hi < 32, 0)) {   // a read at the buffer's start: bytes >= hi are the next read's
-#pragma unroll
-        for (int k = 0; k < 4; ++k) ok[k] &= byte_mask(hi - bo - 4 * k);
-      }
-      v = -1;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) v = max(v, bo + 4 * k + 3 - (int)(ffbh_raw(ok[k]) >> 3));
-    }
-    const int v1 = __builtin_amdgcn_mov_dpp(v, 0x55, 0xF, 0xF, false);   // quad lane 1
-    const int v2 = __builtin_amdgcn_mov_dpp(v, 0xAA, 0xF, 0xF, false);   // quad lane 2
-    const bool live = act && !(rec.y & 0x80000000u);
-    if (left && live) {
-      const int ts = min(v, min(cold_all.e_left_len, n));
-      const int te = max(min(min(cold_all.e_right_len, n - ts), hi - 1 - max(v1, v2)), 0);
-      const uint32_t t = (uint32_t)ts | ((uint32_t)te << 16);
-      if (t) {
-        const uint32_t xs = (rec.x | ((rec.z >> 16) & 3u)) + (uint32_t)ts;
-        const uint32_t xq = (uint32_t)off + (uint32_t)ts, nn = (uint32_t)(n - ts - te);
-        *reinterpret_cast<v4u *>(tab(0, tbx) + 4 * idx) =
-            v4u{xs & ~3u, xq & ~3u, nn | ((xs & 3u) << 16) | ((xq & 3u) << 20), t};
-      }
-      if (A.trim) A.trim[ubase + (size_t)idx] = t;
-    }
-    __builtin_amdgcn_wave_barrier();   // (the group's loads read the records: LDS is in order per wave)
-  };
   auto ngroups_of = [&](int nts) __attribute__((always_inline)) { return ((nts + kU - 1) / kU + 1) & ~1; };
   if (cur.u >= 0) {
     fetch_idx(cur, ia, ie);
     load_block(cur, tb, len, tw, dm, ia, ie, false);
     nxt = it.next();
     fetch_idx(nxt, ia, ie);
-    if (gt) gt_patch(0, tb, 0, cur.u * 8, (size_t)cur.u * kBlock);
     if (PEU) load_group_pe(tb, steps_of(cur, dm), 0, 0);
     else load_group(0, tb, steps_of(cur, dm), 0, 0);
-    if (gt && GTD < ngroups_of(steps_of(cur, dm))) gt_issue(GTD & 1, tb, GTD, cur.u * 8 + GTD);
   }
   constexpr uint64_t not_seg_first = not_seg_first_mask<G>();   // lanes j with j % kSegs != 0
   while (cur.u >= 0) {
@@ -1104,20 +1008,6 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     // an even number of groups per mate, so every mate (and unit) starts in
     // slot 0 (the padding group gathers length-0 reads)
     const int ngroups = ngroups_of(nt);
-    // GT: the windows of the group GTD after group x of this unit (nx false)
-    // or of the next one (nx true); past the next unit nothing is described yet
-    auto gt_ahead = [&](bool nx, int x) __attribute__((always_inline)) {
-      if (!gt) return;
-      int y = x + GTD;
-      if (!nx) {
-        if (y < ngroups) {
-          gt_issue(y & 1, tb, y, cur.u * 8 + y);
-          return;
-        }
-        y -= ngroups;
-      }
-      if (nxt.u >= 0 && y < ngroups_of(nnt)) gt_issue(y & 1, tb ^ 1, y, nxt.u * 8 + y);
-    };
 
     auto run_mate = [&](auto mtag) __attribute__((always_inline)) {
       constexpr int m = decltype(mtag)::value;
@@ -1191,9 +1081,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
         const bool last = g + 2 >= ngroups;
         if (m == NM - 1 && last) issue_dma();   // (the unit's last group pair)
         if (EG && last) gather_next();
-        if (gt) gt_patch(1, tb, g + 1, cur.u * 8 + g + 1, (size_t)cur.u * kBlock);
         load_group(m, tb, nt, g + 1, 1);
-        gt_ahead(false, g + 1);
         process_group(g, 0);
         // PF (C2 and its N / out-of-range variants): every load waited for
         // before the next group's are issued, so a wave holds one group in
@@ -1204,17 +1092,13 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
         // ones (profiles/r06_c2_waits_ab.json); the edit, paired-end and
         // window kernels run faster with exact waits (round 5)
         if (PF) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (NM == 1 && (LATE || GT)) {
+        if (NM == 1 && LATE) {
           // edit: ONE load site for slot 0, this unit's next group or the next
           // unit's first, behind the next unit's prologue (round 5: C4 811 ->
           // 806 us; C2, whose else-branch is a plain load, ran 1.5 % slower
           // this way and keeps the if / else)
-          if (LATE && last) describe_next();
-          const int t0 = last ? tb ^ 1 : tb, g0 = last ? 0 : g + 2;
-          const int u0 = last ? nxt.u : cur.u;
-          if (gt && u0 >= 0) gt_patch(0, t0, g0, u0 * 8 + g0, (size_t)u0 * kBlock);
-          load_group(0, t0, last ? nnt : nt, g0, 0);
-          gt_ahead(last, g0);
+          if (last) describe_next();
+          load_group(0, last ? tb ^ 1 : tb, last ? nnt : nt, last ? 0 : g + 2, 0);
         } else if (!last) {
           load_group(m, tb, nt, g + 2, 0);
         } else {
@@ -1286,9 +1170,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       issue_dma();
       gather_next();
       if (LATE) describe_next();
-      if (gt && nxt.u >= 0) gt_patch(0, tb ^ 1, 0, nxt.u * 8, (size_t)nxt.u * kBlock);
       load_group(0, tb ^ 1, nnt, 0, 0);   // a wholly deferred unit: straight to the next
-      gt_ahead(true, 0);
     }
     since_flush += nt;
 
