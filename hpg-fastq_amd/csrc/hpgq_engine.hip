@@ -254,9 +254,10 @@ static size_t seg_lds(const hpgq_params_t &p, int nm, int xm, int pos, bool foll
   // unit's trim windows, 3 x block x 16 B per mate, tri_body TDMA)
   const bool tdma = p.edit_on && !follow && nm == 2 && xm == 0;
   const size_t dma_words = tdma ? (size_t)nm * 3 * (size_t)block * 4 : 0;
+  const size_t st_words = (xm & hpgq::X_ST) ? (size_t)hpgq::kStWords : 0;   // (tri_body ST's shift buffers)
   // (after the byte-mask table: the reciprocal table [pos + 1] of the epilogue's divisions)
   return (size_t)nm * mate_words * 4 + 16 + 17 * 16 + ((size_t)pos + 1) * 4 +
-         (size_t)hpgq::kWaves * ((size_t)nm * (2 * 256 + 64 * lists + hpgq::kFxWords) + 64 + 4 + dma_words) * 4;
+         (size_t)hpgq::kWaves * ((size_t)nm * (2 * 256 + 64 * lists + hpgq::kFxWords) + 64 + 4 + dma_words + st_words) * 4;
 }
 
 static size_t catch_all_lds(const hpgq_params_t &p, int nm) {
@@ -326,12 +327,22 @@ static int plan_chain(hpgq_ctx *c, Chain &ch, int cus, int geo_force) {
   int geo = (stats && p.lmax > hpgq::Geo<hpgq::GEO_HEX>::kPos && p.lmax <= posw) ? hpgq::GEO_WIDE
                                                                                  : hpgq::GEO_HEX;
   if (geo_force >= 0) geo = geo_force;
-  if (!seg_stage(ch.s1, geo, c->nm, edit, xm, false)) return HPGQ_E_INVALID;
+  // single-end edit on hex with the usual trim windows and a left length <= 12
+  // (every shift fits one lane's bytes and its neighbour's): the trims are
+  // applied at the step (tri_body ST), so no load waits for them
+#ifndef HPGQ_NO_ST
+  const bool st = edit && c->nm == 1 && xm == 0 && geo == hpgq::GEO_HEX && p.edit_left_length <= 12 &&
+                  p.edit_right_length <= 32;
+#else
+  const bool st = false;   // (A/B builds: the unit-prologue trims)
+#endif
+  const int xm1 = st ? hpgq::X_ST : xm;
+  if (!seg_stage(ch.s1, geo, c->nm, edit, xm1, false)) return HPGQ_E_INVALID;
   const int pos1 = seg_pos(geo);
   // a merged read longer than lmax leaves the segmented kernels (the
   // catch-all counts it as a long read)
   ch.s1.defer_len = stats ? std::min(pos1, p.lmax) : pos1;
-  int rc = finish_stage(c, ch.s1, seg_lds(p, c->nm, xm, pos1, false, seg_block(geo)), cus);
+  int rc = finish_stage(c, ch.s1, seg_lds(p, c->nm, xm1, pos1, false, seg_block(geo)), cus);
   if (rc) return rc;
   ch.has2 = geo != hpgq::GEO_WIDE && ch.s1.defer_len < posw && !(stats && p.lmax <= pos1);
   if (ch.has2) {

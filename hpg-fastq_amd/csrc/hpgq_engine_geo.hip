@@ -4,7 +4,7 @@
 // which the variant's registers fit without spills: single-end 4 (tri 5),
 // paired-end 3 (two mates' accumulators), single-end edit 3 (its next trim
 // windows held in VGPRs, tri_body EG; 4 with the extra scans or as a
-// follow-up), see DESIGN.md §4.1.  Every
+// follow-up; 4 with the trims at the step, tri_body ST), see DESIGN.md §4.1.  Every
 // combination of paired-end, edit and the extra filter scans has an instance.
 #include <cstdio>
 
@@ -32,6 +32,11 @@ constexpr int kPeW = HPGQ_PE_WAVES;          // paired-end
 #endif
 constexpr int kEdW = HPGQ_EDIT_WAVES;        // single-end edit (its trim windows in VGPRs a group early: tri_body EG)
 constexpr int kEdXW = kSeW;                  // single-end edit with extra filter scans
+#ifndef HPGQ_ST_WAVES
+#define HPGQ_ST_WAVES 4
+#endif
+constexpr int kStW = HPGQ_ST_WAVES;          // single-end edit, trims at the step (tri_body ST; its 7
+                                             // spilled VGPRs sit outside the group loop)
 constexpr const char *kGeoName = G == GEO_TRI ? "tri" : (G == GEO_HEX ? "hex" : "wide");
 
 template <bool F, int XM, bool EDIT>
@@ -49,6 +54,13 @@ const void *x_kernel_for(int nm, int xm) {
 template <bool F>
 SegChoice pick(int nm, bool edit, int xm, char *name, size_t cap) {
   const void *fn = nullptr;
+  if (xm == X_ST) {   // single-end edit with the trims applied at the step (hex, first stage: tri_body ST)
+    if constexpr (G == GEO_HEX && !F) {
+      if (nm == 1 && edit) fn = (const void *)engine_tri_x_kernel<kStW, 1, G, false, X_ST, true>;
+    }
+    std::snprintf(name, cap, "hpgq::engine_tri_kernel<%d, 1, edit, %s, st>", kStW, kGeoName);
+    return SegChoice{fn, kStW};
+  }
   const int w = nm == 2 ? kPeW : (edit ? (xm || F ? kEdXW : kEdW) : kSeW);
   if (xm) {
     fn = edit ? x_kernel_for<F, true>(nm, xm) : x_kernel_for<F, false>(nm, xm);

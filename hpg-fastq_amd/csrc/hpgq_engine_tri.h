@@ -64,6 +64,10 @@ constexpr int kFxWords = 2 * kFxSlots;   // per wave and mate: kFxSlots u64
 
 constexpr int GEO_TRI = 0, GEO_HEX = 1, GEO_WIDE = 2;
 constexpr int X_NOOR = 1, X_LR = 2;   // extra filter scans (engine_tri_x_kernel)
+constexpr int X_ST = 4;               // single-end edit, trims applied at the step (tri_body ST)
+// ST: per wave, the step's raw seq and quality dwords of every lane (64 x 16 B
+// each, + 32 B read past the last lane), read back from a per-lane byte offset
+constexpr int kStWords = 2 * (64 * 4 + 8);
 
 // kBlock reads (<= 64: lane j <-> read j in the epilogue) in steps of kSegs
 // reads, kU steps per pipeline group, an even number of groups per block.
@@ -438,7 +442,18 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   // (edit, follow-up: their registers would spill; the window variant alone
   // fails few reads and ran 4 % slower with it: 692 vs 665 us per 10 M reads)
   constexpr bool PF = NM == 1 && !EDIT && !FOLLOW && XM != X_LR;
-  constexpr bool LATE = EDIT;   // the unit prologue's place (see the unit loop)
+  // ST (single-end edit, hex, first stage, usual windows with a left length <=
+  // 12 -- the host picks it, plan_chain): the stream loads each read
+  // UNTRIMMED, so no load waits for a trim; the group's trim windows are
+  // gathered right after its stream loads (the same lines: no re-fetch) and
+  // the trims are finished when the group is counted, each step shifting its
+  // reads' bytes by their ts (a register shuffle, only in steps holding a
+  // read with ts > 0) and counting n - ts - te of them; the finished trims
+  // patch the read table for the unit epilogue (lengths, trim words, the
+  // failed reads' re-gather).  See st_trims.
+  constexpr bool ST = (XM & X_ST) != 0;
+  static_assert(!ST || (XM == X_ST && NM == 1 && EDIT && !FOLLOW && G == GEO_HEX), "ST: single-end edit, hex");
+  constexpr bool LATE = EDIT && !ST;   // the unit prologue's place (see the unit loop)
   constexpr bool TABLEN = !FOLLOW;   // epilogue lengths / trims from the read table
   // PEU (paired-end): a group is ONE step of both mates (grp[slot][m]); both
   // are added, the pair is decided from both scans at once (ds_bpermute), and
@@ -537,9 +552,13 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   // TDMA: the next unit's trim windows, DMA'd one unit ahead (see dma_windows):
   // per mate three rows (left, right 0, right 1) of kBlock x 16 B
   constexpr int kDmaWords = TDMA ? NM * 3 * kBlock * 4 : 0;
-  constexpr int kWaveWords = NM * kMateWaveWords + 64 + 4 + NM * kFxWords + kDmaWords;   // (multiple of 4: 16 B tables)
+  constexpr int kWaveWords = NM * kMateWaveWords + 64 + 4 + NM * kFxWords + kDmaWords +
+                             (ST ? kStWords : 0);   // (multiple of 4: 16 B tables)
   const int tab_words = (NM * mate_words + 3) & ~3;   // 16 B aligned (host: + 16 B)
-  uint32_t *wtab = base + tab_words + wave * kWaveWords;
+  // (ST: the shift buffers first in the wave's region, so their reads' offsets
+  // fit the ds_read2 offset fields)
+  uint32_t *wst = base + tab_words + wave * kWaveWords;
+  uint32_t *wtab = wst + (ST ? kStWords : 0);
   auto tab = [&](int m, int tb) __attribute__((always_inline)) { return wtab + m * kMateWaveWords + tb * 256; };
   auto wends = [&](int m) __attribute__((always_inline)) { return wtab + m * kMateWaveWords + 2 * 256; };
   auto wends2 = [&](int m) __attribute__((always_inline)) { return wtab + m * kMateWaveWords + 2 * 256 + 64; };   // NX only
@@ -553,6 +572,10 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     return scratch + 64 + 4 + NM * kFxWords + (m * 3 + w) * kBlock * 4;
   };
   // per-lane exact mean-quality sums, 8 B aligned
+  // ST: the wave's shift buffers (b = 0 seq, 1 quality; 16 B aligned)
+  auto stbuf = [&](int b) __attribute__((always_inline)) {
+    return wst + b * (kStWords / 2);
+  };
   auto fxs = [&](int m) __attribute__((always_inline)) {
     return reinterpret_cast<unsigned long long *>(scratch + 64 + 4 + m * kFxWords);
   };
@@ -670,14 +693,15 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
         tl[m] = trim_issue(cold, rq[m], live ? bq[m] + ia[m] : (int)0xC0000000, ie[m] - ia[m]);
     }
     const bool pre_ok = EG && pre != nullptr && trim_usual(cold);   // EG: issued by gather_next
+    // (ST: described untrimmed; the group's trims patch the records later)
     if (pre_ok) tl[0] = *pre;
 #pragma unroll
     for (int m = 0; m < NM; ++m) {
       int a = ia[m], e = ie[m];
       tw[m] = 0;
       if (EDIT) {   // trim here, then describe the trimmed window
-        tw[m] = !live ? 0u : (usual || pre_ok) ? trim_finish(cold, tl[m], e - a) : trim_word(cold, rq[m], bq[m] + a, e - a);
-        if (A.trim && live) A.trim[(size_t)m * (size_t)A.num_reads + rid] = tw[m];
+        tw[m] = !live || ST ? 0u : (usual || pre_ok) ? trim_finish(cold, tl[m], e - a) : trim_word(cold, rq[m], bq[m] + a, e - a);
+        if (A.trim && live && !ST) A.trim[(size_t)m * (size_t)A.num_reads + rid] = tw[m];
         a += (int)(tw[m] & 0xFFFFu);
         e -= (int)(tw[m] >> 16);
         if (e < a) e = a;
@@ -739,13 +763,104 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   };
 
   TriPending<NW> grp[2][kU];
-  // issue group g (kU steps) of mate m; steps past the unit end gather
-  // lane 63 (length 0: never a read of the unit), so they add nothing
+  // ST: the trim windows of a group PAIR (g, g + 1: the unit's reads 12 g ..
+  // 12 g + 23), two lanes per read (lane 2r + h): h = 0 the first 16 quality
+  // bytes (w0) and the first half of the 32 ending at the read's end (w1),
+  // h = 1 its second half (w0)
+  v4u stw0 = v4u{0u, 0u, 0u, 0u}, stw1 = v4u{0u, 0u, 0u, 0u};
+  // issue group g (kU steps) of mate m; steps past the unit end gather an
+  // entry no read fills (step_off), so they add nothing
   auto load_group = [&](int m, int tb, int nt, int g, int slot) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < kU; ++u) {
       gather_at(m, tb, step_off(g * kU + u, nt), grp[slot][u]);
     }
+    if (ST && slot == 0) {   // (the pair's windows, after group g's stream loads: the same lines)
+      const int r = lane >> 1, h = lane & 1, idx = kSegs * kU * g + r;
+      uint32_t a0 = 0xC0000000u, a1 = 0xC0000000u;   // (out of range: zeros, no traffic)
+      if (r < 2 * kSegs * kU && g * kU < nt) {
+        const v4u rec = *reinterpret_cast<const v4u *>(tab(0, tb) + 4 * idx);
+        const int n = (int)(rec.z & 0xFFFFu), off = (int)(rec.y | ((rec.z >> 20) & 3u));
+        const int pa = max(off + n - 32, 0);
+        if (n > 0 && !(rec.y & 0x80000000u)) {
+          if (h == 0) {
+            if (cold_all.e_left_len > 0) a0 = (uint32_t)off;
+            if (cold_all.e_right_len > 0) a1 = (uint32_t)pa;
+          } else if (cold_all.e_right_len > 0) {
+            a0 = (uint32_t)(pa + 16);
+          }
+        }
+      }
+      stw0 = __builtin_amdgcn_raw_buffer_load_b128(rq[0], a0, 0, 0);
+      stw1 = __builtin_amdgcn_raw_buffer_load_b128(rq[0], a1, 0, 0);
+    }
+  };
+  // ST: the trims of the group pair from g (even, unit ubase); lane 2r returns
+  // read r's ts | te << 16 (0 for a read without one or not live) and patches
+  // its read-table record to the trimmed window (offsets + ts, length n - ts -
+  // te, the trim word) -- after the groups' loads took the untrimmed records.
+  // trim_finish's arithmetic over two lanes per read (the right window's
+  // halves combined by one DPP).
+  auto st_trims = [&](int tbx, int g, size_t ubase) __attribute__((always_inline)) -> uint32_t {
+    const int r = lane >> 1, h = lane & 1, idx = kSegs * kU * g + r;
+    const bool act = r < 2 * kSegs * kU;
+    v4u rec = v4u{0x80000000u, 0x80000000u, 0u, 0u};
+    if (act) rec = *reinterpret_cast<const v4u *>(tab(0, tbx) + 4 * idx);
+    const int n = (int)(rec.z & 0xFFFFu), off = (int)(rec.y | ((rec.z >> 20) & 3u));
+    const int pa = max(off + n - 32, 0), hi = off + n - pa;   // hi: 32 but at the buffer's start
+    const TrimSide &L = cold_all.tl, &R = cold_all.tr;
+    const uint32_t a[4] = {stw0.x, stw0.y, stw0.z, stw0.w}, b[4] = {stw1.x, stw1.y, stw1.z, stw1.w};
+    uint32_t oka[4], okb[4];   // w0 on the lane's side (h = 0 left, 1 right), w1 right
+    if (trim_hi_none(L) && trim_hi_none(R)) {
+      const TrimSide S{h ? R.lq : L.lq, h ? R.l7 : L.l7, 0u, kQFlip};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        oka[k] = trim_side_ok<true>(a[k], S);
+        okb[k] = trim_side_ok<true>(b[k], R);
+      }
+    } else {
+      const TrimSide S{h ? R.lq : L.lq, h ? R.l7 : L.l7, h ? R.hq : L.hq, h ? R.h7 : L.h7};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        oka[k] = trim_side_ok<false>(a[k], S);
+        okb[k] = trim_side_ok<false>(b[k], R);
+      }
+    }
+    if (__builtin_expect(hi < 32, 0)) {   // a read at the buffer's start: bytes >= hi are the next read's
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        okb[k] &= byte_mask(hi - 4 * k);        // (h = 0: tail bytes 0..15)
+        if (h) oka[k] &= byte_mask(hi - 16 - 4 * k);   // (h = 1: tail bytes 16..31)
+      }
+    }
+    // h = 0: first in-range index of the left window; both: last in-range
+    // index of their tail half (h = 1's from w0, at +16; negative when none)
+    uint32_t f = ~0u;
+    int vr = -1;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t x = h ? 0u : oka[k];
+      f = min(f, (ffbl_raw(x) >> 3) + 4u * k);
+      const uint32_t y = h ? oka[k] : okb[k];
+      vr = max(vr, 4 * k + 3 - (int)(ffbh_raw(y) >> 3));
+    }
+    if (h && vr >= 0) vr += 16;
+    const int vr1 = __builtin_amdgcn_mov_dpp(vr, 0xF5, 0xF, 0xF, false);   // quad_perm [1,1,3,3]: lane 2r + 1
+    const bool live = act && !(rec.y & 0x80000000u);
+    uint32_t t = 0;
+    if (h == 0 && live) {
+      const int ts = min((int)min(f, 0x3FFFFFFFu), min(cold_all.e_left_len, n));
+      const int te = max(min(min(cold_all.e_right_len, n - ts), hi - 1 - max(vr, vr1)), 0);
+      t = (uint32_t)ts | ((uint32_t)te << 16);
+      if (t) {
+        const uint32_t xs = (rec.x | ((rec.z >> 16) & 3u)) + (uint32_t)ts;
+        const uint32_t xq = (uint32_t)off + (uint32_t)ts, nn = (uint32_t)(n - ts - te);
+        *reinterpret_cast<v4u *>(tab(0, tbx) + 4 * idx) =
+            v4u{xs & ~3u, xq & ~3u, nn | ((xs & 3u) << 16) | ((xq & 3u) << 20), t};
+      }
+      if (A.trim) A.trim[ubase + (size_t)idx] = t;
+    }
+    return t;
   };
 
   // PEU: group g = step g of both mates
@@ -777,13 +892,42 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
   // or removes (SUB = true) the lane's positions from mate m's counters
   // (count = false: sums only, the values left in sv); NX: x2 = N |
   // out-of-range << 16; LR: x3 = left | right window sums
+  // (trim, ST only: the read's ts | te << 16 -- its bytes start ts later and
+  // it counts n - ts - te of them)
   auto account = [&](auto mtag, const TriPending<NW> &pd, bool count, auto sub_tag, uint32_t &x2,
-                     uint32_t &x3, StepVals &sv) __attribute__((always_inline)) -> uint32_t {
+                     uint32_t &x3, StepVals &sv, uint32_t trim = 0u) __attribute__((always_inline)) -> uint32_t {
     constexpr int m = decltype(mtag)::value;
     constexpr bool SUB = decltype(sub_tag)::value != 0, UNDO = decltype(sub_tag)::value == 2;
     uint32_t sw[NW], qw[NW];
-    {   // realign: word w = bytes [al, al+4) of raw words w, w+1 (the last from lane+1)
-      const uint32_t als = (pd.n >> 16) & 3u, alq = (pd.n >> 20) & 3u;
+    const uint32_t als = (pd.n >> 16) & 3u, alq = (pd.n >> 20) & 3u;
+    int nlen = (int)(pd.n & 0xFFFFu);
+    const uint32_t ts = ST ? trim & 0xFFFFu : 0u;
+    if (ST) nlen = max(nlen - (int)ts - (int)(trim >> 16), 0);
+    if (ST && __builtin_expect(__ballot(ts != 0u) != 0, 1)) {
+      // the lane's bytes start al + ts bytes into its raw words (the rest from
+      // lane + 1's): every lane's raw words go to the wave's LDS buffer and
+      // come back from that byte offset -- as cheap in VALU as the DPP realign
+      // (register shuffles by a per-lane whole-dword count cost 44 VALU per
+      // step and were needed in most steps)
+      auto via_lds = [&](uint32_t *buf, const uint32_t (&r)[NW], uint32_t S, uint32_t (&out)[NW])
+                         __attribute__((always_inline)) {
+        // (the memory clobbers: lane + 1's words are written by ANOTHER lane, so
+        // hipcc, reasoning per lane, would hoist the read of them above the
+        // write -- or sink a read below the next step's write; LDS itself runs
+        // a wave's operations in order)
+        *reinterpret_cast<v4u *>(buf + 4 * lane) = v4u{r[0], r[1], r[2], r[3]};
+        asm volatile("" ::: "memory");
+        const uint32_t *src = buf + 4 * lane + (S >> 2);
+        uint32_t d[NW + 1];
+#pragma unroll
+        for (int k = 0; k <= NW; ++k) d[k] = src[k];
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int w = 0; w < NW; ++w) out[w] = __builtin_amdgcn_alignbyte(d[w + 1], d[w], S & 3u);
+      };
+      via_lds(stbuf(0), pd.s, als + ts, sw);
+      via_lds(stbuf(1), pd.q, alq + ts, qw);
+    } else {   // realign: word w = bytes [al, al+4) of raw words w, w+1 (the last from lane+1)
       const uint32_t ns = next_lane0(pd.s[0]), nq = next_lane0(pd.q[0]);
 #pragma unroll
       for (int w = 0; w < NW; ++w) {
@@ -792,7 +936,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
       }
     }
     uint32_t mk[NW];
-    mask_row((int)(pd.n & 0xFFFFu) - p0, mk);
+    mask_row(nlen - p0, mk);
     uint32_t qm[NW], cd[NW];
     uint32_t bad = 0;
 #pragma unroll
@@ -1009,17 +1153,29 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     // slot 0 (the padding group gathers length-0 reads)
     const int ngroups = ngroups_of(nt);
 
+    uint32_t st_t = 0;   // ST: lane 2r: the current group pair's read r's trims
     auto run_mate = [&](auto mtag) __attribute__((always_inline)) {
       constexpr int m = decltype(mtag)::value;
       auto process_group = [&](int g, int slot) __attribute__((always_inline)) {
+        // ST: the pair's trims when its first group is counted (st_t lives on
+        // to the second)
+        if (ST && slot == 0) {
+          st_t = g * kU < nt ? st_trims(tb, g, (size_t)cur.u * kBlock) : 0u;
+          __builtin_amdgcn_wave_barrier();   // (the patched records: LDS is in order per wave)
+        }
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
           const int t = g * kU + u;
           uint32_t x2 = 0, x3 = 0;
           StepVals sv;
+          // ST: this lane's read's trim, from lane 4r of its group's read r
+          const uint32_t trim =
+              ST ? (uint32_t)__builtin_amdgcn_ds_bpermute(8 * (kSegs * kU * slot + kSegs * u + min(seg, kSegs - 1)),
+                                                          (int)st_t)
+                 : 0u;
           // PF: sums first, the decision, then only passing reads are added;
           // else every read is added and failed ones are taken out in the unit epilogue
-          const uint32_t x = account(MateTag<m>{}, grp[slot][u], stats && !PF, AddTag{}, x2, x3, sv);
+          const uint32_t x = account(MateTag<m>{}, grp[slot][u], stats && !PF, AddTag{}, x2, x3, sv, trim);
           const uint32_t P = wave_scan(x);
           // segment ends (the last lane of each segment) -> wends[kSegs t + seg], no wait needed
           if (ls == kSegW - 1 && seg < kSegs && t < nt) put_end(wends(m), t, P);
