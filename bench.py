@@ -344,8 +344,18 @@ def cpu_baseline(args, params):
                      f"{args.seed}, same generator and options), {done // n} passes in "
                      f"{el:.1f} s; {what}, {threads} OpenMP threads (this GPU's CPU share; "
                      f"{ncores} visible); value_1thread: one pass on 1 thread ({el1:.1f} s); "
-                     f"value_allcores: the same on all {ncores} visible cores{c1}")
+                     f"value_allcores: the same on all {ncores} visible cores"
+                     f"{allcores_note(out.get('cpu_quota_cores'), ncores)}{c1}")
     return out
+
+
+def allcores_note(quota, ncores):
+    """A cgroup CPU quota below the visible cores makes the all-core run
+    time-share that many CPUs: say so beside the number."""
+    if quota and quota < ncores:
+        return (f" (the job's cgroup quota is {quota:g} CPUs, so the {ncores} threads time-share "
+                f"them: the host's {ncores}-core rate is not measurable from this job)")
+    return ""
 
 
 def refarch_baseline(lib, params, batch, n, budget):
