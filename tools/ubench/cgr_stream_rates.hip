@@ -99,14 +99,21 @@ static void run(const char *a, const char *b, uint32_t *out, int grid, int work)
   hipEventDestroy(e1);
 }
 
-int main() {
+int main(int argc, char **argv) {
   char *a, *b;
   uint32_t *out;
   if (hipMalloc(&a, kN + 4096) || hipMalloc(&b, kN + 4096) || hipMalloc(&out, 4096 * kWG * 4)) return 1;
   hipMemset(a, 0x41, kN);
   hipMemset(b, 0x28, kN);
   hipDeviceSynchronize();
-  for (int work : {0, 80, 165, 250}) {
+  // work values (dependent VALU pairs per lane and tile) from the command line
+  // (round 6: pricing VALU cuts per byte for C5)
+  std::vector<int> works = {0, 80, 165, 250};
+  if (argc > 1) {
+    works.clear();
+    for (int i = 1; i < argc; ++i) works.push_back(atoi(argv[i]));
+  }
+  for (int work : works) {
     run<1, true>(a, b, out, 256, work);
     run<2, true>(a, b, out, 256, work);
     run<3, true>(a, b, out, 256, work);
