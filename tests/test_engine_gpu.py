@@ -475,20 +475,25 @@ def test_edit_filters_route_to_segmented_kernel(name, paired, geo_choice):
     assert c[H.S_NUM_EDITED] > 0 and c[H.S_NUM_FAILED] > 0
 
 
+@pytest.mark.parametrize("paired", [0, 1])
 @pytest.mark.parametrize("left", [1, 7, 12, 13])
-def test_edit_trims_at_the_step(left, geo_choice):
+def test_edit_trims_at_the_step(left, paired, geo_choice):
     """Single-end edit on hex with a left length <= 12 and a right one <= 32
-    (C4's shape) applies the trims at the step (tri_body ST: the stream loads
+    (C4's shape; paired-end the same trims on the TDMA kernel) applies the trims at the step (tri_body ST: the stream loads
     the untrimmed read, each step shifts its reads by al + ts <= 15 bytes
     through the wave's LDS buffer); 13 and the other geometries take the
     prologue trims.  Low left qualities make most steps shift; a bounded
     right range takes the five-VALU compare; exact against the oracle."""
     p = H.edit_params(lmax=150, stats=True, left_length=left, left_quality_range="30,",
-                      right_length=32, right_quality_range="25,38")
-    with H.Engine(p) as e:
-        assert (", st>" in e.kernel_name) == (left <= 12 and geo_choice == "auto"), e.kernel_chain
-    r = O.synth(200_000, seed=31, L=150, trunc_pct=15, n_per_1024=8)
-    c = assert_same(p, r)
+                      right_length=32, right_quality_range="25,38",
+                      **(dict(read_quality_range="24,") if paired else {}))
+    p.paired = paired
+    with H.Engine(p) as e:   # (paired-end keeps the prologue trims: tools/probes/pe_st.patch)
+        assert (", st>" in e.kernel_name) == (left <= 12 and geo_choice == "auto" and not paired), e.kernel_chain
+    n = 100_000 if paired else 200_000
+    r1 = O.synth(n, seed=31, L=150, trunc_pct=15, n_per_1024=8, mate=0)
+    r2 = O.synth(n, seed=31, L=150, trunc_pct=15, n_per_1024=8, mate=1) if paired else None
+    c = assert_same(p, r1, r2)
     assert c[H.S_NUM_EDITED] > 0
 
 
