@@ -839,8 +839,7 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     int vr = -1;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const uint32_t x = h ? 0u : oka[k];
-      f = min(f, (ffbl_raw(x) >> 3) + 4u * k);
+      f = min(f, (ffbl_raw(oka[k]) >> 3) + 4u * k);   // (h = 1: unused)
       const uint32_t y = h ? oka[k] : okb[k];
       vr = max(vr, 4 * k + 3 - (int)(ffbh_raw(y) >> 3));
     }
@@ -902,7 +901,9 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     const uint32_t als = (pd.n >> 16) & 3u, alq = (pd.n >> 20) & 3u;
     int nlen = (int)(pd.n & 0xFFFFu);
     const uint32_t ts = ST ? trim & 0xFFFFu : 0u;
-    if (ST) nlen = max(nlen - (int)ts - (int)(trim >> 16), 0);
+    // (no clamp: te <= n - ts for a read, and a lane without one masks all
+    // its bytes whatever the count -- mask_row clamps)
+    if (ST) nlen -= (int)ts + (int)(trim >> 16);
     if (ST && __builtin_expect(__ballot(ts != 0u) != 0, 1)) {
       // the lane's bytes start al + ts bytes into its raw words (the rest from
       // lane + 1's): every lane's raw words go to the wave's LDS buffer and
