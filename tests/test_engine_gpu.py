@@ -100,11 +100,15 @@ def test_edit_trim_stats(geo_choice):
     assert c[H.S_NUM_EDITED] > 0
 
 
-@pytest.mark.parametrize("left,right", [(1, 1), (8, 31), (16, 32), (17, 33), (16, 0), (0, 32)])
+@pytest.mark.parametrize("left,right", [(1, 1), (8, 31), (12, 32), (16, 32), (17, 33), (16, 0), (0, 32)])
 def test_edit_window_sizes(left, right, geo_choice):
     """The trim at the window sizes where the kernel switches from one batch of
-    loads (left <= 16, right <= 32) to the 8-byte loop, on reads as short as 0."""
+    loads (left <= 16, right <= 32) to the 8-byte loop, and (left <= 12) to the
+    trims at the step, on reads as short as 0 -- the batch's first read 20
+    bytes long, so its right window would begin before the buffer."""
     reads = O.synth(12000, seed=40 + left + right, L=150, trunc_pct=60)
+    lowhi = bytes([33 + 5] * 7 + [33 + 30] * 6 + [33 + 8] * 7)
+    reads = O.Reads.from_pairs([(b"ACGTN" * 4, lowhi)] + reads.pairs())
     kw = {}
     if left:
         kw.update(left_length=left, left_quality_range="22,")
