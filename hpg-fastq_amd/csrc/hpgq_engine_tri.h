@@ -723,16 +723,22 @@ __device__ __forceinline__ void tri_body(const EngineArgs &A) {
     return __builtin_popcountll(dm) == U.nr ? 0 : (U.nr + kSegs - 1) / kSegs;
   };
   // lane -> its segment's read (the entry `eoff` bytes into mate m's read table tb)
+  // the stream loads' cache policy: non-temporal (nt) for the PF kernels (C2
+  // and its N / out-of-range variants: round 6, one box, 3 alternating rounds,
+  // C2 528.6 -> 523.5 us); the others re-read lines the stream brought in
+  // (trim windows, step-boundary lines) and ran 3-4 % slower with nt
+  // (C3 1107 -> 1147, C4 815 -> 840; profiles/r06_nt_ab.json)
+  constexpr int kAux = PF ? 2 : 0;
   auto gather_at = [&](int m, int tb, uint32_t eoff, TriPending<NW> &pd) __attribute__((always_inline)) {
     const v4u rec = *reinterpret_cast<const v4u *>(reinterpret_cast<const uint8_t *>(tab(m, tb)) + eoff);
     pd.n = rec.z;
     if (NW == 2) {
-      const v2u a = __builtin_amdgcn_raw_buffer_load_b64(rs[m], rec.x + lane8, 0, 0);
-      const v2u b = __builtin_amdgcn_raw_buffer_load_b64(rq[m], rec.y + lane8, 0, 0);
+      const v2u a = __builtin_amdgcn_raw_buffer_load_b64(rs[m], rec.x + lane8, 0, kAux);
+      const v2u b = __builtin_amdgcn_raw_buffer_load_b64(rq[m], rec.y + lane8, 0, kAux);
       pd.s[0] = a.x; pd.s[1] = a.y; pd.q[0] = b.x; pd.q[1] = b.y;
     } else {
-      const v4u a = __builtin_amdgcn_raw_buffer_load_b128(rs[m], rec.x + lane8, 0, 0);
-      const v4u b = __builtin_amdgcn_raw_buffer_load_b128(rq[m], rec.y + lane8, 0, 0);
+      const v4u a = __builtin_amdgcn_raw_buffer_load_b128(rs[m], rec.x + lane8, 0, kAux);
+      const v4u b = __builtin_amdgcn_raw_buffer_load_b128(rq[m], rec.y + lane8, 0, kAux);
 #pragma unroll
       for (int w = 0; w < NW; ++w) {
         pd.s[w] = a[w & 3];
